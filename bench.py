@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Throughput bench of the MI355X encode hot path (BASELINE.json metric):
+
+    Mpix/s encode (DCT + PatchNorm + LFQ), patch14, 512x512, 1/2/4/8 GPU
+
+One step = one fused encode (dctae_encode) of a batch of B synthetic 512x512
+RGB images already resident in HBM: IPT colour -> global DCT (kept 448x448
+corner) -> 14x14 spectral tokens -> importance order -> packed DCTPatches
+rows (S = 3072) -> PatchNorm (reference-fitted tables) -> LFQ 14 x 2^14 codes.
+Multi-GPU: one process per GPU (torchrun), each rank encodes its own shard
+(weak scaling, no collective on the data path); time = max over ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_MFMA_PEAK_TF = 157.3    # dense fp32 MFMA (= vector) peak
+
+
+def encode_bytes_per_image(h, w, t, ncb, s, images_per_row):
+    """SURVEY §8(d) algorithmic bytes per image: fp32 RGB read + int64 codes,
+    positions (2), channel, image id per token + key_pad_mask share."""
+    return 12 * h * w + t * (8 * ncb + 32) + s / images_per_row
+
+
+def kernel_models(h, w, p, maxp, ncb, s, images_per_row):
+    """Algorithmic work per image of each kernel."""
+    qh, qw = min(h // p, maxp), min(w // p, maxp)
+    kh, kw = p * qh, p * qw
+    t = 3 * qh * qw
+    return {
+        # name: (bound, per-image amount, unit)
+        "rgb_to_ipt": ("hbm", 12 * h * w + 12 * h * w, "B"),
+        "gemm_rows": ("mfma", 3 * 2.0 * kw * h * w, "flop"),
+        "gemm_cols": ("mfma", 3 * 2.0 * kh * kw * h, "flop"),
+        "fft_rows": ("hbm", 12 * h * w, "B"),
+        "fft_cols_epilogue": ("hbm", t * 4 * (2 + ncb // 2), "B"),
+        "tile_epilogue": ("hbm", 12 * kh * kw, "B"),
+        "sort_pack": ("hbm", t * (8 * ncb + 32), "B"),
+        "pad_fill": ("hbm", s / images_per_row, "B"),
+        "encode_fused": ("hbm", encode_bytes_per_image(h, w, t, ncb, s, images_per_row), "B"),
+    }
+
+
+def cpu_baseline(size, seconds, pn_tables, threads):
+    from oracle import ref_cpu
+    torch.set_num_threads(threads)
+    cfg = ref_cpu.FEConfig()
+    lcfg = ref_cpu.LFQConfig()
+    g = torch.Generator().manual_seed(0)
+    n, t0 = 0, time.perf_counter()
+    chunk = 8
+    while True:
+        imgs = [torch.rand(3, size, size, generator=g) for _ in range(chunk)]
+        ref_cpu.encode(imgs, cfg, pn_tables, lcfg, batch_size=None, build_attn_mask=True)
+        n += chunk
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    mpix = n * size * size / 1e6
+    return {"value": round(mpix / el, 3), "unit": "Mpix/s", "cores": threads, "kind": "port",
+            "sample": f"{n} images of {size}x{size} (torch.rand) through oracle/ref_cpu.encode: preprocess "
+                      f"(FFT DCT, sort) + iter_batches (attn_mask built) + PatchNorm + LFQ, {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="images per GPU per step")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import _pkgload
+    pkg = _pkgload.load()
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+
+    P, MAXP, S = 14, 32, 3072
+    fe = pkg.DCTAutoencoderFeatureExtractor(3, P, 0.0, MAXP, MAXP, S)
+    tabs = np.load(os.path.join(ROOT, "tests", "golden", "patchnorm_ref.npz"))
+    pn = pkg.PatchNorm(MAXP, MAXP, P, 3).to(dev)
+    pn.median.data.copy_(torch.from_numpy(tabs["median"]))
+    pn.b.data.copy_(torch.from_numpy(tabs["b"]))
+    pn.n.data.copy_(torch.from_numpy(tabs["n"]))
+    pn.frozen = True
+    pn.eval()
+    lfq = pkg.LFQ(dim=196, codebook_size=2 ** 14, num_codebooks=14).to(dev).eval()
+
+    B, H = args.batch, args.size
+    x = ops.synth_images(B, H, H, seed=1234, first_index=rank * B, device=dev)
+    enc = fe_mod.BatchEncoder(fe, B, H, H, pn, lfq, device=dev)
+    ctx = enc.ctx
+    for _ in range(args.warmup):
+        enc(x)
+    torch.cuda.synchronize(dev)
+
+    timing = not args.no_kernel_timing
+    if timing:
+        ctx.lib.dctae_timing_reset(ctx.h)
+        ctx.lib.dctae_set_timing(ctx.h, 1)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        enc(x)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if timing:
+        ctx.lib.dctae_set_timing(ctx.h, 0)
+        ctx.lib.dctae_timing_collect(ctx.h)
+    el_t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+
+    imgs_per_row = max(1, S // enc.k)
+    pix = args.steps * B * H * H * world
+    mpix_s = pix / el / 1e6
+    ms_step = el / args.steps * 1e3
+    t_tok = enc.k
+    per_img_bytes = encode_bytes_per_image(H, H, t_tok, 14, S, imgs_per_row)
+    hbm_frac = (per_img_bytes * B * world * args.steps / el) / (HBM_PEAK_GBS * 1e9 * world)
+
+    kernels, roof = {}, None
+    if timing:
+        import ctypes as C
+        models = kernel_models(H, H, P, MAXP, 14, S, imgs_per_row)
+        i = 0
+        while True:
+            name = C.c_char_p()
+            ms = C.c_double()
+            n = C.c_int64()
+            if ctx.lib.dctae_timing_get(ctx.h, i, C.byref(name), C.byref(ms), C.byref(n)) != 0:
+                break
+            kernels[name.value.decode()] = {"total_ms": round(ms.value, 4), "launches": int(n.value),
+                                            "avg_ms": round(ms.value / max(1, n.value), 5)}
+            i += 1
+        if kernels:
+            dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+            bound, amt, unit = models.get(dom, ("hbm", 0, "B"))
+            imgs_per_launch = B * args.steps / kernels[dom]["launches"]
+            per_launch = amt * imgs_per_launch
+            avg_s = kernels[dom]["avg_ms"] / 1e3
+            if bound == "mfma":
+                ach = per_launch / avg_s / 1e12
+                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF,
+                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                        "per_launch": f"{per_launch:.4g} flop ({imgs_per_launch:g} images)"}
+            else:
+                ach = per_launch / avg_s / 1e9
+                roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "per_launch": f"{per_launch:.4g} B ({imgs_per_launch:g} images)"}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import ref_cpu
+        threads = min(16, os.cpu_count() or 1)
+        tables = ref_cpu.NormTables(torch.from_numpy(tabs["n"]), torch.from_numpy(tabs["median"]),
+                                    torch.from_numpy(tabs["b"]))
+        cpu = cpu_baseline(H, args.cpu_seconds, tables, threads)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpix/s encode (DCT+PatchNorm+LFQ), patch14 512²; 1/2/4/8 GPU, %HBM roofline",
+            "value": round(mpix_s, 2),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (counter-RNG uniform [0,1) RGB generated on device; reference-fitted PatchNorm tables)",
+            "config": {"workload": f"fused encode of {H}x{H} RGB images, patch14, max_patch 32x32, S={S}, "
+                                   f"LFQ 14 codebooks x 2^14, beta=0",
+                       "images_per_gpu_per_step": B, "global_batch": B * world, "image_hw": [H, H],
+                       "tokens_per_image": t_tok, "parallelism": f"dp{world} (image shards, no collective)"},
+            "hbm_roofline_frac_encode": round(hbm_frac, 5),
+            "encode_bytes_per_image": per_img_bytes,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

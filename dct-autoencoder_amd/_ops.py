@@ -1,0 +1,250 @@
+"""Thin torch-tensor wrappers around the C ABI (include/dctae.h).
+
+Every function enqueues work on torch's current stream of the tensors'
+device and returns device tensors; nothing here computes on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import FECfg, Images, LFQCfg, Norm, PackedOut, Packing, i32, i64, ptr
+
+
+@dataclass(frozen=True)
+class FEParams:
+    channels: int = 3
+    patch_size: int = 14
+    max_patch_h: int = 32
+    max_patch_w: int = 32
+    max_seq_len: int = 3072
+    channel_importances: Tuple[float, float, float] = (8.0, 1.0, 1.0)
+    magnitude_weight: float = 0.1
+
+    def c(self, max_seq_len: Optional[int] = None) -> FECfg:
+        ci = tuple(float(x) for x in self.channel_importances)
+        if len(ci) != 3:
+            raise AssertionError("channel_importances must have 3 entries")
+        return FECfg(self.channels, self.patch_size, self.max_patch_h, self.max_patch_w,
+                     int(max_seq_len if max_seq_len is not None else self.max_seq_len),
+                     (C.c_float * 3)(*ci), float(self.magnitude_weight))
+
+
+@dataclass
+class NormState:
+    median: torch.Tensor   # (C, mh, mw, P*P) fp32 on device, contiguous
+    b: torch.Tensor
+    eps: float = 1e-6
+    min_val: float = -6.0
+    max_val: float = 6.0
+
+    def c(self) -> Norm:
+        return Norm(C.c_void_p(self.median.data_ptr()), C.c_void_p(self.b.data_ptr()), float(self.eps),
+                    float(self.min_val), float(self.max_val))
+
+
+def _check_dev(*ts):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise _lib.DCTAEUnavailable("the MI355X path needs HIP device tensors (got a CPU tensor)")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise AssertionError("tensors on different devices")
+    return dev
+
+
+def image_set(images: Sequence[torch.Tensor]) -> Tuple[Images, torch.device, list]:
+    """Describe a list of (3,H,W) fp32 contiguous device images by a base
+    pointer and element offsets (no copies)."""
+    imgs = [im if (im.dtype == torch.float32 and im.is_contiguous()) else im.float().contiguous()
+            for im in images]
+    dev = _check_dev(*imgs)
+    for im in imgs:
+        if im.dim() != 3:
+            raise AssertionError(f"expected a (c, h, w) image, got {tuple(im.shape)}")
+    ptrs = [im.data_ptr() for im in imgs]
+    base = min(ptrs) if ptrs else 0
+    offs = [(p - base) // 4 for p in ptrs]
+    hw = []
+    for im in imgs:
+        hw += [im.shape[1], im.shape[2]]
+    keep = [imgs, i64(offs), i32(hw)]
+    desc = Images(C.c_void_p(base), C.cast(keep[1], C.POINTER(C.c_int64)), C.cast(keep[2], C.POINTER(C.c_int32)),
+                  len(imgs))
+    return desc, dev, keep
+
+
+def batch_image_set(x: torch.Tensor) -> Tuple[Images, torch.device, list]:
+    """(B,3,H,W) fp32 contiguous device tensor."""
+    if x.dim() != 4:
+        raise AssertionError("expected (B, c, h, w)")
+    x = x if (x.dtype == torch.float32 and x.is_contiguous()) else x.float().contiguous()
+    dev = _check_dev(x)
+    B, c, H, W = x.shape
+    per = c * H * W
+    keep = [x, i64([i * per for i in range(B)]), i32([H, W] * B)]
+    desc = Images(C.c_void_p(x.data_ptr()), C.cast(keep[1], C.POINTER(C.c_int64)),
+                  C.cast(keep[2], C.POINTER(C.c_int32)), B)
+    return desc, dev, keep
+
+
+def encode(imgs_desc: Images, dev: torch.device, p: FEParams, plan, n_rows: int, seq_len: int,
+           norm: Optional[NormState], lfq: Optional[LFQCfg], want_codes=True, want_patches=False,
+           want_raw=False, want_scores=False, out=None):
+    """dctae_encode: returns dict of packed device tensors."""
+    ctx = _lib.context(dev)
+    S = seq_len
+    PP = p.patch_size ** 2
+    o = out or {}
+    def alloc(name, shape, dtype):
+        t = o.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device != dev:
+            t = torch.empty(shape, dtype=dtype, device=dev)
+            o[name] = t
+        return t
+    res = {
+        "positions": alloc("positions", (n_rows, S, 2), torch.long),
+        "channels": alloc("channels", (n_rows, S), torch.long),
+        "image_ids": alloc("image_ids", (n_rows, S), torch.long),
+        "key_pad_mask": alloc("key_pad_mask", (n_rows, S), torch.bool),
+    }
+    if want_codes:
+        res["codes"] = alloc("codes", (n_rows, S, lfq.num_codebooks), torch.long)
+    if want_patches:
+        res["patches"] = alloc("patches", (n_rows, S, PP), torch.float32)
+    if want_raw:
+        res["raw"] = alloc("raw", (n_rows, S, PP), torch.float32)
+    if want_scores:
+        res["scores"] = alloc("scores", (n_rows, S), torch.float32)
+    pk_keep = [i32(plan.row), i32(plan.col), i32(plan.k), i32(plan.local_id), i32(plan.row_len)]
+    pk = Packing(*[C.cast(a, C.POINTER(C.c_int32)) for a in pk_keep], n_rows)
+    po = PackedOut(ptr(res.get("codes")), ptr(res["positions"]), ptr(res["channels"]), ptr(res["image_ids"]),
+                   ptr(res["key_pad_mask"]), ptr(res.get("patches")), ptr(res.get("raw")), ptr(res.get("scores")))
+    nc = norm.c() if norm is not None else None
+    rc = ctx.lib.dctae_encode(ctx.h, C.byref(p.c(S)), C.byref(imgs_desc), C.byref(pk),
+                              C.byref(nc) if nc is not None else None,
+                              C.byref(lfq) if lfq is not None else None, C.byref(po), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_encode")
+    return res
+
+
+def norm_apply(x: torch.Tensor, channels: torch.Tensor, positions: torch.Tensor, norm: NormState, p: FEParams,
+               inverse: bool) -> torch.Tensor:
+    dev = _check_dev(x, channels, positions, norm.median, norm.b)
+    ctx = _lib.context(dev)
+    PP = p.patch_size ** 2
+    if x.shape[-1] != PP:
+        raise AssertionError(f"token dim {x.shape[-1]} != patch_size**2")
+    xs = x.float().contiguous()
+    ch = channels.long().contiguous()
+    pos = positions.long().contiguous()
+    n = xs.numel() // PP
+    if ch.numel() != n or pos.numel() != 2 * n:
+        raise AssertionError("channels/positions do not match patches")
+    y = torch.empty_like(xs)
+    fn = ctx.lib.dctae_norm_inverse if inverse else ctx.lib.dctae_norm_forward
+    rc = fn(ctx.h, C.byref(norm.c()), p.patch_size, p.max_patch_h, p.max_patch_w, ptr(xs), ptr(ch), ptr(pos), n,
+            ptr(y), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_norm")
+    return y
+
+
+def check_device_errors(dev):
+    ctx = _lib.context(dev)
+    ctx.check(ctx.lib.dctae_check_device_errors(ctx.h, _lib.stream_ptr(dev)), "device index check")
+
+
+def lfq_forward(x: torch.Tensor, cfg: LFQCfg, want_quantized=True):
+    dev = _check_dev(x)
+    ctx = _lib.context(dev)
+    xs = x.float().contiguous()
+    d = cfg.codebook_dim * cfg.num_codebooks
+    if xs.shape[-1] != d:
+        raise AssertionError(f"expected dimension of {d} but received {xs.shape[-1]}")
+    n = xs.numel() // d
+    q = torch.empty_like(xs) if want_quantized else None
+    idx = torch.empty((*xs.shape[:-1], cfg.num_codebooks), dtype=torch.long, device=dev)
+    rc = ctx.lib.dctae_lfq_forward(ctx.h, C.byref(cfg), ptr(xs), n, ptr(q), ptr(idx), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_lfq_forward")
+    return q, idx
+
+
+def lfq_codes(idx: torch.Tensor, cfg: LFQCfg) -> torch.Tensor:
+    dev = _check_dev(idx)
+    ctx = _lib.context(dev)
+    ii = idx.long().contiguous()
+    if ii.shape[-1] != cfg.num_codebooks:
+        raise AssertionError("last dim of indices must be num_codebooks")
+    n = ii.numel() // cfg.num_codebooks
+    out = torch.empty((*ii.shape[:-1], cfg.num_codebooks * cfg.codebook_dim), dtype=torch.float32, device=dev)
+    rc = ctx.lib.dctae_lfq_indices_to_codes(ctx.h, C.byref(cfg), ptr(ii), n, ptr(out), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_lfq_indices_to_codes")
+    return out
+
+
+def decode(p: FEParams, ids: torch.Tensor, key_pad: torch.Tensor, positions: torch.Tensor, channels: torch.Tensor,
+           patch_sizes: Sequence, original_sizes: Sequence, codes: Optional[torch.Tensor] = None,
+           patches: Optional[torch.Tensor] = None, norm: Optional[NormState] = None,
+           lfq: Optional[LFQCfg] = None) -> List[torch.Tensor]:
+    """dctae_decode; returns a list of (3, H, W) fp32 device images."""
+    dev = _check_dev(ids, key_pad, positions, channels, codes, patches)
+    ctx = _lib.context(dev)
+    R, S = ids.shape
+    ids_c = ids.long().contiguous()
+    kp = key_pad.to(torch.bool).contiguous()
+    pos = positions.long().contiguous()
+    ch = channels.long().contiguous()
+    # image enumeration: rows in order, ids ascending (FE:619-633); host view
+    ids_h = ids_c.cpu()
+    lut_w = int(ids_h.max().item()) + 1 if ids_h.numel() else 1
+    lut = [-1] * (R * lut_w)
+    n_img = 0
+    for r in range(R):
+        for im in torch.unique(ids_h[r]).tolist():
+            lut[r * lut_w + im] = n_img
+            n_img += 1
+    if n_img > len(patch_sizes) or n_img > len(original_sizes):
+        raise IndexError("more images in the batch than patch_sizes / original_sizes entries")
+    hw, phw, offs = [], [], []
+    total = 0
+    for i in range(n_img):
+        h, w = (int(v) for v in original_sizes[i])
+        ph, pw = (int(v) for v in patch_sizes[i])
+        hw += [h, w]
+        phw += [ph, pw]
+        offs.append(total)
+        total += p.channels * h * w
+    out = torch.empty(total, dtype=torch.float32, device=dev)
+    keep = [i32(lut), i32(hw), i64(offs), i32(phw)]
+    cc = codes.long().contiguous() if codes is not None else None
+    pp = patches.float().contiguous() if patches is not None else None
+    nc = norm.c() if norm is not None else None
+    rc = ctx.lib.dctae_decode(ctx.h, C.byref(p.c(S)), R, C.cast(keep[0], C.POINTER(C.c_int32)), lut_w, n_img,
+                              C.cast(keep[1], C.POINTER(C.c_int32)), C.cast(keep[2], C.POINTER(C.c_int64)),
+                              C.cast(keep[3], C.POINTER(C.c_int32)), ptr(ids_c), ptr(kp), ptr(pos), ptr(ch),
+                              C.byref(nc) if nc is not None else None, C.byref(lfq) if lfq is not None else None,
+                              ptr(cc), ptr(pp), ptr(out), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_decode")
+    imgs = []
+    for i in range(n_img):
+        h, w = hw[2 * i], hw[2 * i + 1]
+        imgs.append(out[offs[i]: offs[i] + p.channels * h * w].view(p.channels, h, w))
+    return imgs
+
+
+def synth_images(n: int, h: int, w: int, seed: int, first_index: int = 0, device=None) -> torch.Tensor:
+    """(n, 3, h, w) counter-RNG images generated on the device (oracle/rng.py hash)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ctx = _lib.context(dev)
+    out = torch.empty((n, 3, h, w), dtype=torch.float32, device=dev)
+    rc = ctx.lib.dctae_synth_images(ctx.h, C.c_uint64(seed), first_index, n, h, w, ptr(out), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_synth_images")
+    return out

@@ -1,0 +1,902 @@
+// C ABI of libdctae.so: context, planning, workspace and launch sequencing.
+// See include/dctae.h for the contract of every entry point.
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/dctae.h"
+#include "dctae_internal.h"
+#include "dctae_launch.h"
+
+using namespace dctae;
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+
+struct TimedLaunch {
+  const char* name;
+  hipEvent_t a, b;
+};
+
+struct TimingEntry {
+  std::string name;
+  double ms = 0.0;
+  int64_t launches = 0;
+};
+
+struct dctae_ctx {
+  int device = 0;
+  std::string err;
+  // DCT-II matrices C_N[rows][N] (fp32, from float64), keyed by (N, rows)
+  std::map<std::pair<int, int>, float*> dct;
+  // workspace (floats) and token staging (bytes), grow-only
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  uint8_t* stage = nullptr;
+  size_t stage_bytes = 0;
+  int64_t ws_limit = 8ll << 30;
+  // plan: host (pinned) + device copies, last uploaded plan bytes for caching
+  uint8_t* plan_host = nullptr;
+  uint8_t* plan_dev = nullptr;
+  size_t plan_cap = 0;
+  std::vector<uint8_t> plan_last;
+  hipEvent_t plan_evt = nullptr;
+  hipEvent_t done_evt = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool have_done = false;
+  int* err_dev = nullptr;
+  ColorMats cm{};
+  // timing
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> evt_pool;
+  std::vector<TimingEntry> totals;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(dctae_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return fail(ctx, DCTAE_EHIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+// reference colour constants (util.py:21-43), built exactly like the
+// reference does in fp32: Trgb2lms = MHPE @ MsRGB; Tlms2rgb = inverse; Mipt^-1.
+// The Python layer overrides these with torch-computed bits (ctx->cm) so the
+// matrix inverses carry the reference's exact fp32 values.
+void default_colors(ColorMats& cm) {
+  const double srgb[9] = {0.4124564, 0.3575761, 0.1804375, 0.2126729, 0.7151522, 0.0721750,
+                          0.0193339, 0.1191920, 0.9503041};
+  const double hpe[9] = {0.4002, 0.7076, -0.0807, -0.2280, 1.1500, 0.0612, 0, 0, 0.9184};
+  const double ipt[9] = {0.4, 0.4, 0.2, 4.455, -4.851, 0.3960, 0.8056, 0.3572, -1.1628};
+  double m[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0;
+      for (int k = 0; k < 3; ++k) s += (double)(float)hpe[3 * i + k] * (double)(float)srgb[3 * k + j];
+      m[3 * i + j] = s;
+    }
+  auto inv3 = [](const double* a, double* o) {
+    double det = a[0] * (a[4] * a[8] - a[5] * a[7]) - a[1] * (a[3] * a[8] - a[5] * a[6]) +
+                 a[2] * (a[3] * a[7] - a[4] * a[6]);
+    o[0] = (a[4] * a[8] - a[5] * a[7]) / det;
+    o[1] = (a[2] * a[7] - a[1] * a[8]) / det;
+    o[2] = (a[1] * a[5] - a[2] * a[4]) / det;
+    o[3] = (a[5] * a[6] - a[3] * a[8]) / det;
+    o[4] = (a[0] * a[8] - a[2] * a[6]) / det;
+    o[5] = (a[2] * a[3] - a[0] * a[5]) / det;
+    o[6] = (a[3] * a[7] - a[4] * a[6]) / det;
+    o[7] = (a[1] * a[6] - a[0] * a[7]) / det;
+    o[8] = (a[0] * a[4] - a[1] * a[3]) / det;
+  };
+  double mi[9], ii[9], ipd[9];
+  for (int i = 0; i < 9; ++i) ipd[i] = (float)ipt[i];
+  inv3(m, mi);
+  inv3(ipd, ii);
+  for (int i = 0; i < 9; ++i) {
+    cm.rgb2lms[i] = (float)m[i];
+    cm.lms2rgb[i] = (float)mi[i];
+    cm.lms2ipt[i] = (float)ipt[i];
+    cm.ipt2lms[i] = (float)ii[i];
+  }
+}
+
+struct Timer {
+  dctae_ctx* ctx;
+  hipStream_t s;
+  const char* name;
+  hipEvent_t a = nullptr;
+  Timer(dctae_ctx* c, hipStream_t st, const char* n) : ctx(c), s(st), name(n) {
+    if (ctx->timing) {
+      a = take();
+      hipEventRecord(a, s);
+    }
+  }
+  hipEvent_t take() {
+    if (ctx->evt_pool.empty()) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      return e;
+    }
+    hipEvent_t e = ctx->evt_pool.back();
+    ctx->evt_pool.pop_back();
+    return e;
+  }
+  ~Timer() {
+    if (ctx->timing) {
+      hipEvent_t b = take();
+      hipEventRecord(b, s);
+      ctx->pending.push_back({name, a, b});
+    }
+  }
+};
+
+// ---- plan serialisation ----------------------------------------------------
+struct PlanBuf {
+  std::vector<uint8_t> bytes;
+  template <class T>
+  size_t add(const T* p, size_t n) {
+    size_t off = (bytes.size() + 255) & ~size_t(255);
+    bytes.resize(off + n * sizeof(T));
+    if (n) std::memcpy(bytes.data() + off, p, n * sizeof(T));
+    return off;
+  }
+};
+
+// order this call after the previous one on a possibly different stream
+void order_after_previous(dctae_ctx* ctx, hipStream_t s) {
+  if (ctx->have_done && ctx->last_stream != s) hipStreamWaitEvent(s, ctx->done_evt, 0);
+}
+
+void mark_done(dctae_ctx* ctx, hipStream_t s) {
+  hipEventRecord(ctx->done_evt, s);
+  ctx->last_stream = s;
+  ctx->have_done = true;
+}
+
+int upload_plan(dctae_ctx* ctx, const PlanBuf& pb, hipStream_t s) {
+  const size_t n = pb.bytes.size();
+  if (n == 0) return 0;
+  if (n == ctx->plan_last.size() && std::memcmp(pb.bytes.data(), ctx->plan_last.data(), n) == 0) return 0;
+  if (n > ctx->plan_cap) {
+    HIPCHK(ctx, hipDeviceSynchronize());
+    if (ctx->plan_host) hipHostFree(ctx->plan_host);
+    if (ctx->plan_dev) hipFree(ctx->plan_dev);
+    ctx->plan_host = nullptr;
+    ctx->plan_dev = nullptr;
+    size_t cap = std::max<size_t>(n * 2, 1 << 20);
+    HIPCHK(ctx, hipHostMalloc((void**)&ctx->plan_host, cap, hipHostMallocDefault));
+    HIPCHK(ctx, hipMalloc((void**)&ctx->plan_dev, cap));
+    ctx->plan_cap = cap;
+  } else {
+    HIPCHK(ctx, hipEventSynchronize(ctx->plan_evt));  // previous upload finished reading plan_host
+  }
+  std::memcpy(ctx->plan_host, pb.bytes.data(), n);
+  HIPCHK(ctx, hipMemcpyAsync(ctx->plan_dev, ctx->plan_host, n, hipMemcpyHostToDevice, s));
+  HIPCHK(ctx, hipEventRecord(ctx->plan_evt, s));
+  ctx->plan_last = pb.bytes;
+  return 0;
+}
+
+int ensure_ws(dctae_ctx* ctx, size_t ws_bytes, size_t stage_bytes) {
+  if (ws_bytes > ctx->ws_bytes) {
+    HIPCHK(ctx, hipDeviceSynchronize());
+    if (ctx->ws) hipFree(ctx->ws);
+    ctx->ws = nullptr;
+    ctx->ws_bytes = 0;
+    if (hipMalloc((void**)&ctx->ws, ws_bytes) != hipSuccess)
+      return fail(ctx, DCTAE_ENOMEM, "workspace allocation of " + std::to_string(ws_bytes) + " bytes failed");
+    ctx->ws_bytes = ws_bytes;
+  }
+  if (stage_bytes > ctx->stage_bytes) {
+    HIPCHK(ctx, hipDeviceSynchronize());
+    if (ctx->stage) hipFree(ctx->stage);
+    ctx->stage = nullptr;
+    ctx->stage_bytes = 0;
+    if (hipMalloc((void**)&ctx->stage, stage_bytes) != hipSuccess)
+      return fail(ctx, DCTAE_ENOMEM, "staging allocation of " + std::to_string(stage_bytes) + " bytes failed");
+    ctx->stage_bytes = stage_bytes;
+  }
+  return 0;
+}
+
+// orthonormal DCT-II matrix rows [0, rows) of size N, fp64 -> fp32
+int dct_matrix(dctae_ctx* ctx, int N, int rows, const float** out) {
+  auto key = std::make_pair(N, rows);
+  auto it = ctx->dct.find(key);
+  if (it != ctx->dct.end()) {
+    *out = it->second;
+    return 0;
+  }
+  std::vector<float> h((size_t)rows * N);
+  const double pi = 3.14159265358979323846;
+  for (int k = 0; k < rows; ++k) {
+    double sk = (k == 0) ? std::sqrt(1.0 / N) : std::sqrt(2.0 / N);
+    for (int n = 0; n < N; ++n) {
+      // reduce the angle exactly: cos(pi*(2n+1)k/(2N)) with (2n+1)k mod 4N
+      long long a = ((long long)(2 * n + 1) * k) % (4ll * N);
+      h[(size_t)k * N + n] = (float)(sk * std::cos(pi * (double)a / (2.0 * N)));
+    }
+  }
+  float* d = nullptr;
+  HIPCHK(ctx, hipMalloc((void**)&d, h.size() * sizeof(float)));
+  HIPCHK(ctx, hipMemcpy(d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
+  ctx->dct[key] = d;
+  *out = d;
+  return 0;
+}
+
+int check_cfg(dctae_ctx* ctx, const dctae_fe_cfg* cfg) {
+  if (!cfg) return fail(ctx, DCTAE_EINVAL, "cfg is NULL");
+  if (cfg->channels != 3) return fail(ctx, DCTAE_EUNSUP, "channels must be 3 (IPT colour transform)");
+  if (cfg->patch_size < 1 || cfg->patch_size > kMaxP)
+    return fail(ctx, DCTAE_EUNSUP, "patch_size must be in [1, 16]");
+  if (cfg->max_patch_h < 1 || cfg->max_patch_w < 1 || cfg->max_seq_len < 1)
+    return fail(ctx, DCTAE_EINVAL, "max_patch_h/w and max_seq_len must be >= 1");
+  return 0;
+}
+
+int check_lfq(dctae_ctx* ctx, const dctae_lfq* lfq, int PP) {
+  if (!lfq) return fail(ctx, DCTAE_EINVAL, "lfq is NULL");
+  if (lfq->codebook_dim < 1 || lfq->codebook_dim > 16)
+    return fail(ctx, DCTAE_EUNSUP, "codebook_dim must be in [1, 16] (codebook_size <= 65536)");
+  if (lfq->codebook_dim * lfq->num_codebooks != PP)
+    return fail(ctx, DCTAE_EUNSUP, "LFQ with projections is not fused: codebook_dim*num_codebooks != P*P");
+  return 0;
+}
+
+// build the per-image descriptor (tokens, crop, kept corner); FE:312-345, 364-399
+int describe(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int H, int W, ImgDesc& d) {
+  const int P = cfg->patch_size;
+  if (H < P || W < P)
+    return fail(ctx, DCTAE_EINVAL, "image " + std::to_string(H) + "x" + std::to_string(W) +
+                                       " is smaller than patch_size (FE:313-314)");
+  std::memset(&d, 0, sizeof(d));
+  d.H = H;
+  d.W = W;
+  d.ph = std::max(H / P, 1);
+  d.pw = std::max(W / P, 1);
+  d.qh = std::min(d.ph, cfg->max_patch_h);
+  d.qw = std::min(d.pw, cfg->max_patch_w);
+  d.Kh = P * d.qh;
+  d.Kw = P * d.qw;
+  d.T = cfg->channels * d.qh * d.qw;
+  return 0;
+}
+
+GemmProblem gemm(const float* A, int64_t sAc, int64_t sAm, int64_t sAk, const float* B, int64_t sBc, int64_t sBn,
+                 int64_t sBk, float* O, int64_t sOc, int64_t sOm, int64_t sOn, int M, int N, int K, int C) {
+  GemmProblem g{};
+  g.A = A;
+  g.B = B;
+  g.O = O;
+  g.sAc = sAc, g.sAm = sAm, g.sAk = sAk;
+  g.sBc = sBc, g.sBn = sBn, g.sBk = sBk;
+  g.sOc = sOc, g.sOm = sOm, g.sOn = sOn;
+  g.M = M, g.N = N, g.K = K, g.C = C;
+  g.tiles_n = (N + 63) / 64;
+  return g;
+}
+
+void add_tiles(std::vector<TileRef>& t, int prob, const GemmProblem& g) {
+  int tm = (g.M + 63) / 64;
+  for (int i = 0; i < tm * g.tiles_n; ++i) t.push_back({prob, i});
+}
+
+EncParams enc_params(const dctae_fe_cfg* cfg, const dctae_norm* norm, const dctae_lfq* lfq) {
+  EncParams ep{};
+  ep.P = cfg->patch_size;
+  ep.C = cfg->channels;
+  ep.maxph = cfg->max_patch_h;
+  ep.maxpw = cfg->max_patch_w;
+  ep.S = cfg->max_seq_len;
+  for (int i = 0; i < 3; ++i) ep.ci[i] = cfg->channel_importances[i];
+  ep.mw = cfg->magnitude_weight;
+  if (norm) {
+    ep.median = norm->median_dev;
+    ep.b = norm->b_dev;
+    ep.eps = norm->eps;
+    ep.min_val = norm->min_val;
+    ep.max_val = norm->max_val;
+  }
+  if (lfq) {
+    ep.cb_dim = lfq->codebook_dim;
+    ep.ncb = lfq->num_codebooks;
+    ep.scale = lfq->codebook_scale;
+  }
+  return ep;
+}
+
+int next_pow2(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Shared front half of encode / spectrum_tokens: per chunk of images, run
+// colour + DCT (FFT kernels where planned, GEMM otherwise) + tile epilogue
+// into token staging; `per_chunk` is then called to consume the staging.
+struct ChunkJob {
+  int i0, i1;              // image range
+  size_t desc_off;         // device offset of ImgDesc array (chunk-local copies)
+  size_t gp_off, rows_t_off, cols_t_off;
+  int n_rows_tiles, n_cols_tiles;
+  int max_T;
+  int64_t max_hw;
+  int64_t tok_base;        // first token (global) of the chunk
+  int fft_mask;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+int dctae_abi_version(void) { return DCTAE_ABI_VERSION; }
+
+int dctae_ctx_create(int device, dctae_ctx** out) {
+  if (!out) return DCTAE_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    g_err = "no HIP device";
+    return DCTAE_EHIP;
+  }
+  if (device < 0 || device >= n) {
+    g_err = "bad device index";
+    return DCTAE_EINVAL;
+  }
+  if (hipSetDevice(device) != hipSuccess) {
+    g_err = "hipSetDevice failed";
+    return DCTAE_EHIP;
+  }
+  dctae_ctx* c = new dctae_ctx();
+  c->device = device;
+  default_colors(c->cm);
+  if (hipEventCreateWithFlags(&c->plan_evt, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done_evt, hipEventDisableTiming) != hipSuccess ||
+      hipMalloc((void**)&c->err_dev, sizeof(int)) != hipSuccess || hipMemset(c->err_dev, 0, sizeof(int)) != hipSuccess) {
+    g_err = "context allocation failed";
+    delete c;
+    return DCTAE_EHIP;
+  }
+  hipEventRecord(c->plan_evt, 0);
+  *out = c;
+  return 0;
+}
+
+int dctae_ctx_destroy(dctae_ctx* ctx) {
+  if (!ctx) return 0;
+  hipSetDevice(ctx->device);
+  hipDeviceSynchronize();
+  for (auto& kv : ctx->dct) hipFree(kv.second);
+  if (ctx->ws) hipFree(ctx->ws);
+  if (ctx->stage) hipFree(ctx->stage);
+  if (ctx->plan_host) hipHostFree(ctx->plan_host);
+  if (ctx->plan_dev) hipFree(ctx->plan_dev);
+  if (ctx->err_dev) hipFree(ctx->err_dev);
+  for (auto& p : ctx->pending) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : ctx->evt_pool) hipEventDestroy(e);
+  hipEventDestroy(ctx->plan_evt);
+  hipEventDestroy(ctx->done_evt);
+  delete ctx;
+  return 0;
+}
+
+const char* dctae_last_error(dctae_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+// Python passes the reference's exact fp32 colour matrices (util.py:40-41, 91)
+int dctae_set_color_matrices(dctae_ctx* ctx, const float* rgb2lms, const float* lms2ipt, const float* ipt2lms,
+                             const float* lms2rgb) {
+  if (!ctx) return DCTAE_EINVAL;
+  std::memcpy(ctx->cm.rgb2lms, rgb2lms, 36);
+  std::memcpy(ctx->cm.lms2ipt, lms2ipt, 36);
+  std::memcpy(ctx->cm.ipt2lms, ipt2lms, 36);
+  std::memcpy(ctx->cm.lms2rgb, lms2rgb, 36);
+  return 0;
+}
+
+int dctae_set_workspace_limit(dctae_ctx* ctx, int64_t bytes) {
+  if (!ctx || bytes < (1 << 20)) return DCTAE_EINVAL;
+  ctx->ws_limit = bytes;
+  return 0;
+}
+
+int dctae_set_timing(dctae_ctx* ctx, int enable) {
+  if (!ctx) return DCTAE_EINVAL;
+  ctx->timing = enable != 0;
+  return 0;
+}
+
+int dctae_timing_collect(dctae_ctx* ctx) {
+  if (!ctx) return DCTAE_EINVAL;
+  for (auto& p : ctx->pending) {
+    float ms = 0;
+    HIPCHK(ctx, hipEventSynchronize(p.b));
+    HIPCHK(ctx, hipEventElapsedTime(&ms, p.a, p.b));
+    TimingEntry* e = nullptr;
+    for (auto& t : ctx->totals)
+      if (t.name == p.name) e = &t;
+    if (!e) {
+      ctx->totals.push_back({p.name, 0.0, 0});
+      e = &ctx->totals.back();
+    }
+    e->ms += ms;
+    e->launches += 1;
+    ctx->evt_pool.push_back(p.a);
+    ctx->evt_pool.push_back(p.b);
+  }
+  ctx->pending.clear();
+  return 0;
+}
+
+int dctae_timing_get(dctae_ctx* ctx, int idx, const char** name, double* total_ms, int64_t* launches) {
+  if (!ctx || idx < 0 || idx >= (int)ctx->totals.size()) return DCTAE_EINVAL;
+  if (name) *name = ctx->totals[idx].name.c_str();
+  if (total_ms) *total_ms = ctx->totals[idx].ms;
+  if (launches) *launches = ctx->totals[idx].launches;
+  return 0;
+}
+
+int dctae_timing_reset(dctae_ctx* ctx) {
+  if (!ctx) return DCTAE_EINVAL;
+  dctae_timing_collect(ctx);
+  ctx->totals.clear();
+  return 0;
+}
+
+int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int h = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&h, ctx->err_dev, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipStreamSynchronize(s));
+  HIPCHK(ctx, hipMemsetAsync(ctx->err_dev, 0, sizeof(int), s));
+  if (h & 1) return fail(ctx, DCTAE_EINVAL, "channel/position index out of range of the PatchNorm tables");
+  if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
+  if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
+  return 0;
+}
+
+int dctae_synth_images(dctae_ctx* ctx, uint64_t seed, int64_t first_index, int32_t n_img, int32_t H, int32_t W,
+                       float* rgb_dev, void* stream) {
+  if (!ctx || !rgb_dev || n_img < 0 || H < 1 || W < 1) return fail(ctx, DCTAE_EINVAL, "bad synth args");
+  if (n_img == 0) return 0;
+  Timer t(ctx, (hipStream_t)stream, "synth");
+  launch_synth(seed, first_index, n_img, H, W, rgb_dev, (hipStream_t)stream);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+// The encode engine.  mode 0: full encode (packed outputs); mode 1: spectrum
+// tokens in flat order (tokens_dev / scores_dev, tok_off given).
+static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                       const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
+                       const dctae_packed_out* out, const int64_t* tok_off_user, float* tokens_dev,
+                       float* scores_dev, hipStream_t s) {
+  int rc = check_cfg(ctx, cfg);
+  if (rc) return rc;
+  if (!imgs || imgs->n_img < 0 || (imgs->n_img > 0 && (!imgs->rgb_dev || !imgs->img_off || !imgs->hw)))
+    return fail(ctx, DCTAE_EINVAL, "bad image descriptor");
+  const bool full = (pack != nullptr);
+  const int n = imgs->n_img;
+  const int P = cfg->patch_size, PP = P * P, C = cfg->channels, S = cfg->max_seq_len;
+  const bool want_codes = full && out && out->codes_dev;
+  if (full) {
+    if (!out || !out->positions_dev || !out->channels_dev || !out->image_ids_dev || !out->key_pad_dev)
+      return fail(ctx, DCTAE_EINVAL, "packed outputs positions/channels/image_ids/key_pad are required");
+    if ((want_codes || out->patches_dev) && !norm) return fail(ctx, DCTAE_EINVAL, "codes/patches need PatchNorm tables");
+    if (want_codes) {
+      rc = check_lfq(ctx, lfq, PP);
+      if (rc) return rc;
+    }
+    if (pack->n_rows < 0 || (n > 0 && (!pack->row || !pack->col || !pack->k || !pack->local_id)) ||
+        (pack->n_rows > 0 && !pack->row_len))
+      return fail(ctx, DCTAE_EINVAL, "bad packing descriptor");
+  }
+  if (norm && (!norm->median_dev || !norm->b_dev)) return fail(ctx, DCTAE_EINVAL, "PatchNorm tables are NULL");
+  const int ncb = want_codes ? lfq->num_codebooks : 0;
+
+  // ---- per-image descriptors and checks
+  std::vector<ImgDesc> D(n);
+  int maxT = 1;
+  for (int i = 0; i < n; ++i) {
+    rc = describe(ctx, cfg, imgs->hw[2 * i], imgs->hw[2 * i + 1], D[i]);
+    if (rc) return rc;
+    D[i].rgb_off = imgs->img_off[i];
+    maxT = std::max(maxT, D[i].T);
+    if (full) {
+      D[i].row = pack->row[i];
+      D[i].col = pack->col[i];
+      D[i].k = pack->k[i];
+      D[i].local_id = pack->local_id[i];
+      if (D[i].k < 1 || D[i].k > D[i].T || D[i].k > S)
+        return fail(ctx, DCTAE_EINVAL, "image " + std::to_string(i) + ": k out of range (FE:429-435)");
+      if (D[i].row < 0 || D[i].row >= pack->n_rows || D[i].col < 0 || D[i].col + D[i].k > S)
+        return fail(ctx, DCTAE_EINVAL, "image " + std::to_string(i) + ": packed span outside (rows, S)");
+    }
+  }
+  if (full)
+    for (int r = 0; r < pack->n_rows; ++r)
+      if (pack->row_len[r] < 0 || pack->row_len[r] > S) return fail(ctx, DCTAE_EINVAL, "row_len out of range");
+  const int np2 = next_pow2(maxT);
+  if ((size_t)np2 * 8 > 64 * 1024) return fail(ctx, DCTAE_EUNSUP, "more than 8192 tokens per image");
+
+  // ---- chunking by workspace size
+  const bool want_raw = (full && out->raw_patches_dev) || (!full && tokens_dev);
+  const bool want_norm = full && out->patches_dev;
+  std::vector<ChunkJob> jobs;
+  {
+    int i = 0;
+    while (i < n) {
+      ChunkJob j{};
+      j.i0 = i;
+      int64_t wsf = 0, stb = 0;
+      while (i < n) {
+        const ImgDesc& d = D[i];
+        int64_t w = 3ll * d.H * d.W + 3ll * d.Kw * d.H + 3ll * d.Kh * d.Kw;
+        int64_t st = (int64_t)d.T * (4 + 2 * ncb + (want_raw ? 4 * PP : 0) + (want_norm ? 4 * PP : 0));
+        if (i > j.i0 && (wsf + w) * 4 + stb + st > ctx->ws_limit) break;
+        wsf += w;
+        stb += st;
+        ++i;
+      }
+      j.i1 = i;
+      jobs.push_back(j);
+    }
+  }
+  // ---- workspace sizes (max over chunks), chunk-local offsets
+  size_t ws_need = 0, st_need = 0;
+  int64_t tok_global = 0;
+  for (auto& j : jobs) {
+    int64_t wsf = 0, tok = 0;
+    j.max_T = 1;
+    j.max_hw = 1;
+    j.tok_base = tok_global;
+    for (int i = j.i0; i < j.i1; ++i) {
+      ImgDesc& d = D[i];
+      d.ws_p = wsf;
+      wsf += 3ll * d.H * d.W;
+      d.ws_t = wsf;
+      wsf += 3ll * d.Kw * d.H;
+      d.ws_y = wsf;
+      wsf += 3ll * d.Kh * d.Kw;
+      d.tok_off = full ? tok : (tok_off_user[i] - 0);
+      tok += d.T;
+      j.max_T = std::max(j.max_T, d.T);
+      j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
+    }
+    tok_global += tok;
+    ws_need = std::max<size_t>(ws_need, (size_t)wsf * 4);
+    st_need = std::max<size_t>(st_need, (size_t)tok * (4 + 2 * ncb + (want_raw && full ? 4 * PP : 0) +
+                                                         (want_norm ? 4 * PP : 0)) + 1024);
+  }
+  rc = ensure_ws(ctx, std::max<size_t>(ws_need, 256), std::max<size_t>(st_need, 256));
+  if (rc) return rc;
+
+  // ---- DCT matrices and GEMM problems
+  const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
+  PlanBuf pb;
+  std::vector<GemmProblem> probs;
+  std::vector<TileRef> rows_t, cols_t;
+  std::vector<size_t> desc_offs;
+  for (auto& j : jobs) {
+    j.desc_off = pb.add(D.data() + j.i0, j.i1 - j.i0);
+    const size_t p0 = probs.size();
+    std::vector<TileRef> rt, ct;
+    for (int i = j.i0; i < j.i1; ++i) {
+      const ImgDesc& d = D[i];
+      const float *CW, *CH;
+      if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW))) return rc;
+      if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH))) return rc;
+      float* ws = ctx->ws;
+      // rows: Tt[c][kx][y] = sum_x CW[kx][x] * P[c][y][x]
+      GemmProblem gr = gemm(CW, 0, d.W, 1, ws + d.ws_p, (int64_t)d.H * d.W, d.W, 1, ws + d.ws_t,
+                            (int64_t)d.Kw * d.H, d.H, 1, d.Kw, d.H, d.W, 3);
+      // cols: Y[c][ky][kx] = sum_y CH[ky][y] * Tt[c][kx][y]
+      GemmProblem gc = gemm(CH, 0, d.H, 1, ws + d.ws_t, (int64_t)d.Kw * d.H, d.H, 1, ws + d.ws_y,
+                            (int64_t)d.Kh * d.Kw, d.Kw, 1, d.Kh, d.Kw, d.H, 3);
+      int pr = (int)(probs.size() - p0);
+      probs.push_back(gr);
+      probs.push_back(gc);
+      add_tiles(rt, pr, gr);
+      add_tiles(ct, pr + 1, gc);
+    }
+    j.gp_off = pb.add(probs.data() + p0, probs.size() - p0);
+    j.rows_t_off = pb.add(rt.data(), rt.size());
+    j.cols_t_off = pb.add(ct.data(), ct.size());
+    j.n_rows_tiles = (int)rt.size();
+    j.n_cols_tiles = (int)ct.size();
+  }
+  size_t rowlen_off = 0;
+  if (full && pack->n_rows > 0) rowlen_off = pb.add(pack->row_len, pack->n_rows);
+  order_after_previous(ctx, s);
+  rc = upload_plan(ctx, pb, s);
+  if (rc) return rc;
+  uint8_t* pd = ctx->plan_dev;
+
+  const EncParams ep = enc_params(cfg, norm, want_codes ? lfq : nullptr);
+  PackSinks ps{};
+  if (full) {
+    ps.codes = out->codes_dev;
+    ps.pos = out->positions_dev;
+    ps.ch = out->channels_dev;
+    ps.ids = out->image_ids_dev;
+    ps.patches = out->patches_dev;
+    ps.raw = out->raw_patches_dev;
+    ps.scores = out->scores_dev;
+    if (pack->n_rows > 0) {
+      Timer t(ctx, s, "pad_fill");
+      launch_pad_fill((const int32_t*)(pd + rowlen_off), pack->n_rows, ep, out->key_pad_dev, ps, s);
+    }
+  }
+
+  for (auto& j : jobs) {
+    const int nj = j.i1 - j.i0;
+    const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
+    {
+      Timer t(ctx, s, "rgb_to_ipt");
+      launch_rgb_to_ipt(dd, nj, j.max_hw, imgs->rgb_dev, ctx->ws, ctx->cm, s);
+    }
+    {
+      Timer t(ctx, s, "gemm_rows");
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, s);
+    }
+    {
+      Timer t(ctx, s, "gemm_cols");
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, s);
+    }
+    TokenSinks sk{};
+    if (full) {
+      int64_t ntok = 0;
+      for (int i = j.i0; i < j.i1; ++i) ntok += D[i].T;
+      uint8_t* st = ctx->stage;
+      sk.scores = (float*)st;
+      st += ((ntok * 4 + 255) & ~255ll);
+      if (ncb) {
+        sk.codes = (uint16_t*)st;
+        st += ((ntok * 2 * ncb + 255) & ~255ll);
+      }
+      if (want_norm) {
+        sk.norm = (float*)st;
+        st += ntok * 4 * PP;
+      }
+      if (out->raw_patches_dev) {
+        sk.raw = (float*)st;
+        st += ntok * 4 * PP;
+      }
+    } else {
+      sk.scores = scores_dev;
+      sk.raw = tokens_dev;
+    }
+    EncParams epj = ep;
+    if (!full) epj.median = nullptr;
+    {
+      Timer t(ctx, s, "tile_epilogue");
+      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, s);
+    }
+    if (full) {
+      Timer t(ctx, s, "sort_pack");
+      launch_sort_pack(dd, nj, next_pow2(j.max_T), ep, sk, ps, s);
+    }
+  }
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
+  return 0;
+}
+
+int dctae_encode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs, const dctae_packing* pack,
+                 const dctae_norm* norm, const dctae_lfq* lfq, const dctae_packed_out* out, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!pack) return fail(ctx, DCTAE_EINVAL, "packing descriptor is NULL");
+  hipSetDevice(ctx->device);
+  return encode_impl(ctx, cfg, imgs, pack, norm, lfq, out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int dctae_spectrum_tokens(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs, const int64_t* tok_off,
+                          float* tokens_dev, float* scores_dev, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!tok_off || !scores_dev) return fail(ctx, DCTAE_EINVAL, "tok_off and scores_dev are required");
+  hipSetDevice(ctx->device);
+  return encode_impl(ctx, cfg, imgs, nullptr, nullptr, nullptr, nullptr, tok_off, tokens_dev, scores_dev,
+                     (hipStream_t)stream);
+}
+
+static int norm_impl(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t mh, int32_t mw, const float* x,
+                     const int64_t* ch, const int64_t* pos, int64_t n, float* y, int inverse, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!norm || !norm->median_dev || !norm->b_dev) return fail(ctx, DCTAE_EINVAL, "PatchNorm tables are NULL");
+  if (P < 1 || mh < 1 || mw < 1 || n < 0) return fail(ctx, DCTAE_EINVAL, "bad PatchNorm shape");
+  if (n == 0) return 0;
+  if (!x || !ch || !pos || !y) return fail(ctx, DCTAE_EINVAL, "NULL tensor");
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, inverse ? "norm_inverse" : "norm_forward");
+  launch_norm(x, ch, pos, n, P * P, mh, mw, norm->median_dev, norm->b_dev, norm->eps, norm->min_val, norm->max_val,
+              inverse, y, ctx->err_dev, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_norm_forward(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t mh, int32_t mw, const float* x,
+                       const int64_t* ch, const int64_t* pos, int64_t n, float* y, void* stream) {
+  return norm_impl(ctx, norm, P, mh, mw, x, ch, pos, n, y, 0, stream);
+}
+
+int dctae_norm_inverse(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t mh, int32_t mw, const float* y,
+                       const int64_t* ch, const int64_t* pos, int64_t n, float* x, void* stream) {
+  return norm_impl(ctx, norm, P, mh, mw, y, ch, pos, n, x, 1, stream);
+}
+
+int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, float* q, int64_t* idx,
+                      void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!lfq || lfq->codebook_dim < 1 || lfq->codebook_dim > 62 || lfq->num_codebooks < 1)
+    return fail(ctx, DCTAE_EINVAL, "bad LFQ config");
+  if (n < 0 || (n > 0 && (!x || !idx))) return fail(ctx, DCTAE_EINVAL, "bad LFQ tensors");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "lfq_forward");
+  launch_lfq_forward(x, n, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, q, idx, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* idx, int64_t n, float* codes,
+                               void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!lfq || lfq->codebook_dim < 1 || lfq->codebook_dim > 31 || lfq->num_codebooks < 1)
+    return fail(ctx, DCTAE_EINVAL, "bad LFQ config (codebook_dim <= 31: lfq.py:117 casts to int32)");
+  if (n < 0 || (n > 0 && (!idx || !codes))) return fail(ctx, DCTAE_EINVAL, "bad LFQ tensors");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "lfq_codes");
+  launch_lfq_codes(idx, n, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, codes, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut, int32_t lut_w,
+                 int32_t n_img, const int32_t* out_hw, const int64_t* out_off, const int32_t* patch_hw,
+                 const int64_t* ids, const uint8_t* key_pad, const int64_t* pos, const int64_t* ch,
+                 const dctae_norm* norm, const dctae_lfq* lfq, const int64_t* codes, const float* patches,
+                 float* rgb, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipSetDevice(ctx->device);
+  int rc = check_cfg(ctx, cfg);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int P = cfg->patch_size, PP = P * P, S = cfg->max_seq_len;
+  if (n_rows < 0 || n_img < 0 || lut_w < 1 || !img_lut || (n_img > 0 && (!out_hw || !out_off || !patch_hw || !rgb)))
+    return fail(ctx, DCTAE_EINVAL, "bad decode descriptor");
+  if (n_rows > 0 && (!ids || !key_pad || !pos || !ch)) return fail(ctx, DCTAE_EINVAL, "NULL batch tensor");
+  if (codes) {
+    if (!norm || !norm->median_dev || !norm->b_dev) return fail(ctx, DCTAE_EINVAL, "decode from codes needs PatchNorm");
+    if ((rc = check_lfq(ctx, lfq, PP))) return rc;
+  } else if (n_rows > 0 && !patches) {
+    return fail(ctx, DCTAE_EINVAL, "decode needs codes or patches");
+  }
+  if (n_img == 0) return 0;
+  for (int64_t i = 0; i < (int64_t)n_rows * lut_w; ++i)
+    if (img_lut[i] < -1 || img_lut[i] >= n_img) return fail(ctx, DCTAE_EINVAL, "image LUT entry out of range");
+  std::vector<ImgDesc> D(n_img);
+  int64_t wsf = 0, max_hw = 1;
+  for (int i = 0; i < n_img; ++i) {
+    ImgDesc& d = D[i];
+    std::memset(&d, 0, sizeof(d));
+    d.H = out_hw[2 * i];
+    d.W = out_hw[2 * i + 1];
+    d.ph = patch_hw[2 * i];
+    d.pw = patch_hw[2 * i + 1];
+    if (d.ph < 1 || d.pw < 1 || P * d.ph > d.H || P * d.pw > d.W)
+      return fail(ctx, DCTAE_EINVAL, "image " + std::to_string(i) + ": patch_sizes do not fit original_sizes (FE:304)");
+    d.qh = std::min(d.ph, cfg->max_patch_h);
+    d.qw = std::min(d.pw, cfg->max_patch_w);
+    d.Kh = P * d.qh;
+    d.Kw = P * d.qw;
+    d.rgb_off = out_off[i];
+    d.ws_y = wsf;
+    wsf += 3ll * d.Kh * d.Kw;
+    d.ws_t = wsf;
+    wsf += 3ll * d.H * d.Kw;
+    d.ws_p = wsf;
+    wsf += 3ll * d.H * d.W;
+    max_hw = std::max<int64_t>(max_hw, (int64_t)d.H * d.W);
+  }
+  if ((rc = ensure_ws(ctx, (size_t)wsf * 4, 256))) return rc;
+  const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
+  std::vector<GemmProblem> probs;
+  std::vector<TileRef> t1, t2;
+  for (int i = 0; i < n_img; ++i) {
+    const ImgDesc& d = D[i];
+    const float *CW, *CH;
+    if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW))) return rc;
+    if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH))) return rc;
+    float* ws = ctx->ws;
+    // U[c][y][kx] = sum_ky CH[ky][y] * Ysp[c][ky][kx]
+    GemmProblem g1 = gemm(CH, 0, 1, d.H, ws + d.ws_y, (int64_t)d.Kh * d.Kw, 1, d.Kw, ws + d.ws_t,
+                          (int64_t)d.H * d.Kw, d.Kw, 1, d.H, d.Kw, d.Kh, 3);
+    // X[c][y][x] = sum_kx U[c][y][kx] * CW[kx][x]
+    GemmProblem g2 = gemm(ws + d.ws_t, (int64_t)d.H * d.Kw, d.Kw, 1, CW, 0, 1, d.W, ws + d.ws_p,
+                          (int64_t)d.H * d.W, d.W, 1, d.H, d.W, d.Kw, 3);
+    int pr = (int)probs.size();
+    probs.push_back(g1);
+    probs.push_back(g2);
+    add_tiles(t1, pr, g1);
+    add_tiles(t2, pr + 1, g2);
+  }
+  PlanBuf pb;
+  size_t d_off = pb.add(D.data(), D.size());
+  size_t g_off = pb.add(probs.data(), probs.size());
+  size_t t1_off = pb.add(t1.data(), t1.size());
+  size_t t2_off = pb.add(t2.data(), t2.size());
+  size_t lut_off = pb.add(img_lut, (size_t)n_rows * lut_w);
+  order_after_previous(ctx, s);
+  if ((rc = upload_plan(ctx, pb, s))) return rc;
+  uint8_t* pd = ctx->plan_dev;
+  const ImgDesc* dd = (const ImgDesc*)(pd + d_off);
+  HIPCHK(ctx, hipMemsetAsync(ctx->ws, 0, (size_t)wsf * 4, s));
+  DecodeArgs a{};
+  a.ids = ids;
+  a.key_pad = key_pad;
+  a.pos = pos;
+  a.ch = ch;
+  a.codes = codes;
+  a.patches = patches;
+  a.lut = (const int32_t*)(pd + lut_off);
+  a.lut_w = lut_w;
+  a.S = S;
+  a.P = P;
+  a.use_codes = codes ? 1 : 0;
+  if (codes) {
+    a.cb_dim = lfq->codebook_dim;
+    a.ncb = lfq->num_codebooks;
+    a.scale = lfq->codebook_scale;
+    a.median = norm->median_dev;
+    a.b = norm->b_dev;
+    a.eps = norm->eps;
+  }
+  a.maxph = cfg->max_patch_h;
+  a.maxpw = cfg->max_patch_w;
+  a.err = ctx->err_dev;
+  {
+    Timer t(ctx, s, "scatter_tokens");
+    launch_scatter_tokens((int64_t)n_rows * S, dd, ctx->ws, a, s);
+  }
+  {
+    Timer t(ctx, s, "idct_cols");
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s);
+  }
+  {
+    Timer t(ctx, s, "idct_rows");
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s);
+  }
+  {
+    Timer t(ctx, s, "ipt_to_rgb");
+    launch_ipt_to_rgb(dd, n_img, max_hw, ctx->ws, rgb, ctx->cm, s);
+  }
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// Internal structures shared by the HIP kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dctae {
+
+constexpr int kMaxP = 16;          // patch_size upper bound of the fused kernels
+constexpr int kMaxCodebooks = 256; // num_codebooks upper bound (P*P / codebook_dim)
+
+// Colour matrices (row-major 3x3, fp32 bits as the reference builds them).
+struct ColorMats {
+  float rgb2lms[9];
+  float lms2ipt[9];
+  float ipt2lms[9];
+  float lms2rgb[9];
+};
+
+// Per-image plan entry (device resident).
+struct ImgDesc {
+  int64_t rgb_off;   // element offset of the (3,H,W) image in the input buffer
+  int64_t ws_p;      // workspace offsets (floats): ipt image (3,H,W)
+  int64_t ws_t;      //   row-pass output  Tt (3, Kw, H)
+  int64_t ws_y;      //   spectrum corner   Y (3, Kh, Kw)
+  int64_t tok_off;   // first flat token of this image in token staging
+  int32_t H, W;
+  int32_t ph, pw;    // uncapped patch grid  (H/P, W/P)
+  int32_t qh, qw;    // capped patch grid    min(ph, max_patch_h) ...
+  int32_t Kh, Kw;    // kept spectrum corner P*qh, P*qw
+  int32_t T;         // tokens = C*qh*qw
+  int32_t row, col, k, local_id;  // packing
+  int32_t fft_rows, fft_cols;     // 1 if the FFT kernels handle this image's rows/cols
+};
+
+// Generic batched strided fp32 GEMM problem:
+//   O[c][m][n] = sum_k A[c][m][k] * B[c][n][k]     (c < C)
+struct GemmProblem {
+  const float* A;
+  const float* B;
+  float* O;
+  int64_t sAc, sAm, sAk;
+  int64_t sBc, sBn, sBk;
+  int64_t sOc, sOm, sOn;
+  int32_t M, N, K, C;
+  int32_t tiles_n;   // ceil(N / 64)
+  int32_t pad;
+};
+
+struct TileRef {
+  int32_t problem;
+  int32_t tile;  // tm * tiles_n + tn
+};
+
+struct EncParams {
+  int32_t P, C, maxph, maxpw, S;
+  float ci[3];
+  float mw;
+  // PatchNorm (nullable median => no norm/codes)
+  const float* median;
+  const float* b;
+  float eps, min_val, max_val;
+  // LFQ
+  int32_t cb_dim, ncb;
+  float scale;
+};
+
+struct TokenSinks {
+  uint16_t* codes;   // (T, ncb) or null
+  float* scores;     // (T)
+  float* raw;        // (T, P*P) or null
+  float* norm;       // (T, P*P) or null
+};
+
+struct PackSinks {
+  int64_t* codes;     // (R,S,ncb)
+  int64_t* pos;       // (R,S,2)
+  int64_t* ch;        // (R,S)
+  int64_t* ids;       // (R,S)
+  float* patches;     // (R,S,PP) gathered from norm staging
+  float* raw;         // (R,S,PP) gathered from raw staging
+  float* scores;      // (R,S)
+};
+
+struct DecodeArgs {
+  const int64_t* ids;       // (R,S)
+  const uint8_t* key_pad;   // (R,S)
+  const int64_t* pos;       // (R,S,2)
+  const int64_t* ch;        // (R,S)
+  const int64_t* codes;     // (R,S,ncb) when use_codes
+  const float* patches;     // (R,S,PP) otherwise
+  const int32_t* lut;       // (R, lut_w) row-local id -> image index (-1 = none)
+  int32_t lut_w, S, P, use_codes;
+  int32_t cb_dim, ncb;
+  float scale;
+  const float* median;
+  const float* b;
+  float eps;
+  int32_t maxph, maxpw;
+  int* err;
+};
+
+}  // namespace dctae

@@ -1,0 +1,569 @@
+// HIP kernels (gfx950 / CDNA4) for the dct-autoencoder feature-extraction
+// hot path.  Host-side planning and the C ABI live in dctae_api.hip.
+//
+// Numerics notes (see DESIGN.md "Bit-exactness"):
+//  * compiled with -ffp-contract=off: every a*b+c below is two roundings
+//    unless written as fmaf() on purpose (only in DCT/colour arithmetic, which
+//    is compared with a tolerance);
+//  * PatchNorm / LFQ / score arithmetic uses __fmul_rn/__fadd_rn/__fdiv_rn
+//    in the reference's op order so it is bit-exact given identical inputs.
+#include "dctae_internal.h"
+#include "dctae_launch.h"
+
+namespace dctae {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ float mat3_row(const float* m, int i, float a, float b, float c) {
+  // lms/ipt channel mix (reference util.py:46-47 einsum "i j, ... j h w")
+  return fmaf(m[3 * i + 2], c, fmaf(m[3 * i + 1], b, m[3 * i + 0] * a));
+}
+
+__device__ __forceinline__ float signed_pow(float x, float p) {
+  // util.py:76-78: y = |x|**p ; y[x<0] = -y
+  float y = powf(fabsf(x), p);
+  return x < 0.0f ? -y : y;
+}
+
+// NaN-propagating max (torch.amax semantics)
+__device__ __forceinline__ float nanmax(float a, float b) {
+  return (a != a || a > b) ? a : ((b != b) ? b : (a > b ? a : b));
+}
+
+// order-preserving float -> uint32 key; every NaN sorts above +inf
+// (torch.sort(descending=True) puts NaN first).
+__device__ __forceinline__ uint32_t float_key(float f) {
+  if (f != f) return 0xFFFFFFFFu;
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// PatchNorm eval for one element, reference op order (patchnorm.py:157-163):
+//   std = b * 2**0.5 + eps ; y = (x - m) / std ; clamp(min, max)
+__device__ __forceinline__ float pn_forward(float x, float m, float b, float eps, float lo, float hi) {
+  float sd = __fadd_rn(__fmul_rn(b, 1.41421353816986083984375f), eps);
+  float y = __fdiv_rn(__fsub_rn(x, m), sd);
+  // torch.clamp_ propagates NaN
+  return (y != y) ? y : fminf(fmaxf(y, lo), hi);
+}
+
+// PatchNorm.inverse_norm (patchnorm.py:167-177): y * std + m, two roundings.
+__device__ __forceinline__ float pn_inverse(float y, float m, float b, float eps) {
+  float sd = __fadd_rn(__fmul_rn(b, 1.41421353816986083984375f), eps);
+  return __fadd_rn(__fmul_rn(y, sd), m);
+}
+
+// ---------------------------------------------------------------------------
+// synthetic images (same hash as oracle/rng.py)
+// ---------------------------------------------------------------------------
+
+__global__ void k_synth(uint64_t seed, int64_t first, int64_t per_img, int32_t n_img, float* out) {
+  const int img = blockIdx.y;
+  const uint64_t key = splitmix64(splitmix64(seed) ^ (uint64_t)(first + img));
+  float* o = out + (int64_t)img * per_img;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < per_img;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t u = splitmix64(key + (uint64_t)e);
+    o[e] = (float)(u >> 40) * 5.9604644775390625e-08f;  // 2^-24
+  }
+}
+
+void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_t W, float* out,
+                  hipStream_t s) {
+  int64_t per = 3ll * H * W;
+  int gx = (int)std::min<int64_t>((per + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_synth, dim3(gx, n_img), dim3(256), 0, s, seed, first, per, n_img, out);
+}
+
+// ---------------------------------------------------------------------------
+// colour transforms (reference util.py:70-97)
+// ---------------------------------------------------------------------------
+
+__global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
+                             float* __restrict__ ws, ColorMats cm) {
+  const ImgDesc d = imgs[blockIdx.y];
+  const int64_t hw = (int64_t)d.H * d.W;
+  const float* src = rgb + d.rgb_off;
+  float* dst = ws + d.ws_p;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hw;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float r = src[e], g = src[hw + e], b = src[2 * hw + e];
+    float l0 = signed_pow(mat3_row(cm.rgb2lms, 0, r, g, b), 0.430000007152557373046875f);
+    float l1 = signed_pow(mat3_row(cm.rgb2lms, 1, r, g, b), 0.430000007152557373046875f);
+    float l2 = signed_pow(mat3_row(cm.rgb2lms, 2, r, g, b), 0.430000007152557373046875f);
+    dst[e] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
+    dst[hw + e] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
+    dst[2 * hw + e] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+  }
+}
+
+void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* rgb, float* ws,
+                       const ColorMats& cm, hipStream_t s) {
+  int gx = (int)std::min<int64_t>((max_hw + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_rgb_to_ipt, dim3(gx, n_img), dim3(256), 0, s, imgs, rgb, ws, cm);
+}
+
+// ipt (3,H,W) in place -> rgb written to out (3,H,W)
+__global__ void k_ipt_to_rgb(const ImgDesc* __restrict__ imgs, const float* __restrict__ ws,
+                             float* __restrict__ out, ColorMats cm) {
+  const ImgDesc d = imgs[blockIdx.y];
+  const int64_t hw = (int64_t)d.H * d.W;
+  const float* src = ws + d.ws_p;
+  float* dst = out + d.rgb_off;
+  const float inv_gamma = 2.3255813121795654296875f;  // fp32(1/0.43)
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hw;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    float i0 = src[e], i1 = src[hw + e], i2 = src[2 * hw + e];
+    float l0 = signed_pow(mat3_row(cm.ipt2lms, 0, i0, i1, i2), inv_gamma);
+    float l1 = signed_pow(mat3_row(cm.ipt2lms, 1, i0, i1, i2), inv_gamma);
+    float l2 = signed_pow(mat3_row(cm.ipt2lms, 2, i0, i1, i2), inv_gamma);
+    dst[e] = mat3_row(cm.lms2rgb, 0, l0, l1, l2);
+    dst[hw + e] = mat3_row(cm.lms2rgb, 1, l0, l1, l2);
+    dst[2 * hw + e] = mat3_row(cm.lms2rgb, 2, l0, l1, l2);
+  }
+}
+
+void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* ws, float* out,
+                       const ColorMats& cm, hipStream_t s) {
+  int gx = (int)std::min<int64_t>((max_hw + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_ipt_to_rgb, dim3(gx, n_img), dim3(256), 0, s, imgs, ws, out, cm);
+}
+
+// ---------------------------------------------------------------------------
+// generic batched strided fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32)
+//   O[c][m][n] = sum_k A[c][m][k] * B[c][n][k]
+// 64x64 output tile per workgroup, 4 waves (2x2) of 32x32, K chunks of 32.
+// Used for the DCT of sizes without an FFT plan and for the decode IDCT.
+// ---------------------------------------------------------------------------
+
+constexpr int GT = 64;      // tile edge
+constexpr int GK = 32;      // k chunk
+constexpr int GLD = GK + 4; // LDS row stride (floats), keeps float4 alignment
+
+template <int NC>
+__global__ __launch_bounds__(256) void k_gemm_f32(const GemmProblem* __restrict__ probs,
+                                                  const TileRef* __restrict__ tiles) {
+  __shared__ __attribute__((aligned(16))) float As[NC][GT * GLD];
+  __shared__ __attribute__((aligned(16))) float Bs[NC][GT * GLD];
+  const TileRef tr = tiles[blockIdx.x];
+  const GemmProblem p = probs[tr.problem];
+  const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
+  const int m0 = tm * GT, n0 = tn * GT;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+  const bool a_shared = (p.sAc == 0), b_shared = (p.sBc == 0);
+
+  floatx16 acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
+
+  for (int k0 = 0; k0 < p.K; k0 += GK) {
+    // ---- stage A and B tiles (generic strides, zero-filled at the edges)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (c == 0 || !a_shared) {
+        const float* A = p.A + (int64_t)c * p.sAc;
+        const bool kfast = (p.sAk == 1);
+#pragma unroll
+        for (int i = 0; i < (GT * GK) / 256; ++i) {
+          int e = tid + 256 * i;
+          int mm = kfast ? (e >> 5) : (e & 63);
+          int kk = kfast ? (e & 31) : (e >> 6);
+          int gm = m0 + mm, gk = k0 + kk;
+          float v = 0.0f;
+          if (gm < p.M && gk < p.K) v = A[(int64_t)gm * p.sAm + (int64_t)gk * p.sAk];
+          As[c][mm * GLD + kk] = v;
+        }
+      }
+      if (c == 0 || !b_shared) {
+        const float* B = p.B + (int64_t)c * p.sBc;
+        const bool kfast = (p.sBk == 1);
+#pragma unroll
+        for (int i = 0; i < (GT * GK) / 256; ++i) {
+          int e = tid + 256 * i;
+          int nn = kfast ? (e >> 5) : (e & 63);
+          int kk = kfast ? (e & 31) : (e >> 6);
+          int gn = n0 + nn, gk = k0 + kk;
+          float v = 0.0f;
+          if (gn < p.N && gk < p.K) v = B[(int64_t)gn * p.sBn + (int64_t)gk * p.sBk];
+          Bs[c][nn * GLD + kk] = v;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- MFMA: lane half h takes k = 8g + 4h + s in step s of group g
+#pragma unroll
+    for (int g = 0; g < GK / 8; ++g) {
+      const int kofs = 8 * g + 4 * half;
+      float4 a4[NC], b4[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int ca = a_shared ? 0 : c, cb = b_shared ? 0 : c;
+        a4[c] = *reinterpret_cast<const float4*>(&As[ca][(wm * 32 + l32) * GLD + kofs]);
+        b4[c] = *reinterpret_cast<const float4*>(&Bs[cb][(wn * 32 + l32) * GLD + kofs]);
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[c].x, b4[c].x, acc[c], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[c].y, b4[c].y, acc[c], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[c].z, b4[c].z, acc[c], 0, 0, 0);
+        acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[c].w, b4[c].w, acc[c], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // ---- store: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float* O = p.O + (int64_t)c * p.sOc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+      int gm = m0 + wm * 32 + row, gn = n0 + wn * 32 + l32;
+      if (gm < p.M && gn < p.N) O[(int64_t)gm * p.sOm + (int64_t)gn * p.sOn] = acc[c][r];
+    }
+  }
+}
+
+void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s) {
+  if (n_tiles <= 0) return;
+  if (nc == 3)
+    hipLaunchKernelGGL(k_gemm_f32<3>, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else
+    hipLaunchKernelGGL(k_gemm_f32<1>, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+}
+
+// ---------------------------------------------------------------------------
+// tile epilogue: spectrum corner Y (3,Kh,Kw) -> per token (flat order
+// f = (h*qw+w)*3 + c): importance score (FE:401-416), LFQ codes of the
+// PatchNorm'd token (patchnorm.py:157-165, lfq.py:174-187), optional raw /
+// normalised token copies.  One 16-lane group per token, lane j = tile row j.
+// ---------------------------------------------------------------------------
+
+
+// one token, called by all 16 lanes of a group; vals[p2] = Y[P*h + j][P*w + p2]
+__device__ void token_epilogue(const EncParams& ep, int c, int h, int w, int j, int g16,
+                               const float* vals, int64_t tok, TokenSinks sk, uint16_t* rowbits) {
+  const int P = ep.P, PP = P * P;
+  float amax = 0.0f;
+  uint32_t bits = 0;
+  const bool lane_on = j < P;
+  if (lane_on) {
+    const int64_t tab = ((((int64_t)c * ep.maxph + h) * ep.maxpw) + w) * PP + (int64_t)j * P;
+    for (int p2 = 0; p2 < P; ++p2) {
+      float v = vals[p2];
+      amax = nanmax(amax, fabsf(v));
+      if (sk.raw) sk.raw[tok * PP + j * P + p2] = v;
+      if (ep.median) {
+        float y = pn_forward(v, ep.median[tab + p2], ep.b[tab + p2], ep.eps, ep.min_val, ep.max_val);
+        if (y > 0.0f) bits |= 1u << p2;
+        if (sk.norm) sk.norm[tok * PP + j * P + p2] = y;
+      }
+    }
+  }
+  // group max over the 16 lanes (xor shuffles stay inside the group)
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
+  if (j == 0) {
+    // score = amax*mw + (-(h+w))/ci[c]      (FE:409-416, fp32 ops)
+    float s = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
+    sk.scores[tok] = s;
+  }
+  if (ep.median && sk.codes) {
+    if (lane_on) rowbits[g16 * kMaxP + j] = (uint16_t)bits;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int q = j; q < ep.ncb; q += 16) {
+      uint32_t code = 0;
+      for (int d = 0; d < ep.cb_dim; ++d) {
+        int e = q * ep.cb_dim + d;
+        uint32_t bit = (rowbits[g16 * kMaxP + e / P] >> (e % P)) & 1u;
+        code |= bit << (ep.cb_dim - 1 - d);
+      }
+      sk.codes[tok * ep.ncb + q] = (uint16_t)code;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// dense path: Y from workspace.  grid (ceil(Tmax/64), n_img), 256 threads:
+// each block handles 64 tokens (16 per pass, 4 passes).
+__global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict__ imgs,
+                                                       const float* __restrict__ ws, EncParams ep,
+                                                       TokenSinks sk) {
+  __shared__ uint16_t rowbits[16 * kMaxP];
+  const ImgDesc d = imgs[blockIdx.y];
+  const int g16 = threadIdx.x >> 4, j = threadIdx.x & 15;
+  const float* Y = ws + d.ws_y;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int f = blockIdx.x * 64 + pass * 16 + g16;
+    if (f >= d.T) break;  // uniform per group; groups past T idle
+    const int c = f % ep.C, s = f / ep.C, h = s / d.qw, w = s % d.qw;
+    float vals[kMaxP];
+    if (j < ep.P) {
+      const float* row = Y + ((int64_t)c * d.Kh + (int64_t)ep.P * h + j) * d.Kw + (int64_t)ep.P * w;
+      for (int p2 = 0; p2 < ep.P; ++p2) vals[p2] = row[p2];
+    }
+    token_epilogue(ep, c, h, w, j, g16, vals, d.tok_off + f, sk, rowbits);
+  }
+}
+
+void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws,
+                          const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
+  hipLaunchKernelGGL(k_tile_epilogue, dim3((max_T + 63) / 64, n_img), dim3(256), 0, s, imgs, ws, ep, sk);
+}
+
+// ---------------------------------------------------------------------------
+// per-image sort (score desc, flat index asc) + scatter into packed rows
+// (FE:418-445 gather, FE:515-605 concatenation).  One block per image.
+// ---------------------------------------------------------------------------
+
+
+__global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ imgs, int np2,
+                                                    EncParams ep, TokenSinks st, PackSinks out) {
+  extern __shared__ uint64_t keys[];
+  const ImgDesc d = imgs[blockIdx.x];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < np2; i += nt) {
+    uint64_t k = 0;
+    if (i < d.T) k = ((uint64_t)float_key(st.scores[d.tok_off + i]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+    keys[i] = k;
+  }
+  // bitonic sort, descending
+  for (int size = 2; size <= np2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int t = tid; t < (np2 >> 1); t += nt) {
+        int i = 2 * t - (t & (stride - 1));
+        int jx = i + stride;
+        uint64_t a = keys[i], b = keys[jx];
+        bool desc = (i & size) == 0;
+        if (desc ? (a < b) : (a > b)) {
+          keys[i] = b;
+          keys[jx] = a;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int S = ep.S, PP = ep.P * ep.P, C = ep.C;
+  const int64_t base = (int64_t)d.row * S + d.col;
+  for (int t = tid; t < d.k; t += nt) {
+    const uint32_t f = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu);
+    const int c = f % C, s = f / C, h = s / d.qw, w = s % d.qw;
+    const int64_t o = base + t;
+    out.pos[2 * o] = h;
+    out.pos[2 * o + 1] = w;
+    out.ch[o] = c;
+    out.ids[o] = d.local_id;
+    if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
+  }
+  if (out.codes) {
+    const int ncb = ep.ncb;
+    for (int e = tid; e < d.k * ncb; e += nt) {
+      const int t = e / ncb, q = e % ncb;
+      const uint32_t f = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu);
+      out.codes[(base + t) * ncb + q] = st.codes[(d.tok_off + f) * ncb + q];
+    }
+  }
+  if (out.patches || out.raw) {
+    for (int64_t e = tid; e < (int64_t)d.k * PP; e += nt) {
+      const int t = (int)(e / PP), q = (int)(e % PP);
+      const uint32_t f = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu);
+      if (out.patches) out.patches[(base + t) * PP + q] = st.norm[(d.tok_off + f) * PP + q];
+      if (out.raw) out.raw[(base + t) * PP + q] = st.raw[(d.tok_off + f) * PP + q];
+    }
+  }
+}
+
+void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
+                      const PackSinks& out, hipStream_t s) {
+  hipLaunchKernelGGL(k_sort_pack, dim3(n_img), dim3(1024), (size_t)np2 * 8, s, imgs, np2, ep, st, out);
+}
+
+// pad positions j >= row_len[r] of each packed row: the reference pads
+// patches with zeros (util.py:149-164), ids/pos/ch with 0 and then runs
+// PatchNorm/LFQ on them like on any token (c = h = w = 0).
+__global__ void k_pad_fill(const int32_t* __restrict__ row_len, int n_rows, EncParams ep, uint8_t* key_pad,
+                           PackSinks out) {
+  const int r = blockIdx.y;
+  const int S = ep.S, PP = ep.P * ep.P;
+  const int len = row_len[r];
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < S; j += gridDim.x * blockDim.x) {
+    const int64_t o = (int64_t)r * S + j;
+    key_pad[o] = (j >= len) ? 1 : 0;
+    if (j < len) continue;
+    out.pos[2 * o] = 0;
+    out.pos[2 * o + 1] = 0;
+    out.ch[o] = 0;
+    out.ids[o] = 0;
+    if (out.scores) out.scores[o] = 0.0f;
+    if (out.raw)
+      for (int e = 0; e < PP; ++e) out.raw[o * PP + e] = 0.0f;
+    if (out.patches)
+      for (int e = 0; e < PP; ++e)
+        out.patches[o * PP + e] = pn_forward(0.0f, ep.median[e], ep.b[e], ep.eps, ep.min_val, ep.max_val);
+    if (out.codes) {
+      for (int q = 0; q < ep.ncb; ++q) {
+        uint32_t code = 0;
+        for (int dd = 0; dd < ep.cb_dim; ++dd) {
+          int e = q * ep.cb_dim + dd;
+          float y = pn_forward(0.0f, ep.median[e], ep.b[e], ep.eps, ep.min_val, ep.max_val);
+          code |= (y > 0.0f ? 1u : 0u) << (ep.cb_dim - 1 - dd);
+        }
+        out.codes[o * ep.ncb + q] = code;
+      }
+    }
+  }
+}
+
+void launch_pad_fill(const int32_t* row_len, int n_rows, const EncParams& ep, uint8_t* key_pad,
+                     const PackSinks& out, hipStream_t s) {
+  int gx = (ep.S + 255) / 256;
+  hipLaunchKernelGGL(k_pad_fill, dim3(gx, n_rows), dim3(256), 0, s, row_len, n_rows, ep, key_pad, out);
+}
+
+// ---------------------------------------------------------------------------
+// standalone elementwise ops on packed tokens
+// ---------------------------------------------------------------------------
+
+__global__ void k_norm(const float* __restrict__ x, const int64_t* __restrict__ ch,
+                       const int64_t* __restrict__ pos, int64_t n, int PP, int maxph, int maxpw,
+                       const float* __restrict__ med, const float* __restrict__ b, float eps, float lo,
+                       float hi, int inverse, float* __restrict__ y, int* __restrict__ err) {
+  const int64_t total = n * PP;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / PP;
+    const int q = (int)(e % PP);
+    const int64_t c = ch[t], h = pos[2 * t], w = pos[2 * t + 1];
+    if (c < 0 || c >= 3 || h < 0 || h >= maxph || w < 0 || w >= maxpw) {
+      // the reference raises IndexError on out-of-range table indices
+      atomicOr(err, 1);
+      y[e] = __int_as_float(0x7fc00000);
+      continue;
+    }
+    const int64_t tab = ((c * maxph + h) * maxpw + w) * PP + q;
+    y[e] = inverse ? pn_inverse(x[e], med[tab], b[tab], eps) : pn_forward(x[e], med[tab], b[tab], eps, lo, hi);
+  }
+}
+
+void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t n, int PP, int maxph,
+                 int maxpw, const float* med, const float* b, float eps, float lo, float hi, int inverse,
+                 float* y, int* err, hipStream_t s) {
+  int64_t total = n * PP;
+  int gx = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (gx <= 0) return;
+  hipLaunchKernelGGL(k_norm, dim3(gx), dim3(256), 0, s, x, ch, pos, n, PP, maxph, maxpw, med, b, eps, lo, hi,
+                     inverse, y, err);
+}
+
+// LFQ forward: one thread per (token, codebook)
+__global__ void k_lfq_forward(const float* __restrict__ x, int64_t n, int cb_dim, int ncb, float scale,
+                              float* __restrict__ q, int64_t* __restrict__ idx) {
+  const int64_t total = n * ncb;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const float* xi = x + e * cb_dim;
+    int64_t code = 0;
+    for (int d = 0; d < cb_dim; ++d) {
+      const bool pos = xi[d] > 0.0f;  // lfq.py:175 (NaN -> False)
+      code += pos ? ((int64_t)1 << (cb_dim - 1 - d)) : 0;
+      if (q) q[e * cb_dim + d] = pos ? scale : -scale;
+    }
+    idx[e] = code;
+  }
+}
+
+void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float scale, float* q, int64_t* idx,
+                        hipStream_t s) {
+  int64_t total = n * ncb;
+  int gx = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (gx <= 0) return;
+  hipLaunchKernelGGL(k_lfq_forward, dim3(gx), dim3(256), 0, s, x, n, cb_dim, ncb, scale, q, idx);
+}
+
+// LFQ.indices_to_codes: bits * scale * 2 - scale
+__global__ void k_lfq_codes(const int64_t* __restrict__ idx, int64_t n, int cb_dim, int ncb, float scale,
+                            float* __restrict__ out) {
+  const int64_t total = n * ncb * cb_dim;
+  const float s2 = scale * 2.0f;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / cb_dim;
+    const int d = (int)(e % cb_dim);
+    const int32_t v = (int32_t)idx[t];  // lfq.py:117 indices.int()
+    const float bit = ((v & (1 << (cb_dim - 1 - d))) != 0) ? 1.0f : 0.0f;
+    out[e] = __fsub_rn(__fmul_rn(bit, s2), scale);
+  }
+}
+
+void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s) {
+  int64_t total = n * ncb * cb_dim;
+  int gx = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  if (gx <= 0) return;
+  hipLaunchKernelGGL(k_lfq_codes, dim3(gx), dim3(256), 0, s, idx, n, cb_dim, ncb, scale, out);
+}
+
+// ---------------------------------------------------------------------------
+// decode: scatter tokens of packed rows into per-image spectrum corners
+// (FE:607-656 revert_patching), optionally dequantising LFQ codes
+// (lfq.py:105-134) and inverting PatchNorm (patchnorm.py:167-177) on the fly.
+// ---------------------------------------------------------------------------
+
+
+__global__ void k_scatter_tokens(int64_t n_tok, const ImgDesc* __restrict__ imgs, float* __restrict__ ws,
+                                 DecodeArgs a) {
+  const int PP = a.P * a.P;
+  const int64_t total = n_tok * PP;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = e / PP;
+    const int q = (int)(e % PP);
+    if (a.key_pad[t]) continue;
+    const int64_t r = t / a.S;
+    const int64_t id = a.ids[t];
+    if (id < 0 || id >= a.lut_w) { atomicOr(a.err, 2); continue; }
+    const int im = a.lut[r * a.lut_w + id];
+    if (im < 0) { atomicOr(a.err, 2); continue; }
+    const ImgDesc d = imgs[im];
+    const int64_t c = a.ch[t], h = a.pos[2 * t], w = a.pos[2 * t + 1];
+    if (c < 0 || c >= 3 || h < 0 || h >= d.qh || w < 0 || w >= d.qw) { atomicOr(a.err, 4); continue; }
+    float v;
+    if (a.use_codes) {
+      const int cbi = q / a.cb_dim, dd = q % a.cb_dim;
+      const int32_t code = (int32_t)a.codes[t * a.ncb + cbi];
+      const float bit = ((code & (1 << (a.cb_dim - 1 - dd))) != 0) ? 1.0f : 0.0f;
+      const float y = __fsub_rn(__fmul_rn(bit, a.scale * 2.0f), a.scale);
+      const int64_t tab = ((c * a.maxph + h) * a.maxpw + w) * PP + q;
+      v = pn_inverse(y, a.median[tab], a.b[tab], a.eps);
+    } else {
+      v = a.patches[e];
+    }
+    const int p1 = q / a.P, p2 = q % a.P;
+    ws[d.ws_y + (c * d.Kh + (int64_t)a.P * h + p1) * d.Kw + (int64_t)a.P * w + p2] = v;
+  }
+}
+
+void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s) {
+  int64_t total = n_tok * a.P * a.P;
+  int gx = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  if (gx <= 0) return;
+  hipLaunchKernelGGL(k_scatter_tokens, dim3(gx), dim3(256), 0, s, n_tok, imgs, ws, a);
+}
+
+}  // namespace dctae

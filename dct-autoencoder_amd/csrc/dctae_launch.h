@@ -1,0 +1,29 @@
+// Host-side launch wrappers of the kernels in dctae_kernels.hip / dctae_fft.hip.
+#pragma once
+#include <algorithm>
+
+#include "dctae_internal.h"
+
+namespace dctae {
+
+void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_t W, float* out, hipStream_t s);
+void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* rgb, float* ws,
+                       const ColorMats& cm, hipStream_t s);
+void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* ws, float* out,
+                       const ColorMats& cm, hipStream_t s);
+void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s);
+void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
+                          const TokenSinks& sk, hipStream_t s);
+void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
+                      const PackSinks& out, hipStream_t s);
+void launch_pad_fill(const int32_t* row_len, int n_rows, const EncParams& ep, uint8_t* key_pad,
+                     const PackSinks& out, hipStream_t s);
+void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t n, int PP, int maxph, int maxpw,
+                 const float* med, const float* b, float eps, float lo, float hi, int inverse, float* y, int* err,
+                 hipStream_t s);
+void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float scale, float* q, int64_t* idx,
+                        hipStream_t s);
+void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
+void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s);
+
+}  // namespace dctae

@@ -1,0 +1,105 @@
+"""LFQ — drop-in for the reference's lookup-free quantizer (dct_autoencoder/lfq.py:35-227).
+
+Same constructor arguments, buffers (``mask``, ``zero``, ``codebook``),
+``forward(x, mask) -> (x_q, indices, commit_loss, distance)`` and
+``indices_to_codes``.  The sign quantisation and index packing run as HIP
+kernels (dctae_lfq_forward / dctae_lfq_indices_to_codes).  When
+``dim != codebook_dim * num_codebooks`` the reference inserts Linear
+projections; those are plain GEMMs and run through torch (hipBLASLt) around
+the kernels.  The training-only losses (commit / entropy, lfq.py:189-204) are
+out of scope of this build.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from math import ceil, log2
+
+import torch
+from einops import rearrange
+from torch import nn
+
+from . import _ops
+from ._lib import LFQCfg
+
+
+def _exists(v):
+    return v is not None
+
+
+class LFQ(nn.Module):
+    def __init__(self, *, dim=None, codebook_size=None, diversity_gamma=2.5,
+                 straight_through_activation=nn.Identity(), num_codebooks=1, keep_num_codebooks_dim=None,
+                 codebook_scale=1.0):
+        super().__init__()
+        assert _exists(dim) or _exists(codebook_size), "either dim or codebook_size must be specified for LFQ"
+        assert not _exists(codebook_size) or log2(codebook_size).is_integer(), \
+            f"your codebook size must be a power of 2 for lookup free quantization (suggested {2 ** ceil(log2(codebook_size))})"
+        codebook_size = codebook_size if _exists(codebook_size) else 2 ** dim
+        codebook_dim = int(log2(codebook_size))
+        codebook_dims = codebook_dim * num_codebooks
+        dim = dim if _exists(dim) else codebook_dims
+        self.has_projections = dim != codebook_dims
+        self.project_in = nn.Linear(dim, codebook_dims) if self.has_projections else nn.Identity()
+        self.project_out = nn.Linear(codebook_dims, dim) if self.has_projections else nn.Identity()
+        self.dim = dim
+        self.codebook_dim = codebook_dim
+        self.num_codebooks = num_codebooks
+        keep_num_codebooks_dim = keep_num_codebooks_dim if _exists(keep_num_codebooks_dim) else num_codebooks > 1
+        assert not (num_codebooks > 1 and not keep_num_codebooks_dim)
+        self.keep_num_codebooks_dim = keep_num_codebooks_dim
+        self.activation = straight_through_activation
+        self.diversity_gamma = diversity_gamma
+        self.codebook_scale = codebook_scale
+        self.register_buffer("mask", 2 ** torch.arange(codebook_dim - 1, -1, -1))
+        self.register_buffer("zero", torch.tensor(0.0), persistent=False)
+        # the (codebook_size, codebook_dim) +-scale table; only materialised for
+        # small codebooks (it is 2**cd x cd floats and no kernel reads it)
+        if codebook_size <= 2 ** 16:
+            bits = ((torch.arange(codebook_size)[..., None].int() & self.mask) != 0).float()
+            self.register_buffer("codebook", bits * codebook_scale * 2 - codebook_scale, persistent=False)
+
+    def cfg(self) -> LFQCfg:
+        return LFQCfg(self.codebook_dim, self.num_codebooks, float(self.codebook_scale))
+
+    @property
+    def dtype(self):
+        return self.mask.dtype if not hasattr(self, "codebook") else self.codebook.dtype
+
+    def bits_to_codes(self, bits):
+        return bits * self.codebook_scale * 2 - self.codebook_scale
+
+    def indices_to_codes(self, indices, project_out=True):
+        """lfq.py:105-134"""
+        is_img_or_video = indices.ndim >= (3 + int(self.keep_num_codebooks_dim))
+        if not self.keep_num_codebooks_dim:
+            indices = rearrange(indices, "... -> ... 1")
+        codes = _ops.lfq_codes(indices, self.cfg())
+        if project_out:
+            codes = self.project_out(codes)
+        if is_img_or_video:
+            codes = rearrange(codes, "b ... d -> b d ...")
+        return codes
+
+    def forward(self, x, mask=None):
+        """lfq.py:136-227 (eval).  ``mask`` (False at padding) is required, as
+        in the reference, and unused in eval."""
+        if mask is None:
+            raise NotImplementedError("mask")
+        if self.training:
+            raise NotImplementedError("LFQ training losses (lfq.py:189-204) are out of scope of the MI355X path")
+        is_img_or_video = x.ndim >= 4
+        if is_img_or_video:
+            x = rearrange(x, "b d ... -> b ... d")
+            shape = x.shape
+            x = x.reshape(shape[0], -1, shape[-1])
+        assert x.shape[-1] == self.dim, f"expected dimension of {self.dim} but received {x.shape[-1]}"
+        x = self.project_in(x)
+        q, indices = _ops.lfq_forward(x, self.cfg())
+        q = self.project_out(q)
+        if is_img_or_video:
+            q = q.reshape(*shape[:-1], q.shape[-1])
+            q = rearrange(q, "b ... d -> b d ...")
+            indices = indices.reshape(*shape[:-1], indices.shape[-1])
+        if not self.keep_num_codebooks_dim:
+            indices = rearrange(indices, "... 1 -> ...")
+        return q, indices, self.zero, self.zero

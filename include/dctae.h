@@ -1,0 +1,205 @@
+/*
+ * dctae.h — C ABI of libdctae.so, the MI355X (gfx950) implementation of the
+ * dct-autoencoder feature-extraction hot path:
+ *
+ *   RGB -> IPT -> global orthonormal DCT-II -> 14x14 spectral tiles ->
+ *   importance order -> packing -> PatchNorm -> LFQ codes          (encode)
+ *   LFQ codes -> +-1 -> inverse PatchNorm -> unpatch -> DCT-III -> RGB (decode)
+ *
+ * The reference (theAdamColton/dct-autoencoder) has no native boundary: its
+ * operator API is the Python class surface.  Each entry point below states
+ * the reference function(s) it replaces (paths relative to the reference
+ * repo; FE = dct_autoencoder/feature_extraction_dct_autoencoder.py).  The
+ * Python layer in dct-autoencoder_amd/ mirrors the reference classes and is
+ * the only intended caller; INTEGRATION.md shows the ctypes binding.
+ *
+ * Conventions
+ *  - Every pointer argument named *_dev is HIP device memory owned by the
+ *    caller; the library never frees or retains it past the call.
+ *  - All work is enqueued on `stream` (a hipStream_t, passed as void*; NULL =
+ *    legacy default stream).  The library never synchronises the host, except
+ *    when it must grow its internal workspace or upload a new plan.
+ *  - Every call returns 0 on success and a negative DCTAE_E* code on error;
+ *    dctae_last_error(ctx) describes the last error of that context.
+ *  - One context per device per host thread (not re-entrant).
+ *  - Integer outputs that the reference returns as torch.long are int64.
+ */
+#ifndef DCTAE_H
+#define DCTAE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCTAE_OK 0
+#define DCTAE_EINVAL (-1)   /* bad argument / shape (reference: AssertionError) */
+#define DCTAE_EHIP (-2)     /* HIP runtime error */
+#define DCTAE_ENOMEM (-3)   /* workspace allocation failed */
+#define DCTAE_EUNSUP (-4)   /* unsupported configuration */
+
+#define DCTAE_ABI_VERSION 1
+
+typedef struct dctae_ctx dctae_ctx;
+
+/* DCTAutoencoderFeatureExtractor.__init__ arguments (FE:108-127). */
+typedef struct {
+  int32_t channels;               /* must be 3 (IPT colour transform, util.py:70-97) */
+  int32_t patch_size;             /* P, 2..16 (reference configs use 14) */
+  int32_t max_patch_h;            /* 32 */
+  int32_t max_patch_w;            /* 32 */
+  int32_t max_seq_len;            /* S */
+  float channel_importances[3];   /* (8, 1, 1) */
+  float magnitude_weight;         /* patch_sample_magnitude_weight, 0.1 */
+} dctae_fe_cfg;
+
+/* Frozen/eval PatchNorm state (patchnorm.py:32-78): tables of shape
+ * (channels, max_patch_h, max_patch_w, P*P), fp32, device. */
+typedef struct {
+  const float* median_dev;
+  const float* b_dev;
+  float eps;        /* 1e-6 */
+  float min_val;    /* -6 */
+  float max_val;    /*  6 */
+} dctae_norm;
+
+/* LFQ without projections (lfq.py:35-96): codebook_dim * num_codebooks must
+ * equal the token dim (P*P); codebook_dim <= 16. */
+typedef struct {
+  int32_t codebook_dim;   /* log2(codebook_size) */
+  int32_t num_codebooks;
+  float codebook_scale;   /* 1.0 */
+} dctae_lfq;
+
+/* Images: `n_img` fp32 RGB images of shape (3, H_i, W_i), contiguous, at
+ * element offsets img_off[i] of rgb_dev (host arrays). */
+typedef struct {
+  const float* rgb_dev;
+  const int64_t* img_off;   /* host, n_img */
+  const int32_t* hw;        /* host, 2*n_img: H0,W0,H1,W1,... */
+  int32_t n_img;
+} dctae_images;
+
+/* Packing of images into rows of length S (host arrays, n_img entries each),
+ * produced by the host mirror of FE._group_patches_by_max_seq_len /
+ * _batch_groups (FE:454-605): image i occupies row[i], positions
+ * [col[i], col[i]+k[i]) and has image id local_id[i] inside its row.
+ * row_len (host, n_rows) = tokens used in each row (key_pad_mask = j >= len). */
+typedef struct {
+  const int32_t* row;
+  const int32_t* col;
+  const int32_t* k;
+  const int32_t* local_id;
+  const int32_t* row_len;
+  int32_t n_rows;
+} dctae_packing;
+
+/* Packed DCTPatches fields (dct_patches.py:6-51), device, rows x S. */
+typedef struct {
+  int64_t* codes_dev;        /* (R, S, num_codebooks) LFQ indices (lfq.py:187) */
+  int64_t* positions_dev;    /* (R, S, 2)  patch_positions [h, w]            */
+  int64_t* channels_dev;     /* (R, S)     patch_channels                    */
+  int64_t* image_ids_dev;    /* (R, S)     batched_image_ids                 */
+  uint8_t* key_pad_dev;      /* (R, S)     key_pad_mask (True = padding)     */
+  float* patches_dev;        /* (R, S, P*P) optional (NULL): PatchNorm output */
+  float* raw_patches_dev;    /* (R, S, P*P) optional (NULL): DCT tokens       */
+  float* scores_dev;         /* (R, S)     optional (NULL): importance score  */
+} dctae_packed_out;
+
+int dctae_abi_version(void);
+int dctae_ctx_create(int device, dctae_ctx** out);
+int dctae_ctx_destroy(dctae_ctx* ctx);
+const char* dctae_last_error(dctae_ctx* ctx);
+
+/* Colour matrices (row-major 3x3 fp32) used by the IPT transforms; the
+ * Python layer passes the reference's exact fp32 values (util.py:40-41, 91:
+ * Trgb2lms = MHPE @ MsRGB, Tlms2rgb = Trgb2lms.inverse(), Mipt, Mipt.inverse()).
+ * Defaults are the same matrices computed in float64 and rounded. */
+int dctae_set_color_matrices(dctae_ctx* ctx, const float* rgb2lms, const float* lms2ipt,
+                             const float* ipt2lms, const float* lms2rgb);
+
+/* Fused encode: FE.preprocess for every image (FE:154-177: rgb_to_ipt,
+ * dct2, _crop_image, _patch_image) + FE._batch_groups (FE:515-605) +
+ * PatchNorm.forward eval (patchnorm.py:157-165) + LFQ.forward eval
+ * (lfq.py:136-227).  Token order inside an image: score desc, flat index asc.
+ * norm may be NULL (then codes_dev must be NULL: only tokens/metadata). */
+int dctae_encode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                 const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
+                 const dctae_packed_out* out, void* stream);
+
+/* Spectrum tokens of each image in flat order f = (h*qw + w)*3 + c, plus the
+ * importance scores (FE:364-416) — the part of FE.preprocess before sorting.
+ * tokens_dev: (sum_i T_i, P*P) fp32; scores_dev: (sum_i T_i); tok_off (host,
+ * n_img): first token row of each image. */
+int dctae_spectrum_tokens(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                          const int64_t* tok_off, float* tokens_dev, float* scores_dev, void* stream);
+
+/* PatchNorm.forward, eval/frozen (patchnorm.py:157-165) on n tokens of dim
+ * P*P with their channel / position (int64 device arrays). Pad tokens are
+ * normalised like the reference does (with c=h=w=0). */
+int dctae_norm_forward(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t max_patch_h,
+                       int32_t max_patch_w, const float* x_dev, const int64_t* channels_dev,
+                       const int64_t* positions_dev, int64_t n, float* y_dev, void* stream);
+
+/* PatchNorm.inverse_norm (patchnorm.py:167-177): y*std + median, no FMA. */
+int dctae_norm_inverse(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t max_patch_h,
+                       int32_t max_patch_w, const float* y_dev, const int64_t* channels_dev,
+                       const int64_t* positions_dev, int64_t n, float* x_dev, void* stream);
+
+/* LFQ.forward eval (lfq.py:136-227): quantized (n, dim) = +-scale (nullable)
+ * and indices (n, num_codebooks) int64. */
+int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, int64_t n,
+                      float* quantized_dev, int64_t* indices_dev, void* stream);
+
+/* LFQ.indices_to_codes (lfq.py:105-134), project_out = identity. */
+int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev,
+                               int64_t n, float* codes_dev, void* stream);
+
+/* Decode of a packed batch back to RGB: FE.postprocess (FE:289-310) =
+ * revert_patching (FE:607-656) -> zero pad to (3,H,W) -> idct2 -> ipt_to_rgb.
+ * With codes_dev != NULL the tokens are first LFQ.indices_to_codes
+ * (lfq.py:105-134) then PatchNorm.inverse_norm (patchnorm.py:167-177), i.e.
+ * DCTAutoencoder.decode_from_codes + inv_normalize_ without the transformer;
+ * with codes_dev == NULL the (un-normalised) patches_dev are used as is.
+ * Images are enumerated row by row and, inside a row, by ascending image id
+ * (FE:628 image_ids.unique()).  img_lut (host, n_rows x lut_w) maps
+ * (row, image id) -> image index (or -1); out_hw / out_off / patch_hw (host,
+ * per image) give the original size, the output element offset in rgb_dev
+ * and the (uncapped) patch_sizes. */
+int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut,
+                 int32_t lut_w, int32_t n_img, const int32_t* out_hw, const int64_t* out_off,
+                 const int32_t* patch_hw, const int64_t* image_ids_dev, const uint8_t* key_pad_dev,
+                 const int64_t* positions_dev, const int64_t* channels_dev, const dctae_norm* norm,
+                 const dctae_lfq* lfq, const int64_t* codes_dev, const float* patches_dev,
+                 float* rgb_dev, void* stream);
+
+/* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an
+ * out-of-range channel / position / image id (the reference raises
+ * IndexError there).  Synchronises `stream`. */
+int dctae_check_device_errors(dctae_ctx* ctx, void* stream);
+
+/* Counter-based synthetic RGB images (same hash as oracle/rng.py):
+ * value(seed, first_index + i, e) for i < n_img, images of (3, H, W)
+ * contiguous. */
+int dctae_synth_images(dctae_ctx* ctx, uint64_t seed, int64_t first_index, int32_t n_img,
+                       int32_t H, int32_t W, float* rgb_dev, void* stream);
+
+/* Per-kernel device timing for benchmarks.  While enabled, every kernel the
+ * library launches is bracketed by a pair of HIP events on its stream (no
+ * host synchronisation).  dctae_timing_collect synchronises those events and
+ * accumulates elapsed time per kernel name; dctae_timing_get(idx) then reads
+ * entry idx (returns DCTAE_EINVAL past the last one); dctae_timing_reset
+ * clears the totals. */
+int dctae_set_timing(dctae_ctx* ctx, int enable);
+int dctae_timing_collect(dctae_ctx* ctx);
+int dctae_timing_get(dctae_ctx* ctx, int idx, const char** name, double* total_ms, int64_t* launches);
+int dctae_timing_reset(dctae_ctx* ctx);
+
+/* Workspace cap in bytes for the chunked encode/decode (default 8 GiB). */
+int dctae_set_workspace_limit(dctae_ctx* ctx, int64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCTAE_H */
