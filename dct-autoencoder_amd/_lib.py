@@ -36,7 +36,7 @@ class FECfg(C.Structure):
 
 class Norm(C.Structure):
     _fields_ = [("median_dev", C.c_void_p), ("b_dev", C.c_void_p), ("eps", C.c_float),
-                ("min_val", C.c_float), ("max_val", C.c_float)]
+                ("min_val", C.c_float), ("max_val", C.c_float), ("thr_dev", C.c_void_p)]
 
 
 class LFQCfg(C.Structure):
@@ -87,6 +87,9 @@ _SIGS = {
                          C.c_int),
     "dctae_timing_reset": ([_P], C.c_int),
     "dctae_set_workspace_limit": ([_P, C.c_int64], C.c_int),
+    "dctae_norm_thresholds": ([_P, C.POINTER(Norm), C.c_int64, _P, _P], C.c_int),
+    "dctae_set_fft": ([_P, C.c_int], C.c_int),
+    "dctae_set_chunk_bytes": ([_P, C.c_int64], C.c_int),
 }
 
 _lib = None

@@ -41,10 +41,33 @@ class NormState:
     eps: float = 1e-6
     min_val: float = -6.0
     max_val: float = 6.0
+    thr: Optional[torch.Tensor] = None   # LFQ-bit thresholds (norm_thresholds), optional
 
     def c(self) -> Norm:
         return Norm(C.c_void_p(self.median.data_ptr()), C.c_void_p(self.b.data_ptr()), float(self.eps),
-                    float(self.min_val), float(self.max_val))
+                    float(self.min_val), float(self.max_val), ptr(self.thr))
+
+
+def norm_thresholds(norm: NormState) -> torch.Tensor:
+    """thr = smallest fp32 x with PatchNorm(x) > 0 per table element (exact;
+    see dctae_norm_thresholds)."""
+    dev = _check_dev(norm.median, norm.b)
+    ctx = _lib.context(dev)
+    thr = torch.empty_like(norm.median)
+    n0 = NormState(norm.median, norm.b, norm.eps, norm.min_val, norm.max_val, None)
+    rc = ctx.lib.dctae_norm_thresholds(ctx.h, C.byref(n0.c()), thr.numel(), ptr(thr), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_norm_thresholds")
+    return thr
+
+
+def set_fft(enable: bool, device=None):
+    ctx = _lib.context(device)
+    ctx.check(ctx.lib.dctae_set_fft(ctx.h, int(bool(enable))), "dctae_set_fft")
+
+
+def set_chunk_bytes(nbytes: int, device=None):
+    ctx = _lib.context(device)
+    ctx.check(ctx.lib.dctae_set_chunk_bytes(ctx.h, int(nbytes)), "dctae_set_chunk_bytes")
 
 
 def _check_dev(*ts):

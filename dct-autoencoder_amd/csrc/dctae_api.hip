@@ -44,12 +44,22 @@ struct dctae_ctx {
   uint8_t* plan_dev = nullptr;
   size_t plan_cap = 0;
   std::vector<uint8_t> plan_last;
+  uint64_t plan_last_id = 0, plan_counter = 0;
   hipEvent_t plan_evt = nullptr;
   hipEvent_t done_evt = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_done = false;
   int* err_dev = nullptr;
   ColorMats cm{};
+  // FFT-DCT plans: tables (W_M^k, alpha/beta) in one device buffer
+  float2* fft_tab = nullptr;
+  int64_t fft_tab_cap = 0, fft_tab_used = 0;
+  std::map<int, FftPlan> fft_plans;   // N -> plan (N = 0 entries never stored)
+  bool fft_enabled = true;
+  int64_t chunk_bytes = 160ll << 20;  // workspace per chunk of the FFT path (MALL-resident T)
+  // cached encode plan
+  std::vector<int64_t> enc_key;
+  struct EncPlan* enc_plan = nullptr;
   // timing
   bool timing = false;
   std::vector<TimedLaunch> pending;
@@ -168,10 +178,14 @@ void mark_done(dctae_ctx* ctx, hipStream_t s) {
   ctx->have_done = true;
 }
 
-int upload_plan(dctae_ctx* ctx, const PlanBuf& pb, hipStream_t s) {
+int upload_plan(dctae_ctx* ctx, const PlanBuf& pb, hipStream_t s, uint64_t plan_id = 0) {
   const size_t n = pb.bytes.size();
   if (n == 0) return 0;
-  if (n == ctx->plan_last.size() && std::memcmp(pb.bytes.data(), ctx->plan_last.data(), n) == 0) return 0;
+  if (plan_id != 0 && plan_id == ctx->plan_last_id) return 0;
+  if (n == ctx->plan_last.size() && std::memcmp(pb.bytes.data(), ctx->plan_last.data(), n) == 0) {
+    ctx->plan_last_id = plan_id;
+    return 0;
+  }
   if (n > ctx->plan_cap) {
     HIPCHK(ctx, hipDeviceSynchronize());
     if (ctx->plan_host) hipHostFree(ctx->plan_host);
@@ -189,6 +203,7 @@ int upload_plan(dctae_ctx* ctx, const PlanBuf& pb, hipStream_t s) {
   HIPCHK(ctx, hipMemcpyAsync(ctx->plan_dev, ctx->plan_host, n, hipMemcpyHostToDevice, s));
   HIPCHK(ctx, hipEventRecord(ctx->plan_evt, s));
   ctx->plan_last = pb.bytes;
+  ctx->plan_last_id = plan_id;
   return 0;
 }
 
@@ -266,6 +281,7 @@ int describe(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int H, int W, ImgDesc& d) 
     return fail(ctx, DCTAE_EINVAL, "image " + std::to_string(H) + "x" + std::to_string(W) +
                                        " is smaller than patch_size (FE:313-314)");
   std::memset(&d, 0, sizeof(d));
+  d.plan_w = d.plan_h = -1;
   d.H = H;
   d.W = W;
   d.ph = std::max(H / P, 1);
@@ -297,6 +313,8 @@ void add_tiles(std::vector<TileRef>& t, int prob, const GemmProblem& g) {
   for (int i = 0; i < tm * g.tiles_n; ++i) t.push_back({prob, i});
 }
 
+const float* norm_thr(const dctae_norm* norm) { return norm ? norm->thr_dev : nullptr; }
+
 EncParams enc_params(const dctae_fe_cfg* cfg, const dctae_norm* norm, const dctae_lfq* lfq) {
   EncParams ep{};
   ep.P = cfg->patch_size;
@@ -327,21 +345,94 @@ int next_pow2(int x) {
   return p;
 }
 
-// Shared front half of encode / spectrum_tokens: per chunk of images, run
-// colour + DCT (FFT kernels where planned, GEMM otherwise) + tile epilogue
-// into token staging; `per_chunk` is then called to consume the staging.
-struct ChunkJob {
-  int i0, i1;              // image range
-  size_t desc_off;         // device offset of ImgDesc array (chunk-local copies)
-  size_t gp_off, rows_t_off, cols_t_off;
-  int n_rows_tiles, n_cols_tiles;
-  int max_T;
-  int64_t max_hw;
-  int64_t tok_base;        // first token (global) of the chunk
-  int fft_mask;
-};
+// FFT plan for length N (Makhoul: M = N/2 point complex FFT); -1 if N has no plan
+int fft_plan_for(dctae_ctx* ctx, int N, FftPlan* out) {
+  if (!ctx->fft_enabled || N < 4 || (N & 1) || N / 2 > 512) return -1;
+  auto it = ctx->fft_plans.find(N);
+  if (it != ctx->fft_plans.end()) {
+    *out = it->second;
+    return it->second.npass > 0 ? 0 : -1;
+  }
+  FftPlan p{};
+  p.N = N;
+  p.M = N / 2;
+  int m = p.M, np = 0;
+  const int rads[7] = {16, 8, 4, 2, 7, 5, 3};
+  while (m > 1 && np < 8) {
+    bool ok = false;
+    for (int r : rads)
+      if (m % r == 0) {
+        p.radix[np++] = r;
+        m /= r;
+        ok = true;
+        break;
+      }
+    if (!ok) break;
+  }
+  if (m != 1) {
+    p.npass = 0;
+    ctx->fft_plans[N] = p;
+    return -1;
+  }
+  p.npass = np;
+  // rows per block of k_fft_rows: 2 (ping-pong) x rows x 3 jobs x (2M+1) floats <= 52 KiB
+  p.rows_per_block = std::max(1, std::min(8, (int)(53248 / (24 * (2 * p.M + 1)))));
+  const int64_t need = p.M + 2ll * (p.M + 1);
+  if (ctx->fft_tab_used + need > ctx->fft_tab_cap) {
+    p.npass = 0;
+    ctx->fft_plans[N] = p;
+    return -1;
+  }
+  std::vector<float2> h(need);
+  const double pi = 3.14159265358979323846;
+  for (int k = 0; k < p.M; ++k) {
+    double a = -2.0 * pi * k / p.M;
+    h[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+  }
+  for (int k = 0; k <= p.M; ++k) {
+    // W = alpha (A + B) + beta (A - B), A = Z[k], B = conj Z[M-k]
+    //   alpha = a/2 * s, beta = -i * a * e^{-2 pi i k / N} / 2 * s, a = e^{-i pi k / (2N)}
+    const double sk = (k == 0) ? std::sqrt(1.0 / N) : std::sqrt(2.0 / N);
+    const double t1 = -pi * k / (2.0 * N), t2 = t1 - 2.0 * pi * k / N;
+    const double ar = std::cos(t1) * 0.5 * sk, ai = std::sin(t1) * 0.5 * sk;
+    const double br = std::cos(t2) * 0.5 * sk, bi = std::sin(t2) * 0.5 * sk;
+    h[p.M + 2 * k] = make_float2((float)ar, (float)ai);
+    h[p.M + 2 * k + 1] = make_float2((float)bi, (float)-br);  // -i * (br + i bi) = bi - i br
+  }
+  if (hipMemcpy(ctx->fft_tab + ctx->fft_tab_used, h.data(), need * sizeof(float2), hipMemcpyHostToDevice) !=
+      hipSuccess) {
+    p.npass = 0;
+    ctx->fft_plans[N] = p;
+    return -1;
+  }
+  p.tw_off = ctx->fft_tab_used;
+  p.post_off = ctx->fft_tab_used + p.M;
+  ctx->fft_tab_used += need;
+  ctx->fft_plans[N] = p;
+  *out = p;
+  return 0;
+}
 
 }  // namespace
+
+// Encode plan: everything the launch sequence needs, cached on the inputs.
+struct ChunkJob {
+  int i0, i1;
+  size_t desc_off, gp_off, rows_t_off, cols_t_off, fr_off, fc_off;
+  int n_rows_tiles, n_cols_tiles, n_fr, n_fc;
+  int max_T, any_gemm_rows, any_gemm_cols;
+  int64_t max_hw;
+  size_t lds_rows, lds_cols;
+};
+
+struct EncPlan {
+  uint64_t id = 0;
+  PlanBuf pb;
+  std::vector<ChunkJob> jobs;
+  size_t rowlen_off = 0, plans_off = 0;
+  size_t ws_need = 0, st_need = 0;
+  int ncb = 0;
+};
 
 // ---------------------------------------------------------------------------
 // C ABI
@@ -377,6 +468,13 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
     delete c;
     return DCTAE_EHIP;
   }
+  c->fft_tab_cap = 1 << 20;
+  if (hipMalloc((void**)&c->fft_tab, c->fft_tab_cap * sizeof(float2)) != hipSuccess) {
+    g_err = "FFT table allocation failed";
+    delete c;
+    return DCTAE_EHIP;
+  }
+  fft_kernel_setup();
   hipEventRecord(c->plan_evt, 0);
   *out = c;
   return 0;
@@ -392,6 +490,8 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->plan_host) hipHostFree(ctx->plan_host);
   if (ctx->plan_dev) hipFree(ctx->plan_dev);
   if (ctx->err_dev) hipFree(ctx->err_dev);
+  if (ctx->fft_tab) hipFree(ctx->fft_tab);
+  delete ctx->enc_plan;
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -419,6 +519,35 @@ int dctae_set_color_matrices(dctae_ctx* ctx, const float* rgb2lms, const float* 
 int dctae_set_workspace_limit(dctae_ctx* ctx, int64_t bytes) {
   if (!ctx || bytes < (1 << 20)) return DCTAE_EINVAL;
   ctx->ws_limit = bytes;
+  return 0;
+}
+
+int dctae_set_fft(dctae_ctx* ctx, int enable) {
+  if (!ctx) return DCTAE_EINVAL;
+  ctx->fft_enabled = enable != 0;
+  return 0;
+}
+
+int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes) {
+  if (!ctx || bytes < (1 << 20)) return DCTAE_EINVAL;
+  ctx->chunk_bytes = bytes;
+  return 0;
+}
+
+int dctae_norm_thresholds(dctae_ctx* ctx, const dctae_norm* norm, int64_t n, float* thr_dev, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!norm || !norm->median_dev || !norm->b_dev || !thr_dev || n < 0)
+    return fail(ctx, DCTAE_EINVAL, "bad threshold arguments");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(ctx, hipMemsetAsync(ctx->err_dev, 0, sizeof(int), s));
+  launch_norm_thresholds(norm->median_dev, norm->b_dev, n, norm->eps, norm->min_val, norm->max_val, thr_dev,
+                         ctx->err_dev, s);
+  HIPCHK(ctx, hipGetLastError());
+  int h = 0;
+  HIPCHK(ctx, hipMemcpyAsync(&h, ctx->err_dev, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(ctx, hipStreamSynchronize(s));
+  HIPCHK(ctx, hipMemsetAsync(ctx->err_dev, 0, sizeof(int), s));
+  if (h) return fail(ctx, DCTAE_EUNSUP, "negative PatchNorm std: thresholds undefined (use thr_dev = NULL)");
   return 0;
 }
 
@@ -488,43 +617,35 @@ int dctae_synth_images(dctae_ctx* ctx, uint64_t seed, int64_t first_index, int32
   return 0;
 }
 
-// The encode engine.  mode 0: full encode (packed outputs); mode 1: spectrum
-// tokens in flat order (tokens_dev / scores_dev, tok_off given).
-static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
-                       const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
-                       const dctae_packed_out* out, const int64_t* tok_off_user, float* tokens_dev,
-                       float* scores_dev, hipStream_t s) {
-  int rc = check_cfg(ctx, cfg);
-  if (rc) return rc;
-  if (!imgs || imgs->n_img < 0 || (imgs->n_img > 0 && (!imgs->rgb_dev || !imgs->img_off || !imgs->hw)))
-    return fail(ctx, DCTAE_EINVAL, "bad image descriptor");
-  const bool full = (pack != nullptr);
+// The encode engine.  Full mode (pack != NULL): packed DCTPatches outputs.
+// Token mode (pack == NULL): spectrum tokens in flat order (tokens_dev /
+// scores_dev at tok_off).  Per image the row DCT (length W) and the column
+// DCT (length H) each run on the FFT kernels when the length has a plan, else
+// on the MFMA GEMM; the intermediate T[c][y][kx] (3, H, Kw) is shared.
+static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                             const dctae_packing* pack, bool full, int ncb, bool want_raw, bool want_norm,
+                             const int64_t* tok_off_user, EncPlan& E) {
   const int n = imgs->n_img;
-  const int P = cfg->patch_size, PP = P * P, C = cfg->channels, S = cfg->max_seq_len;
-  const bool want_codes = full && out && out->codes_dev;
-  if (full) {
-    if (!out || !out->positions_dev || !out->channels_dev || !out->image_ids_dev || !out->key_pad_dev)
-      return fail(ctx, DCTAE_EINVAL, "packed outputs positions/channels/image_ids/key_pad are required");
-    if ((want_codes || out->patches_dev) && !norm) return fail(ctx, DCTAE_EINVAL, "codes/patches need PatchNorm tables");
-    if (want_codes) {
-      rc = check_lfq(ctx, lfq, PP);
-      if (rc) return rc;
-    }
-    if (pack->n_rows < 0 || (n > 0 && (!pack->row || !pack->col || !pack->k || !pack->local_id)) ||
-        (pack->n_rows > 0 && !pack->row_len))
-      return fail(ctx, DCTAE_EINVAL, "bad packing descriptor");
-  }
-  if (norm && (!norm->median_dev || !norm->b_dev)) return fail(ctx, DCTAE_EINVAL, "PatchNorm tables are NULL");
-  const int ncb = want_codes ? lfq->num_codebooks : 0;
-
-  // ---- per-image descriptors and checks
+  const int P = cfg->patch_size, PP = P * P, S = cfg->max_seq_len;
+  int rc;
   std::vector<ImgDesc> D(n);
-  int maxT = 1;
+  std::vector<FftPlan> plans;
+  std::map<int, int> plan_idx;
+  auto plan_of = [&](int N) -> int {
+    auto it = plan_idx.find(N);
+    if (it != plan_idx.end()) return it->second;
+    FftPlan p;
+    int idx = -1;
+    if (fft_plan_for(ctx, N, &p) == 0) {
+      idx = (int)plans.size();
+      plans.push_back(p);
+    }
+    plan_idx[N] = idx;
+    return idx;
+  };
   for (int i = 0; i < n; ++i) {
-    rc = describe(ctx, cfg, imgs->hw[2 * i], imgs->hw[2 * i + 1], D[i]);
-    if (rc) return rc;
+    if ((rc = describe(ctx, cfg, imgs->hw[2 * i], imgs->hw[2 * i + 1], D[i]))) return rc;
     D[i].rgb_off = imgs->img_off[i];
-    maxT = std::max(maxT, D[i].T);
     if (full) {
       D[i].row = pack->row[i];
       D[i].col = pack->col[i];
@@ -535,107 +656,188 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       if (D[i].row < 0 || D[i].row >= pack->n_rows || D[i].col < 0 || D[i].col + D[i].k > S)
         return fail(ctx, DCTAE_EINVAL, "image " + std::to_string(i) + ": packed span outside (rows, S)");
     }
+    D[i].plan_w = plan_of(D[i].W);
+    D[i].plan_h = plan_of(D[i].H);
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
       if (pack->row_len[r] < 0 || pack->row_len[r] > S) return fail(ctx, DCTAE_EINVAL, "row_len out of range");
-  const int np2 = next_pow2(maxT);
-  if ((size_t)np2 * 8 > 64 * 1024) return fail(ctx, DCTAE_EUNSUP, "more than 8192 tokens per image");
-
-  // ---- chunking by workspace size
-  const bool want_raw = (full && out->raw_patches_dev) || (!full && tokens_dev);
-  const bool want_norm = full && out->patches_dev;
-  std::vector<ChunkJob> jobs;
-  {
-    int i = 0;
+  // chunks: FFT images are grouped so the intermediate T of a chunk stays in
+  // the 256 MiB Infinity Cache between the row and column kernels
+  auto ws_of = [&](const ImgDesc& d) {
+    int64_t w = 3ll * d.Kw * d.H;
+    if (d.plan_w < 0) w += 3ll * d.H * d.W;
+    if (d.plan_h < 0) w += 3ll * d.Kh * d.Kw;
+    return w * 4;
+  };
+  auto st_of = [&](const ImgDesc& d) {
+    return (int64_t)d.T * (4 + 2 * ncb + (want_raw && full ? 4 * PP : 0) + (want_norm ? 4 * PP : 0));
+  };
+  for (int i = 0; i < n;) {
+    ChunkJob j{};
+    j.i0 = i;
+    int64_t wsb = 0;
     while (i < n) {
-      ChunkJob j{};
-      j.i0 = i;
-      int64_t wsf = 0, stb = 0;
-      while (i < n) {
-        const ImgDesc& d = D[i];
-        int64_t w = 3ll * d.H * d.W + 3ll * d.Kw * d.H + 3ll * d.Kh * d.Kw;
-        int64_t st = (int64_t)d.T * (4 + 2 * ncb + (want_raw ? 4 * PP : 0) + (want_norm ? 4 * PP : 0));
-        if (i > j.i0 && (wsf + w) * 4 + stb + st > ctx->ws_limit) break;
-        wsf += w;
-        stb += st;
-        ++i;
-      }
-      j.i1 = i;
-      jobs.push_back(j);
+      const int64_t w = ws_of(D[i]);
+      const bool fft = D[i].plan_w >= 0 && D[i].plan_h >= 0;
+      const int64_t cap = fft ? std::min<int64_t>(ctx->chunk_bytes, ctx->ws_limit) : ctx->ws_limit;
+      if (i > j.i0 && wsb + w > cap) break;
+      wsb += w;
+      ++i;
     }
+    j.i1 = i;
+    E.jobs.push_back(j);
   }
-  // ---- workspace sizes (max over chunks), chunk-local offsets
-  size_t ws_need = 0, st_need = 0;
-  int64_t tok_global = 0;
-  for (auto& j : jobs) {
+  const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
+  std::vector<GemmProblem> probs;
+  for (auto& j : E.jobs) {
     int64_t wsf = 0, tok = 0;
     j.max_T = 1;
     j.max_hw = 1;
-    j.tok_base = tok_global;
     for (int i = j.i0; i < j.i1; ++i) {
       ImgDesc& d = D[i];
-      d.ws_p = wsf;
-      wsf += 3ll * d.H * d.W;
       d.ws_t = wsf;
       wsf += 3ll * d.Kw * d.H;
+      d.ws_p = wsf;
+      if (d.plan_w < 0) wsf += 3ll * d.H * d.W;
       d.ws_y = wsf;
-      wsf += 3ll * d.Kh * d.Kw;
-      d.tok_off = full ? tok : (tok_off_user[i] - 0);
+      if (d.plan_h < 0) wsf += 3ll * d.Kh * d.Kw;
+      d.tok_off = full ? tok : tok_off_user[i];
       tok += d.T;
       j.max_T = std::max(j.max_T, d.T);
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
-    tok_global += tok;
-    ws_need = std::max<size_t>(ws_need, (size_t)wsf * 4);
-    st_need = std::max<size_t>(st_need, (size_t)tok * (4 + 2 * ncb + (want_raw && full ? 4 * PP : 0) +
-                                                         (want_norm ? 4 * PP : 0)) + 1024);
+    E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
+    int64_t st = 0;
+    for (int i = j.i0; i < j.i1; ++i) st += st_of(D[i]);
+    E.st_need = std::max<size_t>(E.st_need, (size_t)st + 4096);
   }
-  rc = ensure_ws(ctx, std::max<size_t>(ws_need, 256), std::max<size_t>(st_need, 256));
-  if (rc) return rc;
-
-  // ---- DCT matrices and GEMM problems
-  const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
-  PlanBuf pb;
-  std::vector<GemmProblem> probs;
-  std::vector<TileRef> rows_t, cols_t;
-  std::vector<size_t> desc_offs;
-  for (auto& j : jobs) {
-    j.desc_off = pb.add(D.data() + j.i0, j.i1 - j.i0);
+  if ((rc = ensure_ws(ctx, std::max<size_t>(E.ws_need, 256), std::max<size_t>(E.st_need, 256)))) return rc;
+  float* ws = ctx->ws;
+  for (auto& j : E.jobs) {
+    j.desc_off = E.pb.add(D.data() + j.i0, j.i1 - j.i0);
     const size_t p0 = probs.size();
     std::vector<TileRef> rt, ct;
+    std::vector<int2> fr;
+    std::vector<int4> fc;
+    j.lds_rows = j.lds_cols = 0;
     for (int i = j.i0; i < j.i1; ++i) {
       const ImgDesc& d = D[i];
-      const float *CW, *CH;
-      if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW))) return rc;
-      if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH))) return rc;
-      float* ws = ctx->ws;
-      // rows: Tt[c][kx][y] = sum_x CW[kx][x] * P[c][y][x]
-      GemmProblem gr = gemm(CW, 0, d.W, 1, ws + d.ws_p, (int64_t)d.H * d.W, d.W, 1, ws + d.ws_t,
-                            (int64_t)d.Kw * d.H, d.H, 1, d.Kw, d.H, d.W, 3);
-      // cols: Y[c][ky][kx] = sum_y CH[ky][y] * Tt[c][kx][y]
-      GemmProblem gc = gemm(CH, 0, d.H, 1, ws + d.ws_t, (int64_t)d.Kw * d.H, d.H, 1, ws + d.ws_y,
-                            (int64_t)d.Kh * d.Kw, d.Kw, 1, d.Kh, d.Kw, d.H, 3);
-      int pr = (int)(probs.size() - p0);
-      probs.push_back(gr);
-      probs.push_back(gc);
-      add_tiles(rt, pr, gr);
-      add_tiles(ct, pr + 1, gc);
+      const int li = i - j.i0;
+      if (d.plan_w < 0) {
+        const float* CW;
+        if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW))) return rc;
+        // T[c][y][kx] = sum_x CW[kx][x] * IPT[c][y][x]
+        GemmProblem g = gemm(CW, 0, d.W, 1, ws + d.ws_p, (int64_t)d.H * d.W, d.W, 1, ws + d.ws_t,
+                             (int64_t)d.Kw * d.H, 1, d.Kw, d.Kw, d.H, d.W, 3);
+        add_tiles(rt, (int)(probs.size() - p0), g);
+        probs.push_back(g);
+        j.any_gemm_rows = 1;
+      } else {
+        const FftPlan& p = plans[d.plan_w];
+        for (int y0 = 0; y0 < d.H; y0 += p.rows_per_block) fr.push_back(make_int2(li, y0));
+        j.lds_rows = std::max<size_t>(j.lds_rows, (size_t)2 * p.rows_per_block * 3 * (2 * p.M + 1) * 4);
+      }
+      if (d.plan_h < 0) {
+        const float* CH;
+        if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH))) return rc;
+        // Y[c][ky][kx] = sum_y CH[ky][y] * T[c][y][kx]
+        GemmProblem g = gemm(CH, 0, d.H, 1, ws + d.ws_t, (int64_t)d.Kw * d.H, 1, d.Kw, ws + d.ws_y,
+                             (int64_t)d.Kh * d.Kw, d.Kw, 1, d.Kh, d.Kw, d.H, 3);
+        add_tiles(ct, (int)(probs.size() - p0), g);
+        probs.push_back(g);
+        j.any_gemm_cols = 1;
+      } else {
+        const FftPlan& p = plans[d.plan_h];
+        for (int c = 0; c < 3; ++c)
+          for (int w = 0; w < d.qw; ++w) fc.push_back(make_int4(li, c, w, 0));
+        j.lds_cols = std::max<size_t>(j.lds_cols, (size_t)2 * 2 * p.M * P * 4);
+      }
     }
-    j.gp_off = pb.add(probs.data() + p0, probs.size() - p0);
-    j.rows_t_off = pb.add(rt.data(), rt.size());
-    j.cols_t_off = pb.add(ct.data(), ct.size());
+    j.gp_off = E.pb.add(probs.data() + p0, probs.size() - p0);
+    j.rows_t_off = E.pb.add(rt.data(), rt.size());
+    j.cols_t_off = E.pb.add(ct.data(), ct.size());
+    j.fr_off = E.pb.add(fr.data(), fr.size());
+    j.fc_off = E.pb.add(fc.data(), fc.size());
     j.n_rows_tiles = (int)rt.size();
     j.n_cols_tiles = (int)ct.size();
+    j.n_fr = (int)fr.size();
+    j.n_fc = (int)fc.size();
   }
-  size_t rowlen_off = 0;
-  if (full && pack->n_rows > 0) rowlen_off = pb.add(pack->row_len, pack->n_rows);
-  order_after_previous(ctx, s);
-  rc = upload_plan(ctx, pb, s);
-  if (rc) return rc;
-  uint8_t* pd = ctx->plan_dev;
+  E.plans_off = E.pb.add(plans.data(), plans.size());
+  if (full && pack->n_rows > 0) E.rowlen_off = E.pb.add(pack->row_len, pack->n_rows);
+  E.ncb = ncb;
+  return 0;
+}
 
-  const EncParams ep = enc_params(cfg, norm, want_codes ? lfq : nullptr);
+static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                       const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
+                       const dctae_packed_out* out, const int64_t* tok_off_user, float* tokens_dev,
+                       float* scores_dev, hipStream_t s) {
+  int rc = check_cfg(ctx, cfg);
+  if (rc) return rc;
+  if (!imgs || imgs->n_img < 0 || (imgs->n_img > 0 && (!imgs->rgb_dev || !imgs->img_off || !imgs->hw)))
+    return fail(ctx, DCTAE_EINVAL, "bad image descriptor");
+  const bool full = (pack != nullptr);
+  const int n = imgs->n_img;
+  const int P = cfg->patch_size, PP = P * P;
+  const bool want_codes = full && out && out->codes_dev;
+  if (full) {
+    if (!out || !out->positions_dev || !out->channels_dev || !out->image_ids_dev || !out->key_pad_dev)
+      return fail(ctx, DCTAE_EINVAL, "packed outputs positions/channels/image_ids/key_pad are required");
+    if ((want_codes || out->patches_dev) && !norm) return fail(ctx, DCTAE_EINVAL, "codes/patches need PatchNorm tables");
+    if (want_codes && (rc = check_lfq(ctx, lfq, PP))) return rc;
+    if (pack->n_rows < 0 || (n > 0 && (!pack->row || !pack->col || !pack->k || !pack->local_id)) ||
+        (pack->n_rows > 0 && !pack->row_len))
+      return fail(ctx, DCTAE_EINVAL, "bad packing descriptor");
+  }
+  if (norm && (!norm->median_dev || !norm->b_dev)) return fail(ctx, DCTAE_EINVAL, "PatchNorm tables are NULL");
+  const int ncb = want_codes ? lfq->num_codebooks : 0;
+  const bool want_raw = (full && out->raw_patches_dev) || (!full && tokens_dev);
+  const bool want_norm = full && out->patches_dev;
+
+  // ---- plan cache key: every input that shapes the launch sequence
+  std::vector<int64_t> key;
+  key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
+  key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
+                         (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
+                         (int64_t)ctx->fft_enabled, (int64_t)(intptr_t)ctx->ws});
+  for (int i = 0; i < n; ++i) {
+    key.push_back(imgs->img_off[i]);
+    key.push_back(((int64_t)imgs->hw[2 * i] << 32) | (uint32_t)imgs->hw[2 * i + 1]);
+    if (full) {
+      key.push_back(((int64_t)pack->row[i] << 32) | (uint32_t)pack->col[i]);
+      key.push_back(((int64_t)pack->k[i] << 32) | (uint32_t)pack->local_id[i]);
+    } else {
+      key.push_back(tok_off_user[i]);
+    }
+  }
+  if (full) {
+    key.push_back(pack->n_rows);
+    for (int r = 0; r < pack->n_rows; ++r) key.push_back(pack->row_len[r]);
+  }
+  if (!ctx->enc_plan || key != ctx->enc_key) {
+    EncPlan* E = new EncPlan();
+    E->id = ++ctx->plan_counter;
+    rc = build_encode_plan(ctx, cfg, imgs, pack, full, ncb, want_raw, want_norm, tok_off_user, *E);
+    if (rc) {
+      delete E;
+      return rc;
+    }
+    // the workspace may have moved (ensure_ws) -> the ws pointer is part of the key
+    key[12] = (int64_t)(intptr_t)ctx->ws;
+    delete ctx->enc_plan;
+    ctx->enc_plan = E;
+    ctx->enc_key = key;
+  }
+  EncPlan& E = *ctx->enc_plan;
+  order_after_previous(ctx, s);
+  if ((rc = upload_plan(ctx, E.pb, s, E.id))) return rc;
+  uint8_t* pd = ctx->plan_dev;
+  const FftPlan* plans_d = (const FftPlan*)(pd + E.plans_off);
+
+  EncParams ep = enc_params(cfg, norm, want_codes ? lfq : nullptr);
+  if (norm && !want_norm) ep.thr = norm_thr(norm);
   PackSinks ps{};
   if (full) {
     ps.codes = out->codes_dev;
@@ -647,43 +849,32 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     ps.scores = out->scores_dev;
     if (pack->n_rows > 0) {
       Timer t(ctx, s, "pad_fill");
-      launch_pad_fill((const int32_t*)(pd + rowlen_off), pack->n_rows, ep, out->key_pad_dev, ps, s);
+      launch_pad_fill((const int32_t*)(pd + E.rowlen_off), pack->n_rows, ep, out->key_pad_dev, ps, s);
     }
   }
-
-  for (auto& j : jobs) {
+  for (auto& j : E.jobs) {
     const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
-    {
-      Timer t(ctx, s, "rgb_to_ipt");
-      launch_rgb_to_ipt(dd, nj, j.max_hw, imgs->rgb_dev, ctx->ws, ctx->cm, s);
-    }
-    {
-      Timer t(ctx, s, "gemm_rows");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, s);
-    }
-    {
-      Timer t(ctx, s, "gemm_cols");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, s);
-    }
     TokenSinks sk{};
     if (full) {
-      int64_t ntok = 0;
-      for (int i = j.i0; i < j.i1; ++i) ntok += D[i].T;
+      int64_t nt = 0;
+      // tokens of the chunk: recompute from the plan's host copy
+      const ImgDesc* hdesc = (const ImgDesc*)(E.pb.bytes.data() + j.desc_off);
+      for (int i = 0; i < nj; ++i) nt += hdesc[i].T;
       uint8_t* st = ctx->stage;
       sk.scores = (float*)st;
-      st += ((ntok * 4 + 255) & ~255ll);
+      st += ((nt * 4 + 255) & ~255ll);
       if (ncb) {
         sk.codes = (uint16_t*)st;
-        st += ((ntok * 2 * ncb + 255) & ~255ll);
+        st += ((nt * 2 * ncb + 255) & ~255ll);
       }
       if (want_norm) {
         sk.norm = (float*)st;
-        st += ntok * 4 * PP;
+        st += nt * 4 * PP;
       }
       if (out->raw_patches_dev) {
         sk.raw = (float*)st;
-        st += ntok * 4 * PP;
+        st += nt * 4 * PP;
       }
     } else {
       sk.scores = scores_dev;
@@ -691,9 +882,30 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     }
     EncParams epj = ep;
     if (!full) epj.median = nullptr;
-    {
+    if (j.any_gemm_rows) {
+      {
+        Timer t(ctx, s, "rgb_to_ipt");
+        launch_rgb_to_ipt(dd, nj, j.max_hw, imgs->rgb_dev, ctx->ws, ctx->cm, s);
+      }
+      Timer t(ctx, s, "gemm_rows");
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, s);
+    }
+    if (j.n_fr) {
+      Timer t(ctx, s, "fft_rows");
+      launch_fft_rows(dd, plans_d, (const int2*)(pd + j.fr_off), j.n_fr, j.lds_rows, imgs->rgb_dev, ctx->ws,
+                      ctx->fft_tab, ctx->cm, s);
+    }
+    if (j.any_gemm_cols) {
+      {
+        Timer t(ctx, s, "gemm_cols");
+        launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, s);
+      }
       Timer t(ctx, s, "tile_epilogue");
       launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, s);
+    }
+    if (j.n_fc) {
+      Timer t(ctx, s, "fft_cols");
+      launch_fft_cols(dd, plans_d, (const int4*)(pd + j.fc_off), j.n_fc, j.lds_cols, ctx->ws, ctx->fft_tab, epj, sk, s);
     }
     if (full) {
       Timer t(ctx, s, "sort_pack");
@@ -803,6 +1015,7 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   for (int i = 0; i < n_img; ++i) {
     ImgDesc& d = D[i];
     std::memset(&d, 0, sizeof(d));
+    d.plan_w = d.plan_h = -1;
     d.H = out_hw[2 * i];
     d.W = out_hw[2 * i + 1];
     d.ph = patch_hw[2 * i];

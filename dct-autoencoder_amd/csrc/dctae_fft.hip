@@ -1,0 +1,412 @@
+// FFT-based orthonormal DCT-II for gfx950: the reference's global dct2
+// (torch_dct.dct_2d, reference util.py:333; restated in oracle/ref_cpu.py)
+// computed with Makhoul's algorithm on an M = N/2 point complex FFT
+// (Stockham autosort, radix 2/3/4/5/7/8/16 codelets, LDS ping-pong).
+//
+//   rows:  k_fft_rows  — RGB -> IPT (util.py:70-82) -> row DCT, keeping the
+//                        first Kw coefficients: T[c][y][kx]   (workspace)
+//   cols:  k_fft_cols  — column DCT of T over a strip of P columns, keeping
+//                        Kh rows, then the per-token epilogue (importance
+//                        score FE:401-416, PatchNorm + LFQ codes) into staging.
+//
+// Makhoul (per row of length N, M = N/2):
+//   v[n] = x[2n], v[N-1-n] = x[2n+1];  z[m] = v[2m] + i v[2m+1];  Z = FFT_M(z)
+//   W_k = alpha_k (Z[k] + conj Z[M-k]) + beta_k (Z[k] - conj Z[M-k]),  k = 0..M
+//   X[k] = Re W_k,  X[N-k] = -Im W_k  (alpha/beta fold the twiddles and the
+//   ortho scale; tables built in float64 on the host, dctae_api.hip).
+#include "dctae_device.h"
+#include "dctae_launch.h"
+
+namespace dctae {
+
+__device__ constexpr float kCos3[3] = {1.0f, -0.5f, -0.5f};
+__device__ constexpr float kSin3[3] = {0.0f, 8.660254038e-01f, -8.660254038e-01f};
+__device__ constexpr float kCos5[5] = {1.0f, 3.090169944e-01f, -8.090169944e-01f, -8.090169944e-01f, 3.090169944e-01f};
+__device__ constexpr float kSin5[5] = {0.0f, 9.510565163e-01f, 5.877852523e-01f, -5.877852523e-01f, -9.510565163e-01f};
+__device__ constexpr float kCos7[7] = {1.0f, 6.234898019e-01f, -2.225209340e-01f, -9.009688679e-01f,
+                                       -9.009688679e-01f, -2.225209340e-01f, 6.234898019e-01f};
+__device__ constexpr float kSin7[7] = {0.0f, 7.818314825e-01f, 9.749279122e-01f, 4.338837391e-01f,
+                                       -4.338837391e-01f, -9.749279122e-01f, -7.818314825e-01f};
+__device__ constexpr float kCos16[16] = {1.0f, 9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f,
+                                         -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f,
+                                         -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f, 0.0f,
+                                         3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f};
+__device__ constexpr float kSin16[16] = {0.0f, 3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f, 1.0f,
+                                         9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f,
+                                         -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f,
+                                         -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f};
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // -i * a
+
+// forward DFT codelets, natural order in and out: V[k] = sum_n v[n] e^{-2 pi i nk/R}
+template <int R>
+struct DFT;
+
+template <>
+struct DFT<2> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  }
+};
+
+template <>
+struct DFT<4> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    float2 t2 = cadd(v[1], v[3]), t3 = mul_mi(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+  }
+};
+
+template <>
+struct DFT<8> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 e[4] = {v[0], v[2], v[4], v[6]};
+    float2 o[4] = {v[1], v[3], v[5], v[7]};
+    DFT<4>::run(e);
+    DFT<4>::run(o);
+    const float c = 7.071067812e-01f;
+    float2 w1 = make_float2(c * (o[1].x + o[1].y), c * (o[1].y - o[1].x));    // o1 * (c - ic)
+    float2 w2 = mul_mi(o[2]);                                                  // o2 * -i
+    float2 w3 = make_float2(c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y));   // o3 * (-c - ic)
+    v[0] = cadd(e[0], o[0]);
+    v[4] = csub(e[0], o[0]);
+    v[1] = cadd(e[1], w1);
+    v[5] = csub(e[1], w1);
+    v[2] = cadd(e[2], w2);
+    v[6] = csub(e[2], w2);
+    v[3] = cadd(e[3], w3);
+    v[7] = csub(e[3], w3);
+  }
+};
+
+template <>
+struct DFT<16> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 a[4][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+      for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
+      DFT<4>::run(a[n2]);
+    }
+#pragma unroll
+    for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+      for (int k1 = 1; k1 < 4; ++k1) {
+        const int m = n2 * k1;
+        a[n2][k1] = cmul(a[n2][k1], make_float2(kCos16[m], -kSin16[m]));
+      }
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      float2 b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+      DFT<4>::run(b);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+    }
+  }
+};
+
+template <int R>
+__device__ __forceinline__ void dft_odd(float2* v, const float* C, const float* S) {
+  constexpr int H = (R - 1) / 2;
+  float2 s[H], d[H];
+  float2 x0 = v[0], sum = v[0];
+#pragma unroll
+  for (int n = 1; n <= H; ++n) {
+    s[n - 1] = cadd(v[n], v[R - n]);
+    d[n - 1] = csub(v[n], v[R - n]);
+    sum = cadd(sum, s[n - 1]);
+  }
+  float2 out[R];
+  out[0] = sum;
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
+    float re = x0.x, im = x0.y, re2 = 0.0f, im2 = 0.0f;
+#pragma unroll
+    for (int n = 1; n <= H; ++n) {
+      const int m = (n * k) % R;
+      re = fmaf(s[n - 1].x, C[m], re);
+      im = fmaf(s[n - 1].y, C[m], im);
+      re2 = fmaf(d[n - 1].y, S[m], re2);
+      im2 = fmaf(d[n - 1].x, S[m], im2);
+    }
+    out[k] = make_float2(re + re2, im - im2);
+    out[R - k] = make_float2(re - re2, im + im2);
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = out[k];
+}
+
+template <>
+struct DFT<3> {
+  static __device__ __forceinline__ void run(float2* v) { dft_odd<3>(v, kCos3, kSin3); }
+};
+template <>
+struct DFT<5> {
+  static __device__ __forceinline__ void run(float2* v) { dft_odd<5>(v, kCos5, kSin5); }
+};
+template <>
+struct DFT<7> {
+  static __device__ __forceinline__ void run(float2* v) { dft_odd<7>(v, kCos7, kSin7); }
+};
+
+// complex element m of job j: re at base + j*js + m*cs, im at +im
+struct JobLayout {
+  int js, cs, im;
+};
+
+// one Stockham autosort pass (radix R, Ns = product of the previous radices)
+template <int R>
+__device__ __forceinline__ void stockham_pass(const float* __restrict__ src, float* __restrict__ dst,
+                                              JobLayout L, int n_jobs, int M, int Ns,
+                                              const float2* __restrict__ tw, int tid, int nth) {
+  const int MR = M / R;
+  const int n_items = n_jobs * MR;
+  const int twstep = M / (Ns * R);
+  for (int it = tid; it < n_items; it += nth) {
+    const int job = it % n_jobs;
+    const int j = it / n_jobs;
+    const float* s = src + job * L.js;
+    float2 v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int o = (j + r * MR) * L.cs;
+      v[r] = make_float2(s[o], s[o + L.im]);
+    }
+    const int k1 = j % Ns;
+    if (Ns > 1) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k1 * twstep]);
+    }
+    DFT<R>::run(v);
+    const int idxD = (j / Ns) * Ns * R + k1;
+    float* dd = dst + job * L.js;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int o = (idxD + r * Ns) * L.cs;
+      dd[o] = v[r].x;
+      dd[o + L.im] = v[r].y;
+    }
+  }
+}
+
+__device__ __forceinline__ void run_pass(int R, const float* src, float* dst, JobLayout L, int n_jobs, int M,
+                                         int Ns, const float2* tw, int tid, int nth) {
+  switch (R) {
+    case 16: stockham_pass<16>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    case 8: stockham_pass<8>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    case 4: stockham_pass<4>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    case 2: stockham_pass<2>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    case 7: stockham_pass<7>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    case 5: stockham_pass<5>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    case 3: stockham_pass<3>(src, dst, L, n_jobs, M, Ns, tw, tid, nth); break;
+    default: break;
+  }
+}
+
+// all passes; returns the buffer holding Z (natural order)
+__device__ __forceinline__ float* fft_all(const FftPlan* __restrict__ plp, float* a, float* b, JobLayout L,
+                                          int n_jobs, const float2* tabs, int tid, int nth) {
+  int Ns = 1;
+  const int np = plp->npass, M = plp->M;
+  const float2* tw = tabs + plp->tw_off;
+  for (int p = 0; p < np; ++p) {
+    const int R = plp->radix[p];  // uniform scalar load (a local copy of the array would go to scratch)
+    run_pass(R, a, b, L, n_jobs, M, Ns, tw, tid, nth);
+    __syncthreads();
+    Ns *= R;
+    float* t = a;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+// Makhoul post-processing of one output pair, Z in layout L for job `job`
+__device__ __forceinline__ float2 makhoul_w(const float* z, JobLayout L, int job, int k, int M,
+                                            const float2* __restrict__ post) {
+  const int ka = (k == M) ? 0 : k;
+  const int kb = (k == 0) ? 0 : M - k;
+  const float* s = z + job * L.js;
+  const float2 A = make_float2(s[ka * L.cs], s[ka * L.cs + L.im]);
+  const float2 B = make_float2(s[kb * L.cs], -s[kb * L.cs + L.im]);  // conj Z[M-k]
+  const float2 al = post[2 * k], be = post[2 * k + 1];
+  return cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+}
+
+// ---------------------------------------------------------------------------
+// rows: RGB -> IPT -> row DCT (first Kw coefficients) -> T[c][y][kx]
+// one block = rows [y0, y0 + rows_per_block) of one image, 3 jobs per row
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fft_rows(const ImgDesc* __restrict__ imgs, const FftPlan* __restrict__ plans,
+                                                  const int2* __restrict__ blocks, const float* __restrict__ rgb,
+                                                  float* __restrict__ ws, const float2* __restrict__ tabs,
+                                                  ColorMats cm) {
+  extern __shared__ float lds[];
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const FftPlan* plp = plans + d.plan_w;
+  const int N = plp->N, M = plp->M, y0 = jb.y, rpb = plp->rows_per_block;
+  const int rows = min(rpb, d.H - y0);
+  const int nj = rows * 3;
+  const int js = 2 * M + 1;
+  float* A = lds;
+  float* B = lds + rpb * 3 * js;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int64_t hw = (int64_t)d.H * d.W;
+  const float* src = rgb + d.rgb_off + (int64_t)y0 * N;
+  const float gam = 0.430000007152557373046875f;
+  for (int e = tid; e < rows * N; e += nth) {
+    const int r = e / N, px = e - r * N;
+    const int64_t o = (int64_t)r * N + px;
+    const float R_ = src[o], G_ = src[hw + o], B_ = src[2 * hw + o];
+    const float l0 = signed_pow(mat3_row(cm.rgb2lms, 0, R_, G_, B_), gam);
+    const float l1 = signed_pow(mat3_row(cm.rgb2lms, 1, R_, G_, B_), gam);
+    const float l2 = signed_pow(mat3_row(cm.rgb2lms, 2, R_, G_, B_), gam);
+    const int vidx = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
+    float* a = A + (r * 3) * js + vidx;
+    a[0] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
+    a[js] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
+    a[2 * js] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+  }
+  __syncthreads();
+  const JobLayout L{js, 2, 1};
+  const float* Z = fft_all(plp, A, B, L, nj, tabs, tid, nth);
+  const float2* post = tabs + plp->post_off;
+  const int Kw = d.Kw;
+  for (int e = tid; e < nj * (M + 1); e += nth) {
+    const int job = e / (M + 1), k = e - job * (M + 1);
+    const int r = job / 3, c = job - 3 * r;
+    const float2 W = makhoul_w(Z, L, job, k, M, post);
+    float* trow = ws + d.ws_t + ((int64_t)c * d.H + y0 + r) * Kw;
+    if (k < Kw) trow[k] = W.x;
+    if (k >= 1 && k < M && N - k < Kw) trow[N - k] = -W.y;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cols: column DCT over a strip of P columns of T, then the token epilogue
+// one block = (image, channel, strip) ; strip = tile column w
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fft_cols(const ImgDesc* __restrict__ imgs, const FftPlan* __restrict__ plans,
+                                                  const int4* __restrict__ blocks, const float* __restrict__ ws,
+                                                  const float2* __restrict__ tabs, EncParams ep, TokenSinks sk) {
+  extern __shared__ float lds[];
+  __shared__ uint16_t rowbits[16 * kMaxP];
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const int c = jb.y, strip = jb.z;
+  const FftPlan* plp = plans + d.plan_h;
+  const int N = plp->N, M = plp->M;
+  const int KS = ep.P;
+  const int kx0 = strip * KS;
+  float* A = lds;
+  float* B = lds + 2 * M * KS;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const float* T = ws + d.ws_t + (int64_t)c * d.H * d.Kw + kx0;
+  for (int e = tid; e < N * KS; e += nth) {
+    const int y = e / KS, j = e - y * KS;
+    const int vidx = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
+    A[vidx * KS + j] = T[(int64_t)y * d.Kw + j];
+  }
+  __syncthreads();
+  const JobLayout L{1, 2 * KS, KS};
+  const float* Z = fft_all(plp, A, B, L, KS, tabs, tid, nth);
+  float* Xs = (Z == A) ? B : A;
+  const float2* post = tabs + plp->post_off;
+  const int Kh = d.Kh;
+  for (int e = tid; e < (M + 1) * KS; e += nth) {
+    const int k = e / KS, j = e - k * KS;
+    const float2 W = makhoul_w(Z, L, j, k, M, post);
+    if (k < Kh) Xs[k * KS + j] = W.x;
+    if (k >= 1 && k < M && N - k < Kh) Xs[(N - k) * KS + j] = -W.y;
+  }
+  __syncthreads();
+  const int g16 = tid >> 4, jl = tid & 15;
+  const int w = strip;
+  for (int h = g16; h < d.qh; h += nth >> 4) {
+    float vals[kMaxP];
+    if (jl < ep.P) {
+#pragma unroll
+      for (int p2 = 0; p2 < kMaxP; ++p2)
+        if (p2 < ep.P) vals[p2] = Xs[(ep.P * h + jl) * KS + p2];
+    }
+    const int f = (h * d.qw + w) * ep.C + c;
+    token_epilogue(ep, c, h, w, jl, g16, vals, d.tok_off + f, sk, rowbits);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LFQ-bit thresholds: thr = smallest fp32 x with PatchNorm(x) > 0.
+// PatchNorm(x) = clamp((x - m) / (b*sqrt2 + eps)) is monotone in x for a
+// positive std, so bit(x) == (x >= thr) exactly (thr = NaN: never).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float key_to_float(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+__global__ void k_norm_thresholds(const float* __restrict__ med, const float* __restrict__ b, int64_t n, float eps,
+                                  float lo, float hi, float* __restrict__ thr, int* __restrict__ bad) {
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const float m = med[e], bb = b[e];
+    const float sd = __fadd_rn(__fmul_rn(bb, 1.41421353816986083984375f), eps);
+    if (sd < 0.0f) atomicOr(bad, 1);
+    auto pred = [&](float t) { return pn_forward(t, m, bb, eps, lo, hi) > 0.0f; };
+    const float inf = __uint_as_float(0x7f800000u);
+    float t;
+    if (!pred(inf)) {
+      t = __uint_as_float(0x7fc00000u);
+    } else if (pred(-inf)) {
+      t = -inf;
+    } else {
+      uint32_t klo = float_key(-inf), khi = float_key(inf);
+      while (khi - klo > 1) {
+        const uint32_t mid = klo + (khi - klo) / 2;
+        if (pred(key_to_float(mid))) khi = mid; else klo = mid;
+      }
+      t = key_to_float(khi);
+    }
+    thr[e] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+
+void fft_kernel_setup() {
+  hipFuncSetAttribute((const void*)k_fft_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void*)k_fft_cols, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+void launch_fft_rows(const ImgDesc* imgs, const FftPlan* plans, const int2* blocks, int n_blocks, size_t lds,
+                     const float* rgb, float* ws, const float2* tabs, const ColorMats& cm, hipStream_t s) {
+  if (n_blocks <= 0) return;
+  hipLaunchKernelGGL(k_fft_rows, dim3(n_blocks), dim3(256), lds, s, imgs, plans, blocks, rgb, ws, tabs, cm);
+}
+
+void launch_fft_cols(const ImgDesc* imgs, const FftPlan* plans, const int4* blocks, int n_blocks, size_t lds,
+                     const float* ws, const float2* tabs, const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
+  if (n_blocks <= 0) return;
+  hipLaunchKernelGGL(k_fft_cols, dim3(n_blocks), dim3(256), lds, s, imgs, plans, blocks, ws, tabs, ep, sk);
+}
+
+void launch_norm_thresholds(const float* med, const float* b, int64_t n, float eps, float lo, float hi, float* thr,
+                            int* bad, hipStream_t s) {
+  if (n <= 0) return;
+  int gx = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_norm_thresholds, dim3(gx), dim3(256), 0, s, med, b, n, eps, lo, hi, thr, bad);
+}
+
+}  // namespace dctae

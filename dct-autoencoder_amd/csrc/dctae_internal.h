@@ -29,7 +29,7 @@ struct ImgDesc {
   int32_t Kh, Kw;    // kept spectrum corner P*qh, P*qw
   int32_t T;         // tokens = C*qh*qw
   int32_t row, col, k, local_id;  // packing
-  int32_t fft_rows, fft_cols;     // 1 if the FFT kernels handle this image's rows/cols
+  int32_t plan_w, plan_h;         // FFT plan index for rows (length W) / cols (length H); -1 = GEMM
 };
 
 // Generic batched strided fp32 GEMM problem:
@@ -46,6 +46,14 @@ struct GemmProblem {
   int32_t pad;
 };
 
+// FFT-DCT plan for one length N (M = N/2 point complex FFT), dctae_fft.hip
+struct FftPlan {
+  int32_t N, M, npass, rows_per_block;
+  int32_t radix[8];
+  int64_t tw_off;    // float2 offset of W_M^k (k < M) in the FFT table buffer
+  int64_t post_off;  // float2 offset of (alpha_k, beta_k), k = 0..M
+};
+
 struct TileRef {
   int32_t problem;
   int32_t tile;  // tm * tiles_n + tn
@@ -58,6 +66,7 @@ struct EncParams {
   // PatchNorm (nullable median => no norm/codes)
   const float* median;
   const float* b;
+  const float* thr;   // optional LFQ-bit thresholds (k_norm_thresholds), same shape
   float eps, min_val, max_val;
   // LFQ
   int32_t cb_dim, ncb;

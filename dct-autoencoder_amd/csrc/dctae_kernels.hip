@@ -9,60 +9,10 @@
 //    in the reference's op order so it is bit-exact given identical inputs.
 #include "dctae_internal.h"
 #include "dctae_launch.h"
+#include "dctae_device.h"
 
 namespace dctae {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-// ---------------------------------------------------------------------------
-// small device helpers
-// ---------------------------------------------------------------------------
-
-__device__ __forceinline__ float mat3_row(const float* m, int i, float a, float b, float c) {
-  // lms/ipt channel mix (reference util.py:46-47 einsum "i j, ... j h w")
-  return fmaf(m[3 * i + 2], c, fmaf(m[3 * i + 1], b, m[3 * i + 0] * a));
-}
-
-__device__ __forceinline__ float signed_pow(float x, float p) {
-  // util.py:76-78: y = |x|**p ; y[x<0] = -y
-  float y = powf(fabsf(x), p);
-  return x < 0.0f ? -y : y;
-}
-
-// NaN-propagating max (torch.amax semantics)
-__device__ __forceinline__ float nanmax(float a, float b) {
-  return (a != a || a > b) ? a : ((b != b) ? b : (a > b ? a : b));
-}
-
-// order-preserving float -> uint32 key; every NaN sorts above +inf
-// (torch.sort(descending=True) puts NaN first).
-__device__ __forceinline__ uint32_t float_key(float f) {
-  if (f != f) return 0xFFFFFFFFu;
-  uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// PatchNorm eval for one element, reference op order (patchnorm.py:157-163):
-//   std = b * 2**0.5 + eps ; y = (x - m) / std ; clamp(min, max)
-__device__ __forceinline__ float pn_forward(float x, float m, float b, float eps, float lo, float hi) {
-  float sd = __fadd_rn(__fmul_rn(b, 1.41421353816986083984375f), eps);
-  float y = __fdiv_rn(__fsub_rn(x, m), sd);
-  // torch.clamp_ propagates NaN
-  return (y != y) ? y : fminf(fmaxf(y, lo), hi);
-}
-
-// PatchNorm.inverse_norm (patchnorm.py:167-177): y * std + m, two roundings.
-__device__ __forceinline__ float pn_inverse(float y, float m, float b, float eps) {
-  float sd = __fadd_rn(__fmul_rn(b, 1.41421353816986083984375f), eps);
-  return __fadd_rn(__fmul_rn(y, sd), m);
-}
 
 // ---------------------------------------------------------------------------
 // synthetic images (same hash as oracle/rng.py)
@@ -93,6 +43,7 @@ void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_
 __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
                              float* __restrict__ ws, ColorMats cm) {
   const ImgDesc d = imgs[blockIdx.y];
+  if (d.plan_w >= 0) return;  // rows of this image run through k_fft_rows (IPT fused there)
   const int64_t hw = (int64_t)d.H * d.W;
   const float* src = rgb + d.rgb_off;
   float* dst = ws + d.ws_p;
@@ -255,51 +206,6 @@ void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_t
 // ---------------------------------------------------------------------------
 
 
-// one token, called by all 16 lanes of a group; vals[p2] = Y[P*h + j][P*w + p2]
-__device__ void token_epilogue(const EncParams& ep, int c, int h, int w, int j, int g16,
-                               const float* vals, int64_t tok, TokenSinks sk, uint16_t* rowbits) {
-  const int P = ep.P, PP = P * P;
-  float amax = 0.0f;
-  uint32_t bits = 0;
-  const bool lane_on = j < P;
-  if (lane_on) {
-    const int64_t tab = ((((int64_t)c * ep.maxph + h) * ep.maxpw) + w) * PP + (int64_t)j * P;
-    for (int p2 = 0; p2 < P; ++p2) {
-      float v = vals[p2];
-      amax = nanmax(amax, fabsf(v));
-      if (sk.raw) sk.raw[tok * PP + j * P + p2] = v;
-      if (ep.median) {
-        float y = pn_forward(v, ep.median[tab + p2], ep.b[tab + p2], ep.eps, ep.min_val, ep.max_val);
-        if (y > 0.0f) bits |= 1u << p2;
-        if (sk.norm) sk.norm[tok * PP + j * P + p2] = y;
-      }
-    }
-  }
-  // group max over the 16 lanes (xor shuffles stay inside the group)
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
-  if (j == 0) {
-    // score = amax*mw + (-(h+w))/ci[c]      (FE:409-416, fp32 ops)
-    float s = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
-    sk.scores[tok] = s;
-  }
-  if (ep.median && sk.codes) {
-    if (lane_on) rowbits[g16 * kMaxP + j] = (uint16_t)bits;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int q = j; q < ep.ncb; q += 16) {
-      uint32_t code = 0;
-      for (int d = 0; d < ep.cb_dim; ++d) {
-        int e = q * ep.cb_dim + d;
-        uint32_t bit = (rowbits[g16 * kMaxP + e / P] >> (e % P)) & 1u;
-        code |= bit << (ep.cb_dim - 1 - d);
-      }
-      sk.codes[tok * ep.ncb + q] = (uint16_t)code;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // dense path: Y from workspace.  grid (ceil(Tmax/64), n_img), 256 threads:
 // each block handles 64 tokens (16 per pass, 4 passes).
 __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict__ imgs,
@@ -307,6 +213,7 @@ __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict
                                                        TokenSinks sk) {
   __shared__ uint16_t rowbits[16 * kMaxP];
   const ImgDesc d = imgs[blockIdx.y];
+  if (d.plan_h >= 0) return;  // columns of this image run through k_fft_cols (epilogue fused there)
   const int g16 = threadIdx.x >> 4, j = threadIdx.x & 15;
   const float* Y = ws + d.ws_y;
   for (int pass = 0; pass < 4; ++pass) {

@@ -26,4 +26,12 @@ void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float sc
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
 void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s);
 
+void fft_kernel_setup();
+void launch_fft_rows(const ImgDesc* imgs, const FftPlan* plans, const int2* blocks, int n_blocks, size_t lds,
+                     const float* rgb, float* ws, const float2* tabs, const ColorMats& cm, hipStream_t s);
+void launch_fft_cols(const ImgDesc* imgs, const FftPlan* plans, const int4* blocks, int n_blocks, size_t lds,
+                     const float* ws, const float2* tabs, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
+void launch_norm_thresholds(const float* med, const float* b, int64_t n, float eps, float lo, float hi, float* thr,
+                            int* bad, hipStream_t s);
+
 }  // namespace dctae

@@ -282,7 +282,7 @@ class DCTAutoencoderFeatureExtractor:
             ks = [self._k(h, w) for h, w in sizes]
         max_tok = self.max_patch_h * self.max_patch_w * self.channels
         plans = list(packing.iter_batch_plans([(ks, list(range(len(ks))))], self.max_seq_len, max_tok, batch_size))
-        norm = patchnorm.state() if patchnorm is not None else None
+        norm = patchnorm.state(thresholds=not return_patches) if patchnorm is not None else None
         lcfg = lfq.cfg() if lfq is not None else None
         if lfq is not None:
             if lfq.has_projections:
@@ -360,7 +360,7 @@ class BatchEncoder:
         self.k = k
         self.n_rows = self.plan.n_rows
         self.S = fe.max_seq_len
-        self.norm = patchnorm.state()
+        self.norm = patchnorm.state(thresholds=not want_patches)
         self.lcfg = lfq.cfg()
         self.p = fe.params()
         per = 3 * height * width

@@ -41,13 +41,24 @@ class PatchNorm(nn.Module):
         return FEParams(channels=self.channels, patch_size=self.patch_size, max_patch_h=self.max_patch_h,
                         max_patch_w=self.max_patch_w)
 
-    def state(self) -> NormState:
-        """Device view of the tables handed to the kernels."""
+    def state(self, thresholds: bool = False) -> NormState:
+        """Device view of the tables handed to the kernels.  With thresholds,
+        the exact LFQ-bit thresholds (one compare per element instead of a
+        subtract + divide + two table reads) are attached; they are cached
+        and rebuilt whenever median / b / eps / clamp change."""
         med = self.median.data
         b = self.b.data
         if med.dtype != torch.float32 or b.dtype != torch.float32:
             raise AssertionError("PatchNorm tables must be float32 on the MI355X path")
-        return NormState(med.contiguous(), b.contiguous(), float(self.eps), float(self.min_val), float(self.max_val))
+        st = NormState(med.contiguous(), b.contiguous(), float(self.eps), float(self.min_val), float(self.max_val))
+        if thresholds and med.is_cuda:
+            key = (med.data_ptr(), b.data_ptr(), med._version, b._version, st.eps, st.min_val, st.max_val)
+            cache = getattr(self, "_thr_cache", None)
+            if cache is None or cache[0] != key:
+                cache = (key, _ops.norm_thresholds(st))
+                self._thr_cache = cache
+            st.thr = cache[1]
+        return st
 
     def forward(self, dct_patches: DCTPatches) -> torch.Tensor:
         """patchnorm.py:81-165.  Training (and not frozen): update n / median /

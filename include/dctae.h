@@ -62,6 +62,9 @@ typedef struct {
   float eps;        /* 1e-6 */
   float min_val;    /* -6 */
   float max_val;    /*  6 */
+  /* optional (NULL): LFQ-bit thresholds from dctae_norm_thresholds; when
+   * set, codes-only encodes compare x >= thr instead of normalising */
+  const float* thr_dev;
 } dctae_norm;
 
 /* LFQ without projections (lfq.py:35-96): codebook_dim * num_codebooks must
@@ -173,6 +176,21 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
                  const int64_t* positions_dev, const int64_t* channels_dev, const dctae_norm* norm,
                  const dctae_lfq* lfq, const int64_t* codes_dev, const float* patches_dev,
                  float* rgb_dev, void* stream);
+
+/* thr[e] = the smallest fp32 x with PatchNorm(x)[e] > 0, for the n table
+ * elements (patchnorm.py:157-165 is monotone in x for a positive std), so
+ * that the LFQ bit of a token element is exactly (x >= thr[e]); NaN = never.
+ * Synchronises `stream`. */
+int dctae_norm_thresholds(dctae_ctx* ctx, const dctae_norm* norm, int64_t n, float* thr_dev,
+                          void* stream);
+
+/* Route lengths with an FFT plan through the FFT-DCT kernels (default 1);
+ * 0 forces the MFMA GEMM DCT for every size (A/B and parity testing). */
+int dctae_set_fft(dctae_ctx* ctx, int enable);
+
+/* Target workspace bytes per chunk of FFT-path images (default 160 MiB) so
+ * the row-pass output stays in the Infinity Cache for the column pass. */
+int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
 
 /* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an
  * out-of-range channel / position / image id (the reference raises

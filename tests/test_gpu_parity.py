@@ -242,8 +242,11 @@ def test_decode_reference_codes(pkg, fe, pn, lfq, case):
         if f"img{i}_decoded_rgb" not in g.files:
             continue
         ref = torch.from_numpy(g[f"img{i}_decoded_rgb"])
-        ok, dmax = _rgb_close(imgs[i].cpu(), ref, atol=1e-5, rtol=2e-5)
-        assert ok, (i, dmax)
+        # decoded LFQ images span a wide range (|rgb| up to ~8 after the
+        # 1/0.43 power): 1e-5 of the image's range, as for the round trip
+        scale = max(1.0, float(ref.abs().max()))
+        ok, dmax = _rgb_close(imgs[i].cpu(), ref, atol=1e-5 * scale, rtol=2e-5)
+        assert ok, (i, dmax, scale)
         checked += 1
     assert checked >= 1
 
@@ -295,3 +298,64 @@ def test_beta_sampling_matches_reference_k(pkg):
     for i, x in enumerate(rng.synth_images(m["img_seed"], [tuple(s) for s in m["sizes"]])):
         out = fe.preprocess(torch.from_numpy(x).to(DEV))
         assert out["patches"].shape[0] == int(g[f"img{i}_k"])
+
+
+def _ops():
+    from importlib import import_module
+    return import_module("dct_autoencoder_amd._ops")
+
+
+@pytest.mark.parametrize("shape", [(512, 512), (224, 224), (100, 300), (30, 700)])
+def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
+    """The FFT-DCT kernels and the MFMA GEMM DCT are two evaluations of the
+    same transform: tokens within 2e-6 * max|Y|, codes equal except inside the
+    guard band."""
+    ops = _ops()
+    x = torch.from_numpy(np.stack(rng.synth_images(31, [shape] * 2))).to(DEV)
+    ((dp_f, c_f),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_fft(False)
+    try:
+        ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    finally:
+        ops.set_fft(True)
+    rf, rg = dp_f.patches.cpu(), dp_g.patches.cpu()
+    kp = dp_f.key_pad_mask.cpu()
+    for r in range(kp.shape[0]):
+        gm = {_key(c, p): j for j, (p, c) in enumerate(zip(dp_g.patch_positions[r].tolist(), dp_g.patch_channels[r].tolist()))
+              if not kp[r, j]}
+        fm = [(j, _key(c, p)) for j, (p, c) in enumerate(zip(dp_f.patch_positions[r].tolist(), dp_f.patch_channels[r].tolist()))
+              if not kp[r, j]]
+        fj = torch.tensor([j for j, _ in fm])
+        gj = torch.tensor([gm[k] for _, k in fm])
+        ymax = rg[r, gj].abs().max().item()
+        d = (rf[r, fj] - rg[r, gj]).abs().max().item()
+        assert d <= 2e-6 * ymax, (d, ymax)
+        mism = (c_f.cpu()[r, fj] != c_g.cpu()[r, gj]).sum().item()
+        assert mism <= max(2, fj.numel() * 14 // 10000), mism
+
+
+def test_threshold_bits_equal_normalised_bits(fe, pn, lfq):
+    """codes from the exact thresholds (codes-only encode) == codes from the
+    PatchNorm values (encode with normalised patches), on identical DCT input."""
+    x = torch.from_numpy(np.stack(rng.synth_images(41, [(512, 512)] * 2))).to(DEV)
+    ((dp_a, c_a),) = fe.encode_batch(x, pn, lfq)
+    ((dp_b, c_b),) = fe.encode_batch(x, pn, lfq, return_patches=True)
+    assert torch.equal(c_a, c_b)
+    assert torch.equal(dp_a.patch_positions, dp_b.patch_positions)
+    # and the normalised patches reproduce the codes through the LFQ kernel
+    _, idx, _, _ = lfq(dp_b.patches, mask=~dp_b.key_pad_mask)
+    assert torch.equal(idx, c_b)
+
+
+def test_thresholds_are_exact(pn):
+    st = pn.state(thresholds=True)
+    thr = st.thr.cpu()
+    med, b = st.median.cpu(), st.b.cpu()
+    sd = b * 2 ** 0.5 + st.eps
+    ok = torch.isfinite(thr)
+    t = thr[ok]
+    # PatchNorm(thr) > 0 and PatchNorm(prev float below thr) <= 0
+    y_at = ((t - med[ok]) / sd[ok]).clamp(-6, 6)
+    below = torch.nextafter(t, torch.full_like(t, -float("inf")))
+    y_below = ((below - med[ok]) / sd[ok]).clamp(-6, 6)
+    assert torch.all(y_at > 0) and torch.all(y_below <= 0)
