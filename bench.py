@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -115,6 +116,9 @@ def main():
 
     B, H = args.batch, args.size
     x = ops.synth_images(B, H, H, seed=1234, first_index=rank * B, device=dev)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        ops.set_option(k, int(float(v)), dev)
     enc = fe_mod.BatchEncoder(fe, B, H, H, pn, lfq, device=dev)
     ctx = enc.ctx
     for _ in range(args.warmup):
@@ -213,6 +217,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": kernels,
+            "options": args.opt,
         }
         print(json.dumps(line))
     if dist:

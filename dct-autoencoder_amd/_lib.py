@@ -90,6 +90,7 @@ _SIGS = {
     "dctae_norm_thresholds": ([_P, C.POINTER(Norm), C.c_int64, _P, _P], C.c_int),
     "dctae_set_fft": ([_P, C.c_int], C.c_int),
     "dctae_set_chunk_bytes": ([_P, C.c_int64], C.c_int),
+    "dctae_set_option": ([_P, C.c_char_p, C.c_int64], C.c_int),
 }
 
 _lib = None

@@ -65,6 +65,11 @@ def set_fft(enable: bool, device=None):
     ctx.check(ctx.lib.dctae_set_fft(ctx.h, int(bool(enable))), "dctae_set_fft")
 
 
+def set_option(key: str, value: int, device=None):
+    ctx = _lib.context(device)
+    ctx.check(ctx.lib.dctae_set_option(ctx.h, key.encode(), int(value)), f"dctae_set_option({key})")
+
+
 def set_chunk_bytes(nbytes: int, device=None):
     ctx = _lib.context(device)
     ctx.check(ctx.lib.dctae_set_chunk_bytes(ctx.h, int(nbytes)), "dctae_set_chunk_bytes")

@@ -56,6 +56,8 @@ struct dctae_ctx {
   int64_t fft_tab_cap = 0, fft_tab_used = 0;
   std::map<int, FftPlan> fft_plans;   // N -> plan (N = 0 entries never stored)
   bool fft_enabled = true;
+  bool fft_spec_enabled = true;       // use the compile-time specialised kernels when a plan matches
+  size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 160ll << 20;  // workspace per chunk of the FFT path (MALL-resident T)
   // cached encode plan
   std::vector<int64_t> enc_key;
@@ -346,11 +348,14 @@ int next_pow2(int x) {
 }
 
 // FFT plan for length N (Makhoul: M = N/2 point complex FFT); -1 if N has no plan
-int fft_plan_for(dctae_ctx* ctx, int N, FftPlan* out) {
+int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   if (!ctx->fft_enabled || N < 4 || (N & 1) || N / 2 > 512) return -1;
+  if ((size_t)16 * (N / 2) * kMaxP > ctx->lds_limit) return -1;
   auto it = ctx->fft_plans.find(N);
   if (it != ctx->fft_plans.end()) {
     *out = it->second;
+    out->spec = ctx->fft_spec_enabled ? fft_spec_id(N, out->radix, out->npass, P) : 0;
+    if (out->spec) out->rows_per_block = fft_spec_rows_per_block(out->spec);
     return it->second.npass > 0 ? 0 : -1;
   }
   FftPlan p{};
@@ -410,16 +415,23 @@ int fft_plan_for(dctae_ctx* ctx, int N, FftPlan* out) {
   ctx->fft_tab_used += need;
   ctx->fft_plans[N] = p;
   *out = p;
+  out->spec = ctx->fft_spec_enabled ? fft_spec_id(N, out->radix, out->npass, P) : 0;
+  if (out->spec) out->rows_per_block = fft_spec_rows_per_block(out->spec);
   return 0;
 }
 
 }  // namespace
 
 // Encode plan: everything the launch sequence needs, cached on the inputs.
+constexpr int kVariants = 3;  // 0 = generic FFT kernels, 1.. = dctae_fft2.hip specialisations
+
 struct ChunkJob {
   int i0, i1;
-  size_t desc_off, gp_off, rows_t_off, cols_t_off, fr_off, fc_off;
-  int n_rows_tiles, n_cols_tiles, n_fr, n_fc;
+  size_t desc_off, gp_off, rows_t_off, cols_t_off;
+  size_t fr_off[kVariants], fc_off[kVariants];
+  int n_fr[kVariants], n_fc[kVariants];
+  int64_t tw_off[kVariants], post_off_r[kVariants], tw_off_c[kVariants], post_off_c[kVariants];
+  int n_rows_tiles, n_cols_tiles;
   int max_T, any_gemm_rows, any_gemm_cols;
   int64_t max_hw;
   size_t lds_rows, lds_cols;
@@ -429,6 +441,9 @@ struct EncPlan {
   uint64_t id = 0;
   PlanBuf pb;
   std::vector<ChunkJob> jobs;
+  size_t all_desc_off = 0;   // every image, global token offsets (sort_pack)
+  int n_img = 0, max_T = 1;
+  int64_t n_tok = 0;
   size_t rowlen_off = 0, plans_off = 0;
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
@@ -474,7 +489,7 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
     delete c;
     return DCTAE_EHIP;
   }
-  fft_kernel_setup();
+  c->lds_limit = fft_kernel_setup(device);
   hipEventRecord(c->plan_evt, 0);
   *out = c;
   return 0;
@@ -531,6 +546,17 @@ int dctae_set_fft(dctae_ctx* ctx, int enable) {
 int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes) {
   if (!ctx || bytes < (1 << 20)) return DCTAE_EINVAL;
   ctx->chunk_bytes = bytes;
+  return 0;
+}
+
+int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
+  if (!ctx || !key) return DCTAE_EINVAL;
+  const std::string k(key);
+  if (k == "fft") ctx->fft_enabled = value != 0;
+  else if (k == "fft_spec") ctx->fft_spec_enabled = value != 0;
+  else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
+  else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
+  else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
 
@@ -636,7 +662,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     if (it != plan_idx.end()) return it->second;
     FftPlan p;
     int idx = -1;
-    if (fft_plan_for(ctx, N, &p) == 0) {
+    if (fft_plan_for(ctx, N, P, &p) == 0) {
       idx = (int)plans.size();
       plans.push_back(p);
     }
@@ -690,8 +716,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   }
   const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
   std::vector<GemmProblem> probs;
+  int64_t tok = 0;
   for (auto& j : E.jobs) {
-    int64_t wsf = 0, tok = 0;
+    int64_t wsf = 0;
     j.max_T = 1;
     j.max_hw = 1;
     for (int i = j.i0; i < j.i1; ++i) {
@@ -708,9 +735,14 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
     E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
+    E.max_T = std::max(E.max_T, j.max_T);
+  }
+  E.n_tok = tok;
+  E.n_img = n;
+  {
     int64_t st = 0;
-    for (int i = j.i0; i < j.i1; ++i) st += st_of(D[i]);
-    E.st_need = std::max<size_t>(E.st_need, (size_t)st + 4096);
+    for (int i = 0; i < n; ++i) st += st_of(D[i]);
+    E.st_need = (size_t)st + 4096;
   }
   if ((rc = ensure_ws(ctx, std::max<size_t>(E.ws_need, 256), std::max<size_t>(E.st_need, 256)))) return rc;
   float* ws = ctx->ws;
@@ -718,8 +750,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     j.desc_off = E.pb.add(D.data() + j.i0, j.i1 - j.i0);
     const size_t p0 = probs.size();
     std::vector<TileRef> rt, ct;
-    std::vector<int2> fr;
-    std::vector<int4> fc;
+    std::vector<int2> fr[kVariants];
+    std::vector<int4> fc[kVariants];
     j.lds_rows = j.lds_cols = 0;
     for (int i = j.i0; i < j.i1; ++i) {
       const ImgDesc& d = D[i];
@@ -735,8 +767,13 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         j.any_gemm_rows = 1;
       } else {
         const FftPlan& p = plans[d.plan_w];
-        for (int y0 = 0; y0 < d.H; y0 += p.rows_per_block) fr.push_back(make_int2(li, y0));
-        j.lds_rows = std::max<size_t>(j.lds_rows, (size_t)2 * p.rows_per_block * 3 * (2 * p.M + 1) * 4);
+        for (int y0 = 0; y0 < d.H; y0 += p.rows_per_block) fr[p.spec].push_back(make_int2(li, y0));
+        if (p.spec) {
+          j.tw_off[p.spec] = p.tw_off;
+          j.post_off_r[p.spec] = p.post_off;
+        } else {
+          j.lds_rows = std::max<size_t>(j.lds_rows, (size_t)2 * p.rows_per_block * 3 * (2 * p.M + 1) * 4);
+        }
       }
       if (d.plan_h < 0) {
         const float* CH;
@@ -750,21 +787,29 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       } else {
         const FftPlan& p = plans[d.plan_h];
         for (int c = 0; c < 3; ++c)
-          for (int w = 0; w < d.qw; ++w) fc.push_back(make_int4(li, c, w, 0));
-        j.lds_cols = std::max<size_t>(j.lds_cols, (size_t)2 * 2 * p.M * P * 4);
+          for (int w = 0; w < d.qw; ++w) fc[p.spec].push_back(make_int4(li, c, w, 0));
+        if (p.spec) {
+          j.tw_off_c[p.spec] = p.tw_off;
+          j.post_off_c[p.spec] = p.post_off;
+        } else {
+          j.lds_cols = std::max<size_t>(j.lds_cols, (size_t)2 * 2 * p.M * P * 4);
+        }
       }
     }
     j.gp_off = E.pb.add(probs.data() + p0, probs.size() - p0);
     j.rows_t_off = E.pb.add(rt.data(), rt.size());
     j.cols_t_off = E.pb.add(ct.data(), ct.size());
-    j.fr_off = E.pb.add(fr.data(), fr.size());
-    j.fc_off = E.pb.add(fc.data(), fc.size());
+    for (int v = 0; v < kVariants; ++v) {
+      j.fr_off[v] = E.pb.add(fr[v].data(), fr[v].size());
+      j.fc_off[v] = E.pb.add(fc[v].data(), fc[v].size());
+      j.n_fr[v] = (int)fr[v].size();
+      j.n_fc[v] = (int)fc[v].size();
+    }
     j.n_rows_tiles = (int)rt.size();
     j.n_cols_tiles = (int)ct.size();
-    j.n_fr = (int)fr.size();
-    j.n_fc = (int)fc.size();
   }
   E.plans_off = E.pb.add(plans.data(), plans.size());
+  E.all_desc_off = E.pb.add(D.data(), D.size());
   if (full && pack->n_rows > 0) E.rowlen_off = E.pb.add(pack->row_len, pack->n_rows);
   E.ncb = ncb;
   return 0;
@@ -801,7 +846,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
-                         (int64_t)ctx->fft_enabled, (int64_t)(intptr_t)ctx->ws});
+                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled,
+                         (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
     key.push_back(((int64_t)imgs->hw[2 * i] << 32) | (uint32_t)imgs->hw[2 * i + 1]);
@@ -852,36 +898,34 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       launch_pad_fill((const int32_t*)(pd + E.rowlen_off), pack->n_rows, ep, out->key_pad_dev, ps, s);
     }
   }
+  // token staging for the whole call (flat token order, global offsets)
+  TokenSinks sk{};
+  if (full) {
+    const int64_t nt = E.n_tok;
+    uint8_t* st = ctx->stage;
+    sk.scores = (float*)st;
+    st += ((nt * 4 + 255) & ~255ll);
+    if (ncb) {
+      sk.codes = (uint16_t*)st;
+      st += ((nt * 2 * ncb + 255) & ~255ll);
+    }
+    if (want_norm) {
+      sk.norm = (float*)st;
+      st += nt * 4 * PP;
+    }
+    if (out->raw_patches_dev) {
+      sk.raw = (float*)st;
+      st += nt * 4 * PP;
+    }
+  } else {
+    sk.scores = scores_dev;
+    sk.raw = tokens_dev;
+  }
+  EncParams epj = ep;
+  if (!full) epj.median = nullptr;
   for (auto& j : E.jobs) {
     const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
-    TokenSinks sk{};
-    if (full) {
-      int64_t nt = 0;
-      // tokens of the chunk: recompute from the plan's host copy
-      const ImgDesc* hdesc = (const ImgDesc*)(E.pb.bytes.data() + j.desc_off);
-      for (int i = 0; i < nj; ++i) nt += hdesc[i].T;
-      uint8_t* st = ctx->stage;
-      sk.scores = (float*)st;
-      st += ((nt * 4 + 255) & ~255ll);
-      if (ncb) {
-        sk.codes = (uint16_t*)st;
-        st += ((nt * 2 * ncb + 255) & ~255ll);
-      }
-      if (want_norm) {
-        sk.norm = (float*)st;
-        st += nt * 4 * PP;
-      }
-      if (out->raw_patches_dev) {
-        sk.raw = (float*)st;
-        st += nt * 4 * PP;
-      }
-    } else {
-      sk.scores = scores_dev;
-      sk.raw = tokens_dev;
-    }
-    EncParams epj = ep;
-    if (!full) epj.median = nullptr;
     if (j.any_gemm_rows) {
       {
         Timer t(ctx, s, "rgb_to_ipt");
@@ -890,11 +934,17 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       Timer t(ctx, s, "gemm_rows");
       launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, s);
     }
-    if (j.n_fr) {
+    if (j.n_fr[0]) {
       Timer t(ctx, s, "fft_rows");
-      launch_fft_rows(dd, plans_d, (const int2*)(pd + j.fr_off), j.n_fr, j.lds_rows, imgs->rgb_dev, ctx->ws,
+      launch_fft_rows(dd, plans_d, (const int2*)(pd + j.fr_off[0]), j.n_fr[0], j.lds_rows, imgs->rgb_dev, ctx->ws,
                       ctx->fft_tab, ctx->cm, s);
     }
+    for (int v = 1; v < kVariants; ++v)
+      if (j.n_fr[v]) {
+        Timer t(ctx, s, "fft_rows");
+        launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
+                             ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, s);
+      }
     if (j.any_gemm_cols) {
       {
         Timer t(ctx, s, "gemm_cols");
@@ -903,14 +953,21 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       Timer t(ctx, s, "tile_epilogue");
       launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, s);
     }
-    if (j.n_fc) {
+    if (j.n_fc[0]) {
       Timer t(ctx, s, "fft_cols");
-      launch_fft_cols(dd, plans_d, (const int4*)(pd + j.fc_off), j.n_fc, j.lds_cols, ctx->ws, ctx->fft_tab, epj, sk, s);
+      launch_fft_cols(dd, plans_d, (const int4*)(pd + j.fc_off[0]), j.n_fc[0], j.lds_cols, ctx->ws, ctx->fft_tab,
+                      epj, sk, s);
     }
-    if (full) {
-      Timer t(ctx, s, "sort_pack");
-      launch_sort_pack(dd, nj, next_pow2(j.max_T), ep, sk, ps, s);
-    }
+    for (int v = 1; v < kVariants; ++v)
+      if (j.n_fc[v]) {
+        Timer t(ctx, s, "fft_cols");
+        launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
+                             ctx->fft_tab + j.post_off_c[v], epj, sk, s);
+      }
+  }
+  if (full && E.n_img > 0) {
+    Timer t(ctx, s, "sort_pack");
+    launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), ep, sk, ps, s);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);

@@ -18,6 +18,14 @@ __device__ __forceinline__ float signed_pow(float x, float p) {
   return x < 0.0f ? -y : y;
 }
 
+// |x|^p through the hardware log2/exp2 (v_log_f32 / v_exp_f32, ~2 ulp):
+// the encode colour transform is compared with a tolerance (SURVEY §7 hard
+// part 7), and generic powf costs ~10x the instructions.
+__device__ __forceinline__ float signed_pow_fast(float x, float p) {
+  const float y = __builtin_amdgcn_exp2f(p * __builtin_amdgcn_logf(fabsf(x)));
+  return x < 0.0f ? -y : y;
+}
+
 // NaN-propagating max (torch.amax semantics)
 __device__ __forceinline__ float nanmax(float a, float b) {
   return (a != a || a > b) ? a : ((b != b) ? b : (a > b ? a : b));

@@ -1,0 +1,250 @@
+// Compile-time specialised two-pass FFT-DCT kernels (M = N/2 = R1 * R2,
+// at most 64/3 butterflies per job and pass) for the headline image sizes:
+//   N = 512: M = 256 = 16 x 16        N = 224: M = 112 = 16 x 7
+// Same maths as dctae_fft.hip (Makhoul + Stockham), but every index is a
+// compile-time expression, passes are done in place (register staged), and
+// the row kernel gives each image row to one wave (no block barriers).
+#include "dctae_device.h"
+#include "dctae_fft_common.h"
+#include "dctae_launch.h"
+
+namespace dctae {
+
+// padded complex slot of element m: one spare slot every 16 keeps the
+// stride-16 Stockham accesses on distinct LDS banks
+__device__ __forceinline__ constexpr int pad16(int m) { return m + (m >> 4); }
+
+// ---------------------------------------------------------------------------
+// rows: one wave = one image row, its 3 IPT channels are 3 jobs
+// ---------------------------------------------------------------------------
+template <int N, int R1, int R2>
+__global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                                                   const float* __restrict__ rgb, float* __restrict__ ws,
+                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                   ColorMats cm) {
+  constexpr int M = N / 2;
+  constexpr int MP = pad16(M - 1) + 2;
+  constexpr int B1 = M / R1, B2 = M / R2;
+  static_assert(R1 * R2 == M, "two-pass plan");
+  static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
+  static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
+  __shared__ float2 zs[4][3][MP];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const int y = jb.y + wave;
+  if (y >= d.H) return;
+  float2(*z)[MP] = zs[wave];
+  float* zf0 = reinterpret_cast<float*>(z[0]);
+  float* zf1 = reinterpret_cast<float*>(z[1]);
+  float* zf2 = reinterpret_cast<float*>(z[2]);
+  // ---- load, IPT (util.py:70-82), Makhoul reorder
+  const int64_t hw = (int64_t)d.H * N;
+  const float* src = rgb + d.rgb_off + (int64_t)y * N;
+  const float gam = 0.430000007152557373046875f;
+#pragma unroll
+  for (int i = 0; i < (N + 63) / 64; ++i) {
+    const int px = lane + 64 * i;
+    if (px < N) {
+      const float R_ = src[px], G_ = src[hw + px], B_ = src[2 * hw + px];
+      const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, R_, G_, B_), gam);
+      const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, R_, G_, B_), gam);
+      const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, R_, G_, B_), gam);
+      const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
+      const int o = 2 * pad16(v >> 1) + (v & 1);
+      zf0[o] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
+      zf1[o] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
+      zf2[o] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+    }
+  }
+  // ---- pass 1: radix R1, Ns = 1 (no twiddles); in place, one butterfly per lane
+  if (lane < 3 * B1) {
+    const int c = lane / B1, j = lane - c * B1;
+    float2 v[R1];
+#pragma unroll
+    for (int r = 0; r < R1; ++r) v[r] = z[c][pad16(j + r * B1)];
+    DFT<R1>::run(v);
+#pragma unroll
+    for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = v[r];
+  }
+  // ---- pass 2: radix R2, Ns = R1; twiddle W_M^{r*j}
+  if (lane < 3 * B2) {
+    const int c = lane / B2, j = lane - c * B2;  // j < B2 = R1 = Ns
+    float2 v[R2];
+#pragma unroll
+    for (int r = 0; r < R2; ++r) v[r] = z[c][pad16(j + r * B2)];
+#pragma unroll
+    for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw[r * j]);
+    DFT<R2>::run(v);
+#pragma unroll
+    for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
+  }
+  // ---- Makhoul post-processing, write T[c][y][kx] for kx < Kw
+  const int Kw = d.Kw;
+  constexpr int NI = 3 * (M + 1);
+#pragma unroll 2
+  for (int it = lane; it < NI; it += 64) {
+    const int c = it / (M + 1), k = it - c * (M + 1);
+    const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
+    const float2 A = z[c][pad16(ka)];
+    float2 B = z[c][pad16(kb)];
+    B.y = -B.y;
+    const float2 al = post[2 * k], be = post[2 * k + 1];
+    const float2 W = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+    float* trow = ws + d.ws_t + ((int64_t)c * d.H + y) * Kw;
+    if (k < Kw) trow[k] = W.x;
+    if (k >= 1 && k < M && N - k < Kw) trow[N - k] = -W.y;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cols: one block = (image, channel, tile column); KS = P columns of T
+// ---------------------------------------------------------------------------
+template <int N, int R1, int R2, int KS>
+__global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+  constexpr int M = N / 2;
+  constexpr int B1 = M / R1, B2 = M / R2;
+  static_assert(KS * B1 <= 256 && KS * B2 <= 256, "one butterfly per thread per pass");
+  static_assert(R1 == 16, "first radix 16");
+  // complex m of column j: re at (2m)*KS + j, im at (2m+1)*KS + j; reused as X[ky][j]
+  __shared__ float zs[2 * M * KS];
+  __shared__ uint16_t rowbits[16 * kMaxP];
+  const int tid = threadIdx.x;
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const int c = jb.y, strip = jb.z;
+  const float* T = ws + d.ws_t + (int64_t)c * d.H * d.Kw + strip * KS;
+  const int Kw = d.Kw;
+#pragma unroll 4
+  for (int e = tid; e < N * KS; e += 256) {
+    const int y = e / KS, j = e - y * KS;
+    const int v = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
+    zs[v * KS + j] = T[(int64_t)y * Kw + j];
+  }
+  __syncthreads();
+  // ---- pass 1 (Ns = 1)
+  {
+    float2 v[R1];
+    const bool on = tid < KS * B1;
+    const int col = tid % KS, j = tid / KS;
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        const int m = j + r * B1;
+        v[r] = make_float2(zs[(2 * m) * KS + col], zs[(2 * m + 1) * KS + col]);
+      }
+      DFT<R1>::run(v);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        const int m = j * R1 + r;
+        zs[(2 * m) * KS + col] = v[r].x;
+        zs[(2 * m + 1) * KS + col] = v[r].y;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- pass 2 (Ns = R1)
+  {
+    float2 v[R2];
+    const bool on = tid < KS * B2;
+    const int col = tid % KS, j = tid / KS;
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R2; ++r) {
+        const int m = j + r * B2;
+        v[r] = make_float2(zs[(2 * m) * KS + col], zs[(2 * m + 1) * KS + col]);
+      }
+#pragma unroll
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw[r * j]);
+      DFT<R2>::run(v);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R2; ++r) {
+        const int m = j + r * R1;
+        zs[(2 * m) * KS + col] = v[r].x;
+        zs[(2 * m + 1) * KS + col] = v[r].y;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- Makhoul post-processing into registers, then X[ky][j] in place
+  constexpr int NI = (M + 1) * KS;
+  constexpr int PER = (NI + 255) / 256;
+  float2 wv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int it = tid + 256 * i;
+    if (it < NI) {
+      const int k = it / KS, col = it - k * KS;
+      const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
+      const float2 A = make_float2(zs[(2 * ka) * KS + col], zs[(2 * ka + 1) * KS + col]);
+      const float2 B = make_float2(zs[(2 * kb) * KS + col], -zs[(2 * kb + 1) * KS + col]);
+      const float2 al = post[2 * k], be = post[2 * k + 1];
+      wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+    }
+  }
+  __syncthreads();
+  const int Kh = d.Kh;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int it = tid + 256 * i;
+    if (it < NI) {
+      const int k = it / KS, col = it - k * KS;
+      if (k < Kh) zs[k * KS + col] = wv[i].x;
+      if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KS + col] = -wv[i].y;
+    }
+  }
+  __syncthreads();
+  // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
+  const int g16 = tid >> 4, jl = tid & 15;
+  for (int h = g16; h < d.qh; h += 16) {
+    float vals[kMaxP];
+    if (jl < KS) {
+#pragma unroll
+      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = zs[(KS * h + jl) * KS + p2];
+    }
+    const int f = (h * d.qw + strip) * ep.C + c;
+    token_epilogue(ep, c, h, strip, jl, g16, vals, d.tok_off + f, sk, rowbits);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dispatch
+// ---------------------------------------------------------------------------
+
+int fft_spec_id(int N, const int* radix, int npass, int P) {
+  if (P != 14 || npass != 2) return 0;
+  if (N == 512 && radix[0] == 16 && radix[1] == 16) return 1;
+  if (N == 224 && radix[0] == 16 && radix[1] == 7) return 2;
+  return 0;
+}
+
+int fft_spec_rows_per_block(int spec) { return spec ? 4 : 0; }
+
+void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
+                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s) {
+  if (n_blocks <= 0) return;
+  if (spec == 1)
+    hipLaunchKernelGGL((k_fft_rows2<512, 16, 16>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+  else if (spec == 2)
+    hipLaunchKernelGGL((k_fft_rows2<224, 16, 7>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+}
+
+void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
+                          const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
+                          hipStream_t s) {
+  if (n_blocks <= 0) return;
+  if (spec == 1)
+    hipLaunchKernelGGL((k_fft_cols2<512, 16, 16, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
+  else if (spec == 2)
+    hipLaunchKernelGGL((k_fft_cols2<224, 16, 7, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
+}
+
+}  // namespace dctae

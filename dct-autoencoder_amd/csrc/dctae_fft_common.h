@@ -1,0 +1,151 @@
+// FFT codelets shared by dctae_fft.hip (generic plans) and dctae_fft2.hip
+// (compile-time specialised plans): forward DFTs of size 2, 3, 4, 5, 7, 8, 16
+// on float2 registers, natural order in and out.
+#pragma once
+#include "dctae_device.h"
+
+namespace dctae {
+
+__device__ constexpr float kCos3[3] = {1.0f, -0.5f, -0.5f};
+__device__ constexpr float kSin3[3] = {0.0f, 8.660254038e-01f, -8.660254038e-01f};
+__device__ constexpr float kCos5[5] = {1.0f, 3.090169944e-01f, -8.090169944e-01f, -8.090169944e-01f, 3.090169944e-01f};
+__device__ constexpr float kSin5[5] = {0.0f, 9.510565163e-01f, 5.877852523e-01f, -5.877852523e-01f, -9.510565163e-01f};
+__device__ constexpr float kCos7[7] = {1.0f, 6.234898019e-01f, -2.225209340e-01f, -9.009688679e-01f,
+                                       -9.009688679e-01f, -2.225209340e-01f, 6.234898019e-01f};
+__device__ constexpr float kSin7[7] = {0.0f, 7.818314825e-01f, 9.749279122e-01f, 4.338837391e-01f,
+                                       -4.338837391e-01f, -9.749279122e-01f, -7.818314825e-01f};
+__device__ constexpr float kCos16[16] = {1.0f, 9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f,
+                                         -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f,
+                                         -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f, 0.0f,
+                                         3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f};
+__device__ constexpr float kSin16[16] = {0.0f, 3.826834324e-01f, 7.071067812e-01f, 9.238795325e-01f, 1.0f,
+                                         9.238795325e-01f, 7.071067812e-01f, 3.826834324e-01f, 0.0f,
+                                         -3.826834324e-01f, -7.071067812e-01f, -9.238795325e-01f, -1.0f,
+                                         -9.238795325e-01f, -7.071067812e-01f, -3.826834324e-01f};
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // -i * a
+
+// forward DFT codelets, natural order in and out: V[k] = sum_n v[n] e^{-2 pi i nk/R}
+template <int R>
+struct DFT;
+
+template <>
+struct DFT<2> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 a = v[0], b = v[1];
+    v[0] = cadd(a, b);
+    v[1] = csub(a, b);
+  }
+};
+
+template <>
+struct DFT<4> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    float2 t2 = cadd(v[1], v[3]), t3 = mul_mi(csub(v[1], v[3]));
+    v[0] = cadd(t0, t2);
+    v[2] = csub(t0, t2);
+    v[1] = cadd(t1, t3);
+    v[3] = csub(t1, t3);
+  }
+};
+
+template <>
+struct DFT<8> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 e[4] = {v[0], v[2], v[4], v[6]};
+    float2 o[4] = {v[1], v[3], v[5], v[7]};
+    DFT<4>::run(e);
+    DFT<4>::run(o);
+    const float c = 7.071067812e-01f;
+    float2 w1 = make_float2(c * (o[1].x + o[1].y), c * (o[1].y - o[1].x));    // o1 * (c - ic)
+    float2 w2 = mul_mi(o[2]);                                                  // o2 * -i
+    float2 w3 = make_float2(c * (o[3].y - o[3].x), -c * (o[3].x + o[3].y));   // o3 * (-c - ic)
+    v[0] = cadd(e[0], o[0]);
+    v[4] = csub(e[0], o[0]);
+    v[1] = cadd(e[1], w1);
+    v[5] = csub(e[1], w1);
+    v[2] = cadd(e[2], w2);
+    v[6] = csub(e[2], w2);
+    v[3] = cadd(e[3], w3);
+    v[7] = csub(e[3], w3);
+  }
+};
+
+template <>
+struct DFT<16> {
+  static __device__ __forceinline__ void run(float2* v) {
+    float2 a[4][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+      for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
+      DFT<4>::run(a[n2]);
+    }
+#pragma unroll
+    for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+      for (int k1 = 1; k1 < 4; ++k1) {
+        const int m = n2 * k1;
+        a[n2][k1] = cmul(a[n2][k1], make_float2(kCos16[m], -kSin16[m]));
+      }
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      float2 b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+      DFT<4>::run(b);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+    }
+  }
+};
+
+template <int R>
+__device__ __forceinline__ void dft_odd(float2* v, const float* C, const float* S) {
+  constexpr int H = (R - 1) / 2;
+  float2 s[H], d[H];
+  float2 x0 = v[0], sum = v[0];
+#pragma unroll
+  for (int n = 1; n <= H; ++n) {
+    s[n - 1] = cadd(v[n], v[R - n]);
+    d[n - 1] = csub(v[n], v[R - n]);
+    sum = cadd(sum, s[n - 1]);
+  }
+  float2 out[R];
+  out[0] = sum;
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
+    float re = x0.x, im = x0.y, re2 = 0.0f, im2 = 0.0f;
+#pragma unroll
+    for (int n = 1; n <= H; ++n) {
+      const int m = (n * k) % R;
+      re = fmaf(s[n - 1].x, C[m], re);
+      im = fmaf(s[n - 1].y, C[m], im);
+      re2 = fmaf(d[n - 1].y, S[m], re2);
+      im2 = fmaf(d[n - 1].x, S[m], im2);
+    }
+    out[k] = make_float2(re + re2, im - im2);
+    out[R - k] = make_float2(re - re2, im + im2);
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = out[k];
+}
+
+template <>
+struct DFT<3> {
+  static __device__ __forceinline__ void run(float2* v) { dft_odd<3>(v, kCos3, kSin3); }
+};
+template <>
+struct DFT<5> {
+  static __device__ __forceinline__ void run(float2* v) { dft_odd<5>(v, kCos5, kSin5); }
+};
+template <>
+struct DFT<7> {
+  static __device__ __forceinline__ void run(float2* v) { dft_odd<7>(v, kCos7, kSin7); }
+};
+
+}  // namespace dctae

@@ -50,6 +50,7 @@ struct GemmProblem {
 struct FftPlan {
   int32_t N, M, npass, rows_per_block;
   int32_t radix[8];
+  int32_t spec, spec_pad;  // compile-time specialised kernel id (dctae_fft2.hip), 0 = generic
   int64_t tw_off;    // float2 offset of W_M^k (k < M) in the FFT table buffer
   int64_t post_off;  // float2 offset of (alpha_k, beta_k), k = 0..M
 };

@@ -50,9 +50,9 @@ __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __re
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hw;
        e += (int64_t)gridDim.x * blockDim.x) {
     float r = src[e], g = src[hw + e], b = src[2 * hw + e];
-    float l0 = signed_pow(mat3_row(cm.rgb2lms, 0, r, g, b), 0.430000007152557373046875f);
-    float l1 = signed_pow(mat3_row(cm.rgb2lms, 1, r, g, b), 0.430000007152557373046875f);
-    float l2 = signed_pow(mat3_row(cm.rgb2lms, 2, r, g, b), 0.430000007152557373046875f);
+    float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), 0.430000007152557373046875f);
+    float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), 0.430000007152557373046875f);
+    float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), 0.430000007152557373046875f);
     dst[e] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
     dst[hw + e] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
     dst[2 * hw + e] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);

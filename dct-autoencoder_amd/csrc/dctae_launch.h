@@ -26,12 +26,20 @@ void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float sc
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
 void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s);
 
-void fft_kernel_setup();
+size_t fft_kernel_setup(int device);
 void launch_fft_rows(const ImgDesc* imgs, const FftPlan* plans, const int2* blocks, int n_blocks, size_t lds,
                      const float* rgb, float* ws, const float2* tabs, const ColorMats& cm, hipStream_t s);
 void launch_fft_cols(const ImgDesc* imgs, const FftPlan* plans, const int4* blocks, int n_blocks, size_t lds,
                      const float* ws, const float2* tabs, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
 void launch_norm_thresholds(const float* med, const float* b, int64_t n, float eps, float lo, float hi, float* thr,
                             int* bad, hipStream_t s);
+
+int fft_spec_id(int N, const int* radix, int npass, int P);
+int fft_spec_rows_per_block(int spec);
+void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
+                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s);
+void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
+                          const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
+                          hipStream_t s);
 
 }  // namespace dctae

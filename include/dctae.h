@@ -192,6 +192,10 @@ int dctae_set_fft(dctae_ctx* ctx, int enable);
  * the row-pass output stays in the Infinity Cache for the column pass. */
 int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
 
+/* Tuning / test knobs: "fft" (0/1), "fft_spec" (0/1: compile-time
+ * specialised FFT kernels), "chunk_bytes", "workspace_limit" (bytes). */
+int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
+
 /* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an
  * out-of-range channel / position / image id (the reference raises
  * IndexError there).  Synchronises `stream`. */

@@ -321,10 +321,11 @@ def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
     rf, rg = dp_f.patches.cpu(), dp_g.patches.cpu()
     kp = dp_f.key_pad_mask.cpu()
     for r in range(kp.shape[0]):
-        gm = {_key(c, p): j for j, (p, c) in enumerate(zip(dp_g.patch_positions[r].tolist(), dp_g.patch_channels[r].tolist()))
-              if not kp[r, j]}
-        fm = [(j, _key(c, p)) for j, (p, c) in enumerate(zip(dp_f.patch_positions[r].tolist(), dp_f.patch_channels[r].tolist()))
-              if not kp[r, j]]
+        ids_g, ids_f = dp_g.batched_image_ids[r].tolist(), dp_f.batched_image_ids[r].tolist()
+        gm = {(ids_g[j],) + _key(c, p): j for j, (p, c) in
+              enumerate(zip(dp_g.patch_positions[r].tolist(), dp_g.patch_channels[r].tolist())) if not kp[r, j]}
+        fm = [(j, (ids_f[j],) + _key(c, p)) for j, (p, c) in
+              enumerate(zip(dp_f.patch_positions[r].tolist(), dp_f.patch_channels[r].tolist())) if not kp[r, j]]
         fj = torch.tensor([j for j, _ in fm])
         gj = torch.tensor([gm[k] for _, k in fm])
         ymax = rg[r, gj].abs().max().item()
@@ -359,3 +360,28 @@ def test_thresholds_are_exact(pn):
     below = torch.nextafter(t, torch.full_like(t, -float("inf")))
     y_below = ((below - med[ok]) / sd[ok]).clamp(-6, 6)
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
+
+
+@pytest.mark.parametrize("shape", [(512, 512), (224, 224)])
+def test_specialised_kernels_match_generic(fe, pn, lfq, shape):
+    """dctae_fft2.hip (compile-time plans) vs dctae_fft.hip (runtime plans):
+    same algorithm, different op order -> tokens within 1e-6 * max|Y|."""
+    ops = _ops()
+    x = torch.from_numpy(np.stack(rng.synth_images(53, [shape] * 3))).to(DEV)
+    ((dp_s, c_s),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
+    ops.set_option("fft_spec", 0)
+    try:
+        ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
+    finally:
+        ops.set_option("fft_spec", 1)
+    kp = dp_s.key_pad_mask.cpu()
+    ids_s, ids_g = dp_s.batched_image_ids.cpu(), dp_g.batched_image_ids.cpu()
+    for r in range(kp.shape[0]):
+        gm = {(int(ids_g[r, j]),) + _key(c, p): j for j, (p, c) in
+              enumerate(zip(dp_g.patch_positions[r].tolist(), dp_g.patch_channels[r].tolist())) if not kp[r, j]}
+        pairs = [(j, gm[(int(ids_s[r, j]),) + _key(c, p)]) for j, (p, c) in
+                 enumerate(zip(dp_s.patch_positions[r].tolist(), dp_s.patch_channels[r].tolist())) if not kp[r, j]]
+        sj = torch.tensor([a for a, _ in pairs]); gj = torch.tensor([b for _, b in pairs])
+        a, b = dp_s.patches.cpu()[r, sj], dp_g.patches.cpu()[r, gj]
+        assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item()
+        assert (c_s.cpu()[r, sj] != c_g.cpu()[r, gj]).sum().item() <= 4
