@@ -684,6 +684,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     }
     D[i].plan_w = plan_of(D[i].W);
     D[i].plan_h = plan_of(D[i].H);
+    // strip-major T when both passes run on the specialised kernels
+    D[i].t_strips = (P == 14 && D[i].plan_w >= 0 && D[i].plan_h >= 0 && plans[D[i].plan_w].spec &&
+                     plans[D[i].plan_h].spec) ? 1 : 0;
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
@@ -691,9 +694,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   // chunks: FFT images are grouped so the intermediate T of a chunk stays in
   // the 256 MiB Infinity Cache between the row and column kernels
   auto ws_of = [&](const ImgDesc& d) {
-    int64_t w = 3ll * d.Kw * d.H;
-    if (d.plan_w < 0) w += 3ll * d.H * d.W;
-    if (d.plan_h < 0) w += 3ll * d.Kh * d.Kw;
+    int64_t w = 3ll * d.Kw * d.H + 64;
+    if (d.plan_w < 0) w += 3ll * d.H * d.W + 64;
+    if (d.plan_h < 0) w += 3ll * d.Kh * d.Kw + 64;
     return w * 4;
   };
   auto st_of = [&](const ImgDesc& d) {
@@ -721,14 +724,15 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     int64_t wsf = 0;
     j.max_T = 1;
     j.max_hw = 1;
+    auto up = [](int64_t v) { return (v + 63) & ~63ll; };  // 256-byte aligned regions (float4 strip loads)
     for (int i = j.i0; i < j.i1; ++i) {
       ImgDesc& d = D[i];
       d.ws_t = wsf;
-      wsf += 3ll * d.Kw * d.H;
+      wsf += up(3ll * d.Kw * d.H);
       d.ws_p = wsf;
-      if (d.plan_w < 0) wsf += 3ll * d.H * d.W;
+      if (d.plan_w < 0) wsf += up(3ll * d.H * d.W);
       d.ws_y = wsf;
-      if (d.plan_h < 0) wsf += 3ll * d.Kh * d.Kw;
+      if (d.plan_h < 0) wsf += up(3ll * d.Kh * d.Kw);
       d.tok_off = full ? tok : tok_off_user[i];
       tok += d.T;
       j.max_T = std::max(j.max_T, d.T);

@@ -25,6 +25,8 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   constexpr int M = N / 2;
   constexpr int MP = pad16(M - 1) + 2;
   constexpr int B1 = M / R1, B2 = M / R2;
+  constexpr int PX = (N + 63) / 64;        // pixels per lane and row
+  constexpr int RPW = 4;                   // rows per wave (block = 16 rows)
   static_assert(R1 * R2 == M, "two-pass plan");
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
@@ -32,68 +34,97 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int2 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
-  const int y = jb.y + wave;
-  if (y >= d.H) return;
   float2(*z)[MP] = zs[wave];
   float* zf0 = reinterpret_cast<float*>(z[0]);
   float* zf1 = reinterpret_cast<float*>(z[1]);
   float* zf2 = reinterpret_cast<float*>(z[2]);
-  // ---- load, IPT (util.py:70-82), Makhoul reorder
   const int64_t hw = (int64_t)d.H * N;
-  const float* src = rgb + d.rgb_off + (int64_t)y * N;
+  const float* src = rgb + d.rgb_off;
   const float gam = 0.430000007152557373046875f;
+  const int Kw = d.Kw, H = d.H;
+  float* T = ws + d.ws_t;
+  // rows of this wave: y0 + wave + 4*rr
+  float pr[PX], pg[PX], pb[PX];
+  auto fetch = [&](int y) {
 #pragma unroll
-  for (int i = 0; i < (N + 63) / 64; ++i) {
-    const int px = lane + 64 * i;
-    if (px < N) {
-      const float R_ = src[px], G_ = src[hw + px], B_ = src[2 * hw + px];
-      const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, R_, G_, B_), gam);
-      const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, R_, G_, B_), gam);
-      const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, R_, G_, B_), gam);
-      const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
-      const int o = 2 * pad16(v >> 1) + (v & 1);
-      zf0[o] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
-      zf1[o] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
-      zf2[o] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+    for (int i = 0; i < PX; ++i) {
+      const int px = lane + 64 * i;
+      if (px < N && y < H) {
+        const int64_t o = (int64_t)y * N + px;
+        pr[i] = src[o];
+        pg[i] = src[hw + o];
+        pb[i] = src[2 * hw + o];
+      }
     }
-  }
-  // ---- pass 1: radix R1, Ns = 1 (no twiddles); in place, one butterfly per lane
-  if (lane < 3 * B1) {
-    const int c = lane / B1, j = lane - c * B1;
-    float2 v[R1];
+  };
+  int y = jb.y + wave;
+  fetch(y);
+#pragma unroll 1
+  for (int rr = 0; rr < RPW; ++rr, y += 4) {
+    if (y >= H) break;
+    // ---- IPT (util.py:70-82) + Makhoul reorder into LDS
 #pragma unroll
-    for (int r = 0; r < R1; ++r) v[r] = z[c][pad16(j + r * B1)];
-    DFT<R1>::run(v);
+    for (int i = 0; i < PX; ++i) {
+      const int px = lane + 64 * i;
+      if (px < N) {
+        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, pr[i], pg[i], pb[i]), gam);
+        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, pr[i], pg[i], pb[i]), gam);
+        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, pr[i], pg[i], pb[i]), gam);
+        const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
+        const int o = 2 * pad16(v >> 1) + (v & 1);
+        zf0[o] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
+        zf1[o] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
+        zf2[o] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+      }
+    }
+    fetch(y + 4);  // next row of this wave: in flight while this one is transformed
+    // ---- pass 1: radix R1, Ns = 1 (no twiddles); in place, one butterfly per lane
+    if (lane < 3 * B1) {
+      const int c = lane / B1, j = lane - c * B1;
+      float2 v[R1];
 #pragma unroll
-    for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = v[r];
-  }
-  // ---- pass 2: radix R2, Ns = R1; twiddle W_M^{r*j}
-  if (lane < 3 * B2) {
-    const int c = lane / B2, j = lane - c * B2;  // j < B2 = R1 = Ns
-    float2 v[R2];
+      for (int r = 0; r < R1; ++r) v[r] = z[c][pad16(j + r * B1)];
+      DFT<R1>::run(v);
 #pragma unroll
-    for (int r = 0; r < R2; ++r) v[r] = z[c][pad16(j + r * B2)];
+      for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = v[r];
+    }
+    // ---- pass 2: radix R2, Ns = R1; twiddle W_M^{r*j}
+    if (lane < 3 * B2) {
+      const int c = lane / B2, j = lane - c * B2;
+      float2 v[R2];
 #pragma unroll
-    for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw[r * j]);
-    DFT<R2>::run(v);
+      for (int r = 0; r < R2; ++r) v[r] = z[c][pad16(j + r * B2)];
 #pragma unroll
-    for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
-  }
-  // ---- Makhoul post-processing, write T[c][y][kx] for kx < Kw
-  const int Kw = d.Kw;
-  constexpr int NI = 3 * (M + 1);
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw[r * j]);
+      DFT<R2>::run(v);
+#pragma unroll
+      for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
+    }
+    // ---- Makhoul post-processing -> T
+    constexpr int NI = 3 * (M + 1);
 #pragma unroll 2
-  for (int it = lane; it < NI; it += 64) {
-    const int c = it / (M + 1), k = it - c * (M + 1);
-    const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
-    const float2 A = z[c][pad16(ka)];
-    float2 B = z[c][pad16(kb)];
-    B.y = -B.y;
-    const float2 al = post[2 * k], be = post[2 * k + 1];
-    const float2 W = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
-    float* trow = ws + d.ws_t + ((int64_t)c * d.H + y) * Kw;
-    if (k < Kw) trow[k] = W.x;
-    if (k >= 1 && k < M && N - k < Kw) trow[N - k] = -W.y;
+    for (int it = lane; it < NI; it += 64) {
+      const int c = it / (M + 1), k = it - c * (M + 1);
+      const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
+      const float2 A = z[c][pad16(ka)];
+      float2 B = z[c][pad16(kb)];
+      B.y = -B.y;
+      const float2 al = post[2 * k], be = post[2 * k + 1];
+      const float2 W = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+      if (d.t_strips) {
+        // T[c][w][y][p2], w = kx / 14: each strip of a 16-row block is 896 contiguous bytes
+        float* tc = T + (int64_t)c * H * Kw + (int64_t)y * 14;
+        if (k < Kw) tc[(int64_t)(k / 14) * H * 14 + (k % 14)] = W.x;
+        if (k >= 1 && k < M && N - k < Kw) {
+          const int kx = N - k;
+          tc[(int64_t)(kx / 14) * H * 14 + (kx % 14)] = -W.y;
+        }
+      } else {
+        float* trow = T + ((int64_t)c * H + y) * Kw;
+        if (k < Kw) trow[k] = W.x;
+        if (k >= 1 && k < M && N - k < Kw) trow[N - k] = -W.y;
+      }
+    }
   }
 }
 
@@ -115,13 +146,31 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
   const int4 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
   const int c = jb.y, strip = jb.z;
-  const float* T = ws + d.ws_t + (int64_t)c * d.H * d.Kw + strip * KS;
   const int Kw = d.Kw;
+  if (d.t_strips) {
+    // strip (c, w) is N*KS contiguous floats: 16-byte loads
+    const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * Kw + (int64_t)strip * N * KS);
+    static_assert((N * KS) % 4 == 0, "strip of whole float4s");
+#pragma unroll
+    for (int q = tid; q < N * KS / 4; q += 256) {
+      const float4 t4 = T4[q];
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = 4 * q + u;
+        const int y = e / KS, j = e - y * KS;
+        const int v = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
+        zs[v * KS + j] = tv[u];
+      }
+    }
+  } else {
+    const float* T = ws + d.ws_t + (int64_t)c * d.H * Kw + strip * KS;
 #pragma unroll 4
-  for (int e = tid; e < N * KS; e += 256) {
-    const int y = e / KS, j = e - y * KS;
-    const int v = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
-    zs[v * KS + j] = T[(int64_t)y * Kw + j];
+    for (int e = tid; e < N * KS; e += 256) {
+      const int y = e / KS, j = e - y * KS;
+      const int v = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
+      zs[v * KS + j] = T[(int64_t)y * Kw + j];
+    }
   }
   __syncthreads();
   // ---- pass 1 (Ns = 1)
@@ -226,7 +275,7 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
   return 0;
 }
 
-int fft_spec_rows_per_block(int spec) { return spec ? 4 : 0; }
+int fft_spec_rows_per_block(int spec) { return spec ? 16 : 0; }
 
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                           const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s) {
