@@ -112,4 +112,50 @@ __device__ inline void token_epilogue(const EncParams& ep, int c, int h, int w, 
 }
 
 
+// token_epilogue specialised for a compile-time patch size with one LFQ
+// codebook per tile row (codebook_dim == P): lane j's code is its row's sign
+// bits in MSB-first order (lfq.py:187), i.e. a bit reversal — no exchange.
+// vals: this lane's row, thr: thresholds row (nullable -> PatchNorm values).
+template <int P>
+__device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int h, int w, int j,
+                                                 const float* vals, int64_t tok, TokenSinks sk) {
+  constexpr int PP = P * P;
+  float amax = 0.0f;
+  uint32_t bits = 0;
+  if (j < P) {
+    const int64_t tab = ((((int64_t)c * ep.maxph + h) * ep.maxpw) + w) * PP + (int64_t)j * P;
+#pragma unroll
+    for (int p2 = 0; p2 < P; ++p2) amax = nanmax(amax, fabsf(vals[p2]));
+    if (sk.raw) {
+#pragma unroll
+      for (int p2 = 0; p2 < P; ++p2) sk.raw[tok * PP + j * P + p2] = vals[p2];
+    }
+    if (ep.median) {
+      if (sk.norm || !ep.thr) {
+#pragma unroll
+        for (int p2 = 0; p2 < P; ++p2) {
+          const float y = pn_forward(vals[p2], ep.median[tab + p2], ep.b[tab + p2], ep.eps, ep.min_val, ep.max_val);
+          bits |= (y > 0.0f ? 1u : 0u) << p2;
+          if (sk.norm) sk.norm[tok * PP + j * P + p2] = y;
+        }
+      } else if ((P & 1) == 0) {
+        const float2* t2 = reinterpret_cast<const float2*>(ep.thr + tab);
+#pragma unroll
+        for (int p = 0; p < P / 2; ++p) {
+          const float2 t = t2[p];
+          bits |= (vals[2 * p] >= t.x ? 1u : 0u) << (2 * p);
+          bits |= (vals[2 * p + 1] >= t.y ? 1u : 0u) << (2 * p + 1);
+        }
+      } else {
+#pragma unroll
+        for (int p2 = 0; p2 < P; ++p2) bits |= (vals[p2] >= ep.thr[tab + p2] ? 1u : 0u) << p2;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
+  if (j == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
+  if (ep.median && sk.codes && j < P) sk.codes[tok * P + j] = (uint16_t)(__builtin_bitreverse32(bits) >> (32 - P));
+}
+
 }  // namespace dctae

@@ -31,7 +31,12 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
   __shared__ float2 zs[4][3][MP];
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  __syncthreads();
   const int2 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
   float2(*z)[MP] = zs[wave];
@@ -95,21 +100,20 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
 #pragma unroll
       for (int r = 0; r < R2; ++r) v[r] = z[c][pad16(j + r * B2)];
 #pragma unroll
-      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw[r * j]);
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * j]);
       DFT<R2>::run(v);
 #pragma unroll
       for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
     }
     // ---- Makhoul post-processing -> T
     constexpr int NI = 3 * (M + 1);
-#pragma unroll 2
     for (int it = lane; it < NI; it += 64) {
       const int c = it / (M + 1), k = it - c * (M + 1);
       const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
       const float2 A = z[c][pad16(ka)];
       float2 B = z[c][pad16(kb)];
       B.y = -B.y;
-      const float2 al = post[2 * k], be = post[2 * k + 1];
+      const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
       const float2 W = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
       if (d.t_strips) {
         // T[c][w][y][p2], w = kx / 14: each strip of a 16-row block is 896 contiguous bytes
@@ -129,7 +133,10 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
-// cols: one block = (image, channel, tile column); KS = P columns of T
+// cols: one block = (image, channel, tile column); KS = P columns of T.
+// LDS column layout: complex m of column col at re [2*pad16(m)*KSP + col],
+// im [+KSP], KSP odd: with 16 butterflies of one column on consecutive lanes
+// every Stockham read and write of a half-wave hits 32 distinct banks.
 // ---------------------------------------------------------------------------
 template <int N, int R1, int R2, int KS>
 __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
@@ -137,18 +144,27 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
                                                    const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
   constexpr int M = N / 2;
   constexpr int B1 = M / R1, B2 = M / R2;
-  static_assert(KS * B1 <= 256 && KS * B2 <= 256, "one butterfly per thread per pass");
-  static_assert(R1 == 16, "first radix 16");
-  // complex m of column j: re at (2m)*KS + j, im at (2m+1)*KS + j; reused as X[ky][j]
-  __shared__ float zs[2 * M * KS];
-  __shared__ uint16_t rowbits[16 * kMaxP];
+  constexpr int KSP = KS | 1;              // odd row stride
+  constexpr int ZROWS = 2 * (pad16(M - 1) + 1);
+  static_assert(KS * 16 <= 256, "16 butterfly lanes per column");
+  static_assert(B1 <= 16 && B2 <= 16 && R1 == 16, "plan shape");
+  __shared__ float zs[ZROWS * KSP];
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
   const int tid = threadIdx.x;
   const int4 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
   const int c = jb.y, strip = jb.z;
   const int Kw = d.Kw;
+  for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
+  for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
+  auto zre = [&](int m, int col) -> float& { return zs[2 * pad16(m) * KSP + col]; };
+  auto zim = [&](int m, int col) -> float& { return zs[(2 * pad16(m) + 1) * KSP + col]; };
+  auto put = [&](int y, int j, float v) {
+    const int vv = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
+    zs[(2 * pad16(vv >> 1) + (vv & 1)) * KSP + j] = v;
+  };
   if (d.t_strips) {
-    // strip (c, w) is N*KS contiguous floats: 16-byte loads
     const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * Kw + (int64_t)strip * N * KS);
     static_assert((N * KS) % 4 == 0, "strip of whole float4s");
 #pragma unroll
@@ -159,8 +175,7 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
       for (int u = 0; u < 4; ++u) {
         const int e = 4 * q + u;
         const int y = e / KS, j = e - y * KS;
-        const int v = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
-        zs[v * KS + j] = tv[u];
+        put(y, j, tv[u]);
       }
     }
   } else {
@@ -168,31 +183,27 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
 #pragma unroll 4
     for (int e = tid; e < N * KS; e += 256) {
       const int y = e / KS, j = e - y * KS;
-      const int v = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
-      zs[v * KS + j] = T[(int64_t)y * Kw + j];
+      put(y, j, T[(int64_t)y * Kw + j]);
     }
   }
   __syncthreads();
+  const int jj = tid & 15, col = tid >> 4;   // butterfly on the lane, column across 16-lane groups
+  const bool on_col = col < KS;
   // ---- pass 1 (Ns = 1)
   {
     float2 v[R1];
-    const bool on = tid < KS * B1;
-    const int col = tid % KS, j = tid / KS;
+    const bool on = on_col && jj < B1;
     if (on) {
 #pragma unroll
-      for (int r = 0; r < R1; ++r) {
-        const int m = j + r * B1;
-        v[r] = make_float2(zs[(2 * m) * KS + col], zs[(2 * m + 1) * KS + col]);
-      }
+      for (int r = 0; r < R1; ++r) v[r] = make_float2(zre(jj + r * B1, col), zim(jj + r * B1, col));
       DFT<R1>::run(v);
     }
     __syncthreads();
     if (on) {
 #pragma unroll
       for (int r = 0; r < R1; ++r) {
-        const int m = j * R1 + r;
-        zs[(2 * m) * KS + col] = v[r].x;
-        zs[(2 * m + 1) * KS + col] = v[r].y;
+        zre(jj * R1 + r, col) = v[r].x;
+        zim(jj * R1 + r, col) = v[r].y;
       }
     }
     __syncthreads();
@@ -200,67 +211,57 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
   // ---- pass 2 (Ns = R1)
   {
     float2 v[R2];
-    const bool on = tid < KS * B2;
-    const int col = tid % KS, j = tid / KS;
+    const bool on = on_col && jj < B2;
     if (on) {
 #pragma unroll
-      for (int r = 0; r < R2; ++r) {
-        const int m = j + r * B2;
-        v[r] = make_float2(zs[(2 * m) * KS + col], zs[(2 * m + 1) * KS + col]);
-      }
+      for (int r = 0; r < R2; ++r) v[r] = make_float2(zre(jj + r * B2, col), zim(jj + r * B2, col));
 #pragma unroll
-      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw[r * j]);
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
       DFT<R2>::run(v);
     }
     __syncthreads();
     if (on) {
 #pragma unroll
       for (int r = 0; r < R2; ++r) {
-        const int m = j + r * R1;
-        zs[(2 * m) * KS + col] = v[r].x;
-        zs[(2 * m + 1) * KS + col] = v[r].y;
+        zre(jj + r * R1, col) = v[r].x;
+        zim(jj + r * R1, col) = v[r].y;
       }
     }
     __syncthreads();
   }
-  // ---- Makhoul post-processing into registers, then X[ky][j] in place
-  constexpr int NI = (M + 1) * KS;
-  constexpr int PER = (NI + 255) / 256;
-  float2 wv[PER];
+  // ---- Makhoul post-processing into registers, then X[ky][col] (row stride KSP) in place
+  constexpr int KPL = (M + 1 + 15) / 16;   // k values per lane
+  float2 wv[KPL];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int it = tid + 256 * i;
-    if (it < NI) {
-      const int k = it / KS, col = it - k * KS;
+  for (int i = 0; i < KPL; ++i) {
+    const int k = jj + 16 * i;
+    if (on_col && k <= M) {
       const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
-      const float2 A = make_float2(zs[(2 * ka) * KS + col], zs[(2 * ka + 1) * KS + col]);
-      const float2 B = make_float2(zs[(2 * kb) * KS + col], -zs[(2 * kb + 1) * KS + col]);
-      const float2 al = post[2 * k], be = post[2 * k + 1];
+      const float2 A = make_float2(zre(ka, col), zim(ka, col));
+      const float2 B = make_float2(zre(kb, col), -zim(kb, col));
+      const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
       wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
     }
   }
   __syncthreads();
   const int Kh = d.Kh;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int it = tid + 256 * i;
-    if (it < NI) {
-      const int k = it / KS, col = it - k * KS;
-      if (k < Kh) zs[k * KS + col] = wv[i].x;
-      if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KS + col] = -wv[i].y;
+  for (int i = 0; i < KPL; ++i) {
+    const int k = jj + 16 * i;
+    if (on_col && k <= M) {
+      if (k < Kh) zs[k * KSP + col] = wv[i].x;
+      if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KSP + col] = -wv[i].y;
     }
   }
   __syncthreads();
   // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
   const int g16 = tid >> 4, jl = tid & 15;
   for (int h = g16; h < d.qh; h += 16) {
-    float vals[kMaxP];
-    if (jl < KS) {
+    float vals[KS];
 #pragma unroll
-      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = zs[(KS * h + jl) * KS + p2];
-    }
+    for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
     const int f = (h * d.qw + strip) * ep.C + c;
-    token_epilogue(ep, c, h, strip, jl, g16, vals, d.tok_off + f, sk, rowbits);
+    token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
   }
 }
 
