@@ -56,7 +56,8 @@ struct dctae_ctx {
   int64_t fft_tab_cap = 0, fft_tab_used = 0;
   std::map<int, FftPlan> fft_plans;   // N -> plan (N = 0 entries never stored)
   bool fft_enabled = true;
-  bool fft_spec_enabled = true;       // use the compile-time specialised kernels when a plan matches
+  bool fft_spec_enabled = true;
+  int rows_prefetch = 0;              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 160ll << 20;  // workspace per chunk of the FFT path (MALL-resident T)
   // cached encode plan
@@ -555,6 +556,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   if (k == "fft") ctx->fft_enabled = value != 0;
   else if (k == "fft_spec") ctx->fft_spec_enabled = value != 0;
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
+  else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -947,7 +949,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       if (j.n_fr[v]) {
         Timer t(ctx, s, "fft_rows");
         launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
-                             ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, s);
+                             ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, s,
+                             ctx->rows_prefetch);
       }
     if (j.any_gemm_cols) {
       {

@@ -17,7 +17,7 @@ __device__ __forceinline__ constexpr int pad16(int m) { return m + (m >> 4); }
 // ---------------------------------------------------------------------------
 // rows: one wave = one image row, its 3 IPT channels are 3 jobs
 // ---------------------------------------------------------------------------
-template <int N, int R1, int R2>
+template <int N, int R1, int R2, bool PF>
 __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                    const float* __restrict__ rgb, float* __restrict__ ws,
                                                    const float2* __restrict__ tw, const float2* __restrict__ post,
@@ -26,6 +26,7 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   constexpr int MP = pad16(M - 1) + 2;
   constexpr int B1 = M / R1, B2 = M / R2;
   constexpr int PX = (N + 63) / 64;        // pixels per lane and row
+  constexpr int KI = (M + 63) / 64;        // k = lane + 64 i, i < KI, covers k < M (k = M by lane 0)
   constexpr int RPW = 4;                   // rows per wave (block = 16 rows)
   static_assert(R1 * R2 == M, "two-pass plan");
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
@@ -43,12 +44,31 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   float* zf0 = reinterpret_cast<float*>(z[0]);
   float* zf1 = reinterpret_cast<float*>(z[1]);
   float* zf2 = reinterpret_cast<float*>(z[2]);
-  const int64_t hw = (int64_t)d.H * N;
+  const int H = d.H, Kw = d.Kw;
+  const int64_t hw = (int64_t)H * N;
   const float* src = rgb + d.rgb_off;
   const float gam = 0.430000007152557373046875f;
-  const int Kw = d.Kw, H = d.H;
-  float* T = ws + d.ws_t;
-  // rows of this wave: y0 + wave + 4*rr
+  const bool strips = d.t_strips != 0;
+  // ---- lane-invariant index maps (the same for every row)
+  int zo[PX];                               // Makhoul slot of pixel lane + 64 i
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int px = lane + 64 * i;
+    const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
+    zo[i] = 2 * pad16(v >> 1) + (v & 1);
+  }
+  // T offset of coefficient kx within (channel, row): strips: (kx/14)*H*14 + kx%14, else kx; -1 = not kept
+  int oa[KI], ob[KI];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = lane + 64 * i;
+    const int kx2 = N - k;
+    oa[i] = (k < Kw) ? (strips ? (k / 14) * H * 14 + k % 14 : k) : -1;
+    ob[i] = (k >= 1 && kx2 < Kw) ? (strips ? (kx2 / 14) * H * 14 + kx2 % 14 : kx2) : -1;
+  }
+  const int oM = (M < Kw) ? (strips ? (M / 14) * H * 14 + M % 14 : M) : -1;
+  const int ystride = strips ? 14 : Kw;     // T offset step per row
+  const int64_t cstride = (int64_t)H * Kw;  // per channel
   float pr[PX], pg[PX], pb[PX];
   auto fetch = [&](int y) {
 #pragma unroll
@@ -63,26 +83,27 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
     }
   };
   int y = jb.y + wave;
-  fetch(y);
+  if (PF) fetch(y);
 #pragma unroll 1
   for (int rr = 0; rr < RPW; ++rr, y += 4) {
     if (y >= H) break;
+    if (!PF) fetch(y);
     // ---- IPT (util.py:70-82) + Makhoul reorder into LDS
 #pragma unroll
     for (int i = 0; i < PX; ++i) {
-      const int px = lane + 64 * i;
-      if (px < N) {
+      if (lane + 64 * i < N) {
         const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, pr[i], pg[i], pb[i]), gam);
         const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, pr[i], pg[i], pb[i]), gam);
         const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, pr[i], pg[i], pb[i]), gam);
-        const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
-        const int o = 2 * pad16(v >> 1) + (v & 1);
-        zf0[o] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
-        zf1[o] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
-        zf2[o] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+        zf0[zo[i]] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
+        zf1[zo[i]] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
+        zf2[zo[i]] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
       }
     }
-    fetch(y + 4);  // next row of this wave: in flight while this one is transformed
+    if (PF) {
+      __builtin_amdgcn_sched_barrier(0);
+      fetch(y + 4);  // next row of this wave: in flight while this one is transformed
+    }
     // ---- pass 1: radix R1, Ns = 1 (no twiddles); in place, one butterfly per lane
     if (lane < 3 * B1) {
       const int c = lane / B1, j = lane - c * B1;
@@ -105,28 +126,29 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
 #pragma unroll
       for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
     }
-    // ---- Makhoul post-processing -> T
-    constexpr int NI = 3 * (M + 1);
-    for (int it = lane; it < NI; it += 64) {
-      const int c = it / (M + 1), k = it - c * (M + 1);
-      const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
-      const float2 A = z[c][pad16(ka)];
-      float2 B = z[c][pad16(kb)];
-      B.y = -B.y;
-      const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
-      const float2 W = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
-      if (d.t_strips) {
-        // T[c][w][y][p2], w = kx / 14: each strip of a 16-row block is 896 contiguous bytes
-        float* tc = T + (int64_t)c * H * Kw + (int64_t)y * 14;
-        if (k < Kw) tc[(int64_t)(k / 14) * H * 14 + (k % 14)] = W.x;
-        if (k >= 1 && k < M && N - k < Kw) {
-          const int kx = N - k;
-          tc[(int64_t)(kx / 14) * H * 14 + (kx % 14)] = -W.y;
+    // ---- Makhoul post-processing -> T (k = lane + 64 i; X[k] = Re W_k, X[N-k] = -Im W_k)
+#pragma unroll 1
+    for (int c = 0; c < 3; ++c) {
+      float* tb = ws + d.ws_t + c * cstride + (int64_t)y * ystride;
+#pragma unroll
+      for (int i = 0; i < KI; ++i) {
+        const int k = lane + 64 * i;
+        if (k < M) {
+          const float2 A = z[c][pad16(k)];
+          float2 B = z[c][pad16(k == 0 ? 0 : M - k)];
+          B.y = -B.y;
+          const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
+          const float2 W = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+          if (oa[i] >= 0) tb[oa[i]] = W.x;
+          if (ob[i] >= 0) tb[ob[i]] = -W.y;
         }
-      } else {
-        float* trow = T + ((int64_t)c * H + y) * Kw;
-        if (k < Kw) trow[k] = W.x;
-        if (k >= 1 && k < M && N - k < Kw) trow[N - k] = -W.y;
+        __builtin_amdgcn_sched_barrier(0);  // bound register pressure: one k-slice in flight
+      }
+      if (lane == 0 && oM >= 0) {  // k = M: A = B = conj-paired Z[0]
+        const float2 A = z[c][0];
+        const float2 B = make_float2(A.x, -A.y);
+        const float2 W = cadd(cmul(post_s[2 * M], cadd(A, B)), cmul(post_s[2 * M + 1], csub(A, B)));
+        tb[oM] = W.x;
       }
     }
   }
@@ -279,12 +301,16 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
 int fft_spec_rows_per_block(int spec) { return spec ? 16 : 0; }
 
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s) {
+                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int prefetch) {
   if (n_blocks <= 0) return;
-  if (spec == 1)
-    hipLaunchKernelGGL((k_fft_rows2<512, 16, 16>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
-  else if (spec == 2)
-    hipLaunchKernelGGL((k_fft_rows2<224, 16, 7>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+  if (spec == 1) {
+    if (prefetch)
+      hipLaunchKernelGGL((k_fft_rows2<512, 16, 16, true>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+    else
+      hipLaunchKernelGGL((k_fft_rows2<512, 16, 16, false>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+  } else if (spec == 2) {
+    hipLaunchKernelGGL((k_fft_rows2<224, 16, 7, false>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+  }
 }
 
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,

@@ -37,7 +37,7 @@ void launch_norm_thresholds(const float* med, const float* b, int64_t n, float e
 int fft_spec_id(int N, const int* radix, int npass, int P);
 int fft_spec_rows_per_block(int spec);
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s);
+                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int prefetch);
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
                           hipStream_t s);
