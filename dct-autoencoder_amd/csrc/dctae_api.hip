@@ -57,7 +57,8 @@ struct dctae_ctx {
   std::map<int, FftPlan> fft_plans;   // N -> plan (N = 0 entries never stored)
   bool fft_enabled = true;
   bool fft_spec_enabled = true;
-  int rows_prefetch = 0;              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
+  int rows_prefetch = 0;
+  int t_layout = 1;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 160ll << 20;  // workspace per chunk of the FFT path (MALL-resident T)
   // cached encode plan
@@ -557,6 +558,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "fft_spec") ctx->fft_spec_enabled = value != 0;
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
+  else if (k == "t_layout" && value >= 0 && value <= 2) ctx->t_layout = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -688,7 +690,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     D[i].plan_h = plan_of(D[i].H);
     // strip-major T when both passes run on the specialised kernels
     D[i].t_strips = (P == 14 && D[i].plan_w >= 0 && D[i].plan_h >= 0 && plans[D[i].plan_w].spec &&
-                     plans[D[i].plan_h].spec) ? 1 : 0;
+                     plans[D[i].plan_h].spec) ? ctx->t_layout : 0;
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
@@ -696,7 +698,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   // chunks: FFT images are grouped so the intermediate T of a chunk stays in
   // the 256 MiB Infinity Cache between the row and column kernels
   auto ws_of = [&](const ImgDesc& d) {
-    int64_t w = 3ll * d.Kw * d.H + 64;
+    int64_t w = 3ll * (d.Kw + d.Kw / 7) * d.H + 64;  // room for 16-wide strips
     if (d.plan_w < 0) w += 3ll * d.H * d.W + 64;
     if (d.plan_h < 0) w += 3ll * d.Kh * d.Kw + 64;
     return w * 4;
@@ -730,7 +732,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     for (int i = j.i0; i < j.i1; ++i) {
       ImgDesc& d = D[i];
       d.ws_t = wsf;
-      wsf += up(3ll * d.Kw * d.H);
+      wsf += up(3ll * (d.t_strips == 2 ? (d.Kw / 14) * 16 : d.Kw) * d.H);
       d.ws_p = wsf;
       if (d.plan_w < 0) wsf += up(3ll * d.H * d.W);
       d.ws_y = wsf;
@@ -852,7 +854,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
-                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled,
+                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);

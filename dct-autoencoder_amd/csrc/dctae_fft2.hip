@@ -48,7 +48,8 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   const int64_t hw = (int64_t)H * N;
   const float* src = rgb + d.rgb_off;
   const float gam = 0.430000007152557373046875f;
-  const bool strips = d.t_strips != 0;
+  const int lay = d.t_strips;               // 0 row-major, 1 strips of 14, 2 strips padded to 16
+  const int SW = (lay == 2) ? 16 : 14;       // strip row width (floats)
   // ---- lane-invariant index maps (the same for every row)
   int zo[PX];                               // Makhoul slot of pixel lane + 64 i
 #pragma unroll
@@ -63,12 +64,12 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   for (int i = 0; i < KI; ++i) {
     const int k = lane + 64 * i;
     const int kx2 = N - k;
-    oa[i] = (k < Kw) ? (strips ? (k / 14) * H * 14 + k % 14 : k) : -1;
-    ob[i] = (k >= 1 && kx2 < Kw) ? (strips ? (kx2 / 14) * H * 14 + kx2 % 14 : kx2) : -1;
+    oa[i] = (k < Kw) ? (lay ? (k / 14) * H * SW + k % 14 : k) : -1;
+    ob[i] = (k >= 1 && kx2 < Kw) ? (lay ? (kx2 / 14) * H * SW + kx2 % 14 : kx2) : -1;
   }
-  const int oM = (M < Kw) ? (strips ? (M / 14) * H * 14 + M % 14 : M) : -1;
-  const int ystride = strips ? 14 : Kw;     // T offset step per row
-  const int64_t cstride = (int64_t)H * Kw;  // per channel
+  const int oM = (M < Kw) ? (lay ? (M / 14) * H * SW + M % 14 : M) : -1;
+  const int ystride = lay ? SW : Kw;        // T offset step per row
+  const int64_t cstride = lay == 2 ? (int64_t)H * (Kw / 14) * 16 : (int64_t)H * Kw;  // per channel
   float pr[PX], pg[PX], pb[PX];
   auto fetch = [&](int y) {
 #pragma unroll
@@ -186,7 +187,20 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
     const int vv = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
     zs[(2 * pad16(vv >> 1) + (vv & 1)) * KSP + j] = v;
   };
-  if (d.t_strips) {
+  if (d.t_strips == 2) {
+    // padded strips: row y of strip (c, w) = 16 floats at 64-byte alignment, 14 used
+    const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * (Kw / KS) * 16 +
+                                                       (int64_t)strip * N * 16);
+#pragma unroll
+    for (int q = tid; q < N * 4; q += 256) {
+      const float4 t4 = T4[q];
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+      const int y = q >> 2, j0 = (q & 3) * 4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (j0 + u < KS) put(y, j0 + u, tv[u]);
+    }
+  } else if (d.t_strips) {
     const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * Kw + (int64_t)strip * N * KS);
     static_assert((N * KS) % 4 == 0, "strip of whole float4s");
 #pragma unroll
