@@ -58,7 +58,7 @@ struct dctae_ctx {
   bool fft_enabled = true;
   bool fft_spec_enabled = true;
   int rows_prefetch = 0;
-  int t_layout = 1;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
+  int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 160ll << 20;  // workspace per chunk of the FFT path (MALL-resident T)
   // cached encode plan
@@ -794,8 +794,11 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         j.any_gemm_cols = 1;
       } else {
         const FftPlan& p = plans[d.plan_h];
+        // generic kernel: one tile column per block; specialised: groups of
+        // up to 16 adjacent tile columns walked by one block
+        const int G = p.spec ? 16 : 1;
         for (int c = 0; c < 3; ++c)
-          for (int w = 0; w < d.qw; ++w) fc[p.spec].push_back(make_int4(li, c, w, 0));
+          for (int w = 0; w < d.qw; w += G) fc[p.spec].push_back(make_int4(li, c, w, std::min(G, d.qw - w)));
         if (p.spec) {
           j.tw_off_c[p.spec] = p.tw_off;
           j.post_off_c[p.spec] = p.post_off;
