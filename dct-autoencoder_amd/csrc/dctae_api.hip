@@ -58,6 +58,8 @@ struct dctae_ctx {
   bool fft_enabled = true;
   bool fft_spec_enabled = true;
   int rows_prefetch = 0;
+  int col_group = 1;                  // tile columns walked per column block (specialised kernel)
+  int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 160ll << 20;  // workspace per chunk of the FFT path (MALL-resident T)
@@ -559,6 +561,8 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
   else if (k == "t_layout" && value >= 0 && value <= 2) ctx->t_layout = (int)value;
+  else if (k == "col_group" && value >= 1 && value <= 32) ctx->col_group = (int)value;
+  else if (k == "xcd_order") ctx->xcd_order = value != 0;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -796,7 +800,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         const FftPlan& p = plans[d.plan_h];
         // generic kernel: one tile column per block; specialised: groups of
         // up to 16 adjacent tile columns walked by one block
-        const int G = p.spec ? 16 : 1;
+        const int G = p.spec ? ctx->col_group : 1;
         for (int c = 0; c < 3; ++c)
           for (int w = 0; w < d.qw; w += G) fc[p.spec].push_back(make_int4(li, c, w, std::min(G, d.qw - w)));
         if (p.spec) {
@@ -810,6 +814,35 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     j.gp_off = E.pb.add(probs.data() + p0, probs.size() - p0);
     j.rows_t_off = E.pb.add(rt.data(), rt.size());
     j.cols_t_off = E.pb.add(ct.data(), ct.size());
+    // XCD-aware order of the column blocks (speed only; any order is correct):
+    // blocks b and b+8 are dealt to the same XCD, so give all the blocks of
+    // one (image, channel) the same b % 8 and consecutive b / 8 — the 56-byte
+    // row slices of neighbouring tile columns then share that XCD's L2 lines.
+    if (ctx->xcd_order) {
+      for (int v = 1; v < kVariants; ++v) {
+        std::vector<int4>& L = fc[v];
+        if (L.size() < 16) continue;
+        // units = runs of blocks with the same (image, channel), in list order
+        std::vector<std::pair<size_t, size_t>> units;
+        for (size_t a0 = 0; a0 < L.size();) {
+          size_t a1 = a0 + 1;
+          while (a1 < L.size() && L[a1].x == L[a0].x && L[a1].y == L[a0].y) ++a1;
+          units.push_back({a0, a1});
+          a0 = a1;
+        }
+        std::vector<std::vector<int4>> lanes(8);
+        for (size_t u = 0; u < units.size(); ++u)
+          for (size_t a = units[u].first; a < units[u].second; ++a) lanes[u % 8].push_back(L[a]);
+        std::vector<int4> out;
+        out.reserve(L.size());
+        size_t maxlen = 0;
+        for (auto& l : lanes) maxlen = std::max(maxlen, l.size());
+        for (size_t q = 0; q < maxlen; ++q)
+          for (int x = 0; x < 8; ++x)
+            if (q < lanes[x].size()) out.push_back(lanes[x][q]);
+        L.swap(out);
+      }
+    }
     for (int v = 0; v < kVariants; ++v) {
       j.fr_off[v] = E.pb.add(fr[v].data(), fr[v].size());
       j.fc_off[v] = E.pb.add(fc[v].data(), fc[v].size());
@@ -857,7 +890,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
-                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout,
+                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout +
+                             16 * ctx->col_group + 1024 * ctx->xcd_order,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
