@@ -58,7 +58,6 @@ struct dctae_ctx {
   bool fft_enabled = true;
   bool fft_spec_enabled = true;
   int rows_prefetch = 0;
-  int col_group = 1;                  // tile columns walked per column block (specialised kernel)
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
@@ -561,7 +560,6 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
   else if (k == "t_layout" && value >= 0 && value <= 2) ctx->t_layout = (int)value;
-  else if (k == "col_group" && value >= 1 && value <= 32) ctx->col_group = (int)value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
@@ -800,7 +798,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         const FftPlan& p = plans[d.plan_h];
         // generic kernel: one tile column per block; specialised: groups of
         // up to 16 adjacent tile columns walked by one block
-        const int G = p.spec ? ctx->col_group : 1;
+        const int G = 1;
         for (int c = 0; c < 3; ++c)
           for (int w = 0; w < d.qw; w += G) fc[p.spec].push_back(make_int4(li, c, w, std::min(G, d.qw - w)));
         if (p.spec) {
@@ -891,7 +889,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout +
-                             16 * ctx->col_group + 1024 * ctx->xcd_order,
+                             1024 * ctx->xcd_order,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);

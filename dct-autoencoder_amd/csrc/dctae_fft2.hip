@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
   const int tid = threadIdx.x;
   const int4 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
-  const int c = jb.y;
+  const int c = jb.y, strip = jb.z;
   const int Kw = d.Kw;
   for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
   for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
@@ -187,124 +187,128 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
     const int vv = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
     zs[(2 * pad16(vv >> 1) + (vv & 1)) * KSP + j] = v;
   };
-  // walk jb.w adjacent tile columns: with row-major T the 128-byte lines shared by
-  // neighbouring 56-byte slices are then re-read from L2, not HBM
-#pragma unroll 1
-  for (int strip = jb.z; strip < jb.z + jb.w; ++strip) {
-    __syncthreads();  // previous strip's epilogue is done with zs
-    if (d.t_strips == 2) {
-      // padded strips: row y of strip (c, w) = 16 floats at 64-byte alignment, 14 used
-      const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * (Kw / KS) * 16 +
-                                                         (int64_t)strip * N * 16);
-  #pragma unroll
-      for (int q = tid; q < N * 4; q += 256) {
-        const float4 t4 = T4[q];
-        const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
-        const int y = q >> 2, j0 = (q & 3) * 4;
-  #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (j0 + u < KS) put(y, j0 + u, tv[u]);
-      }
-    } else if (d.t_strips) {
-      const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * Kw + (int64_t)strip * N * KS);
-      static_assert((N * KS) % 4 == 0, "strip of whole float4s");
-  #pragma unroll
-      for (int q = tid; q < N * KS / 4; q += 256) {
-        const float4 t4 = T4[q];
-        const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
-  #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = 4 * q + u;
-          const int y = e / KS, j = e - y * KS;
-          put(y, j, tv[u]);
-        }
-      }
-    } else {
-      const float* T = ws + d.ws_t + (int64_t)c * d.H * Kw + strip * KS;
-  #pragma unroll 4
-      for (int e = tid; e < N * KS; e += 256) {
+  if (d.t_strips == 2) {
+    // padded strips: row y of strip (c, w) = 16 floats at 64-byte alignment, 14 used
+    const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * (Kw / KS) * 16 +
+                                                       (int64_t)strip * N * 16);
+#pragma unroll
+    for (int q = tid; q < N * 4; q += 256) {
+      const float4 t4 = T4[q];
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+      const int y = q >> 2, j0 = (q & 3) * 4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (j0 + u < KS) put(y, j0 + u, tv[u]);
+    }
+  } else if (d.t_strips) {
+    const float4* T4 = reinterpret_cast<const float4*>(ws + d.ws_t + (int64_t)c * d.H * Kw + (int64_t)strip * N * KS);
+    static_assert((N * KS) % 4 == 0, "strip of whole float4s");
+#pragma unroll
+    for (int q = tid; q < N * KS / 4; q += 256) {
+      const float4 t4 = T4[q];
+      const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = 4 * q + u;
         const int y = e / KS, j = e - y * KS;
-        put(y, j, T[(int64_t)y * Kw + j]);
+        put(y, j, tv[u]);
+      }
+    }
+  } else if ((KS & 1) == 0 && (Kw & 1) == 0) {
+    // row-major T: KS/2 float2 per row (8-byte aligned: KS and Kw even)
+    const float2* T2 = reinterpret_cast<const float2*>(ws + d.ws_t + (int64_t)c * d.H * Kw + strip * KS);
+    const int rs = Kw / 2;
+#pragma unroll 2
+    for (int q = tid; q < N * (KS / 2); q += 256) {
+      const int y = q / (KS / 2), p = q - y * (KS / 2);
+      const float2 t2 = T2[(int64_t)y * rs + p];
+      put(y, 2 * p, t2.x);
+      put(y, 2 * p + 1, t2.y);
+    }
+  } else {
+    const float* T = ws + d.ws_t + (int64_t)c * d.H * Kw + strip * KS;
+#pragma unroll 4
+    for (int e = tid; e < N * KS; e += 256) {
+      const int y = e / KS, j = e - y * KS;
+      put(y, j, T[(int64_t)y * Kw + j]);
+    }
+  }
+  __syncthreads();
+  const int jj = tid & 15, col = tid >> 4;   // butterfly on the lane, column across 16-lane groups
+  const bool on_col = col < KS;
+  // ---- pass 1 (Ns = 1)
+  {
+    float2 v[R1];
+    const bool on = on_col && jj < B1;
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R1; ++r) v[r] = make_float2(zre(jj + r * B1, col), zim(jj + r * B1, col));
+      DFT<R1>::run(v);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        zre(jj * R1 + r, col) = v[r].x;
+        zim(jj * R1 + r, col) = v[r].y;
       }
     }
     __syncthreads();
-    const int jj = tid & 15, col = tid >> 4;   // butterfly on the lane, column across 16-lane groups
-    const bool on_col = col < KS;
-    // ---- pass 1 (Ns = 1)
-    {
-      float2 v[R1];
-      const bool on = on_col && jj < B1;
-      if (on) {
-  #pragma unroll
-        for (int r = 0; r < R1; ++r) v[r] = make_float2(zre(jj + r * B1, col), zim(jj + r * B1, col));
-        DFT<R1>::run(v);
-      }
-      __syncthreads();
-      if (on) {
-  #pragma unroll
-        for (int r = 0; r < R1; ++r) {
-          zre(jj * R1 + r, col) = v[r].x;
-          zim(jj * R1 + r, col) = v[r].y;
-        }
-      }
-      __syncthreads();
+  }
+  // ---- pass 2 (Ns = R1)
+  {
+    float2 v[R2];
+    const bool on = on_col && jj < B2;
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R2; ++r) v[r] = make_float2(zre(jj + r * B2, col), zim(jj + r * B2, col));
+#pragma unroll
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
+      DFT<R2>::run(v);
     }
-    // ---- pass 2 (Ns = R1)
-    {
-      float2 v[R2];
-      const bool on = on_col && jj < B2;
-      if (on) {
-  #pragma unroll
-        for (int r = 0; r < R2; ++r) v[r] = make_float2(zre(jj + r * B2, col), zim(jj + r * B2, col));
-  #pragma unroll
-        for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
-        DFT<R2>::run(v);
-      }
-      __syncthreads();
-      if (on) {
-  #pragma unroll
-        for (int r = 0; r < R2; ++r) {
-          zre(jj + r * R1, col) = v[r].x;
-          zim(jj + r * R1, col) = v[r].y;
-        }
-      }
-      __syncthreads();
-    }
-    // ---- Makhoul post-processing into registers, then X[ky][col] (row stride KSP) in place
-    constexpr int KPL = (M + 1 + 15) / 16;   // k values per lane
-    float2 wv[KPL];
-  #pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      const int k = jj + 16 * i;
-      if (on_col && k <= M) {
-        const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
-        const float2 A = make_float2(zre(ka, col), zim(ka, col));
-        const float2 B = make_float2(zre(kb, col), -zim(kb, col));
-        const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
-        wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+    __syncthreads();
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R2; ++r) {
+        zre(jj + r * R1, col) = v[r].x;
+        zim(jj + r * R1, col) = v[r].y;
       }
     }
     __syncthreads();
-    const int Kh = d.Kh;
-  #pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      const int k = jj + 16 * i;
-      if (on_col && k <= M) {
-        if (k < Kh) zs[k * KSP + col] = wv[i].x;
-        if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KSP + col] = -wv[i].y;
-      }
+  }
+  // ---- Makhoul post-processing into registers, then X[ky][col] (row stride KSP) in place
+  constexpr int KPL = (M + 1 + 15) / 16;   // k values per lane
+  float2 wv[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = jj + 16 * i;
+    if (on_col && k <= M) {
+      const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
+      const float2 A = make_float2(zre(ka, col), zim(ka, col));
+      const float2 B = make_float2(zre(kb, col), -zim(kb, col));
+      const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
+      wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
     }
-    __syncthreads();
-    // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
-    const int g16 = tid >> 4, jl = tid & 15;
-    for (int h = g16; h < d.qh; h += 16) {
-      float vals[KS];
-  #pragma unroll
-      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
-      const int f = (h * d.qw + strip) * ep.C + c;
-      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+  }
+  __syncthreads();
+  const int Kh = d.Kh;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = jj + 16 * i;
+    if (on_col && k <= M) {
+      if (k < Kh) zs[k * KSP + col] = wv[i].x;
+      if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KSP + col] = -wv[i].y;
     }
-
+  }
+  __syncthreads();
+  // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
+  const int g16 = tid >> 4, jl = tid & 15;
+  for (int h = g16; h < d.qh; h += 16) {
+    float vals[KS];
+#pragma unroll
+    for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
+    const int f = (h * d.qw + strip) * ep.C + c;
+    token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
   }
 }
 
