@@ -158,4 +158,31 @@ __device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int
   if (ep.median && sk.codes && j < P) sk.codes[tok * P + j] = (uint16_t)(__builtin_bitreverse32(bits) >> (32 - P));
 }
 
+// token_epilogue_p with the thresholds already in registers (thr[p] covers
+// elements 2p, 2p+1 of this lane's row); codes-only path.
+template <int P>
+__device__ __forceinline__ void token_epilogue_thr(const EncParams& ep, int c, int h, int w, int j, const float* vals,
+                                                   const float2* thr, int64_t tok, TokenSinks sk) {
+  constexpr int PP = P * P;
+  float amax = 0.0f;
+  uint32_t bits = 0;
+  if (j < P) {
+#pragma unroll
+    for (int p = 0; p < P / 2; ++p) {
+      amax = nanmax(amax, fabsf(vals[2 * p]));
+      amax = nanmax(amax, fabsf(vals[2 * p + 1]));
+      bits |= (vals[2 * p] >= thr[p].x ? 1u : 0u) << (2 * p);
+      bits |= (vals[2 * p + 1] >= thr[p].y ? 1u : 0u) << (2 * p + 1);
+    }
+    if (sk.raw) {
+#pragma unroll
+      for (int p2 = 0; p2 < P; ++p2) sk.raw[tok * PP + j * P + p2] = vals[p2];
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
+  if (j == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
+  if (sk.codes && j < P) sk.codes[tok * P + j] = (uint16_t)(__builtin_bitreverse32(bits) >> (32 - P));
+}
+
 }  // namespace dctae

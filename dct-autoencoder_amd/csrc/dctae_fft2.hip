@@ -179,6 +179,24 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
   const ImgDesc d = imgs[jb.x];
   const int c = jb.y, strip = jb.z;
   const int Kw = d.Kw;
+  // LFQ-bit thresholds of this thread's epilogue rows, fetched now so their
+  // latency hides behind the transform (tiles h = g16 + 16 r, row jl)
+  constexpr int EPR = 2;                    // epilogue rounds (qh <= 32 tiles, 16 groups)
+  const int g16 = tid >> 4, jl = tid & 15;
+  const bool use_thr = ep.median && ep.thr && !sk.norm && (KS % 2 == 0);
+  float2 thr_r[EPR][KS / 2];
+  if (use_thr) {
+#pragma unroll
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh && jl < KS) {
+        const float2* t2 = reinterpret_cast<const float2*>(
+            ep.thr + ((((int64_t)c * ep.maxph + h) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jl * KS);
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
+      }
+    }
+  }
   for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
   for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
   auto zre = [&](int m, int col) -> float& { return zs[2 * pad16(m) * KSP + col]; };
@@ -302,13 +320,26 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
   }
   __syncthreads();
   // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
-  const int g16 = tid >> 4, jl = tid & 15;
-  for (int h = g16; h < d.qh; h += 16) {
-    float vals[KS];
+  if (use_thr && d.qh <= 16 * EPR) {
 #pragma unroll
-    for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
-    const int f = (h * d.qw + strip) * ep.C + c;
-    token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh) {
+        float vals[KS];
+#pragma unroll
+        for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
+        const int f = (h * d.qw + strip) * ep.C + c;
+        token_epilogue_thr<KS>(ep, c, h, strip, jl, vals, thr_r[r], d.tok_off + f, sk);
+      }
+    }
+  } else {
+    for (int h = g16; h < d.qh; h += 16) {
+      float vals[KS];
+#pragma unroll
+      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
+      const int f = (h * d.qw + strip) * ep.C + c;
+      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+    }
   }
 }
 
