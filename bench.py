@@ -39,17 +39,18 @@ def kernel_models(h, w, p, maxp, ncb, s, images_per_row):
     qh, qw = min(h // p, maxp), min(w // p, maxp)
     kh, kw = p * qh, p * qw
     t = 3 * qh * qw
+    stage = t * (4 + 2 * ncb)            # score (f32) + LFQ codes (u16) per token, flat order
+    inter = 12 * h * kw                   # row-pass output T: 3 channels x H x Kw fp32
     return {
-        # name: (bound, per-image amount, unit)
+        # name: (bound, per-image amount, unit) — DESIGN.md "Kernels"
         "rgb_to_ipt": ("hbm", 12 * h * w + 12 * h * w, "B"),
         "gemm_rows": ("mfma", 3 * 2.0 * kw * h * w, "flop"),
         "gemm_cols": ("mfma", 3 * 2.0 * kh * kw * h, "flop"),
-        "fft_rows": ("hbm", 12 * h * w, "B"),
-        "fft_cols_epilogue": ("hbm", t * 4 * (2 + ncb // 2), "B"),
-        "tile_epilogue": ("hbm", 12 * kh * kw, "B"),
-        "sort_pack": ("hbm", t * (8 * ncb + 32), "B"),
+        "fft_rows": ("hbm", 12 * h * w + inter, "B"),            # RGB in, T out
+        "fft_cols": ("hbm", inter + stage, "B"),                  # T in, token staging out
+        "tile_epilogue": ("hbm", 12 * kh * kw + stage, "B"),
+        "sort_pack": ("hbm", stage + t * (8 * ncb + 32) + s / images_per_row, "B"),
         "pad_fill": ("hbm", s / images_per_row, "B"),
-        "encode_fused": ("hbm", encode_bytes_per_image(h, w, t, ncb, s, images_per_row), "B"),
     }
 
 
@@ -175,15 +176,23 @@ def main():
             imgs_per_launch = B * args.steps / kernels[dom]["launches"]
             per_launch = amt * imgs_per_launch
             avg_s = kernels[dom]["avg_ms"] / 1e3
+            traffic = None
+            pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
+            if os.path.exists(pmc_path):
+                pmc = json.load(open(pmc_path))
+                ent = pmc.get("kernels", {}).get(dom)
+                if ent and ent.get("images_per_dispatch"):
+                    # HBM bytes per launch from the committed rocprofv3 PMC passes, scaled per image
+                    traffic = round(ent["hbm_bytes_per_image"] * imgs_per_launch)
             if bound == "mfma":
                 ach = per_launch / avg_s / 1e12
                 roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF,
-                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": traffic,
                         "per_launch": f"{per_launch:.4g} flop ({imgs_per_launch:g} images)"}
             else:
                 ach = per_launch / avg_s / 1e9
                 roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "per_launch": f"{per_launch:.4g} B ({imgs_per_launch:g} images)"}
 
     cpu = None

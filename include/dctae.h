@@ -188,8 +188,9 @@ int dctae_norm_thresholds(dctae_ctx* ctx, const dctae_norm* norm, int64_t n, flo
  * 0 forces the MFMA GEMM DCT for every size (A/B and parity testing). */
 int dctae_set_fft(dctae_ctx* ctx, int enable);
 
-/* Target workspace bytes per chunk of FFT-path images (default 160 MiB) so
- * the row-pass output stays in the Infinity Cache for the column pass. */
+/* Target workspace bytes per chunk of FFT-path images (default: unlimited,
+ * one chunk; smaller chunks keep the row-pass output Infinity-Cache resident
+ * but measured slower on MI355X because of the extra launch boundaries). */
 int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
 
 /* Tuning / test knobs: "fft" (0/1), "fft_spec" (0/1: compile-time
