@@ -91,6 +91,13 @@ _SIGS = {
     "dctae_set_fft": ([_P, C.c_int], C.c_int),
     "dctae_set_chunk_bytes": ([_P, C.c_int64], C.c_int),
     "dctae_set_option": ([_P, C.c_char_p, C.c_int64], C.c_int),
+    "dctae_norm_batch_stats": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int64, _P, _P,
+                                _P], C.c_int),
+    "dctae_norm_batch_mad": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int64, _P, _P,
+                              _P], C.c_int),
+    "dctae_norm_merge": ([_P, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32, _P], C.c_int),
+    "dctae_norm_train_step": ([_P, C.POINTER(Norm), _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P,
+                               C.c_int64, _P, _P], C.c_int),
 }
 
 _lib = None

@@ -185,6 +185,79 @@ def norm_apply(x: torch.Tensor, channels: torch.Tensor, positions: torch.Tensor,
     return y
 
 
+def _stats_inputs(x, channels, positions, key_pad, p: FEParams):
+    dev = _check_dev(x, channels, positions)
+    PP = p.patch_size ** 2
+    if x.shape[-1] != PP:
+        raise AssertionError(f"token dim {x.shape[-1]} != patch_size**2")
+    xs = x.float().contiguous()
+    n = xs.numel() // PP
+    ch = channels.long().contiguous()
+    pos = positions.long().contiguous()
+    if ch.numel() != n or pos.numel() != 2 * n:
+        raise AssertionError("channels/positions do not match patches")
+    kp = None
+    if key_pad is not None:
+        kp = key_pad.to(device=dev, dtype=torch.bool).contiguous()
+        if kp.numel() != n:
+            raise AssertionError("key_pad_mask does not match patches")
+    return dev, xs, ch, pos, kp, n
+
+
+def norm_batch_stats(x, channels, positions, key_pad, p: FEParams):
+    """patchnorm.py:104-130 on the GPU: (batch_n (C,mh,mw), batch_median (C,mh,mw,P*P))."""
+    dev, xs, ch, pos, kp, n = _stats_inputs(x, channels, positions, key_pad, p)
+    ctx = _lib.context(dev)
+    PP = p.patch_size ** 2
+    bn = torch.empty(p.channels, p.max_patch_h, p.max_patch_w, device=dev)
+    bm = torch.empty(p.channels, p.max_patch_h, p.max_patch_w, PP, device=dev)
+    rc = ctx.lib.dctae_norm_batch_stats(ctx.h, p.patch_size, p.channels, p.max_patch_h, p.max_patch_w, ptr(xs),
+                                        ptr(ch), ptr(pos), ptr(kp), n, ptr(bn), ptr(bm), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_norm_batch_stats")
+    return bn, bm
+
+
+def norm_batch_mad(x, channels, positions, key_pad, median, p: FEParams):
+    """patchnorm.py:140-144 on the GPU: batch_b around `median` (C,mh,mw,P*P)."""
+    dev, xs, ch, pos, kp, n = _stats_inputs(x, channels, positions, key_pad, p)
+    ctx = _lib.context(dev)
+    med = median.float().contiguous()
+    bb = torch.empty_like(med)
+    rc = ctx.lib.dctae_norm_batch_mad(ctx.h, p.patch_size, p.channels, p.max_patch_h, p.max_patch_w, ptr(xs),
+                                      ptr(ch), ptr(pos), ptr(kp), n, ptr(med), ptr(bb), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_norm_batch_mad")
+    return bb
+
+
+def norm_merge_(table, batch, n, batch_n, n_update: bool):
+    """patchnorm.py:135-138 / 146-150 in place: table <- (table*n + batch*bn)/clamp(n+bn,1); n += bn."""
+    dev = _check_dev(table, batch, n, batch_n)
+    for t in (table, batch, n, batch_n):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise AssertionError("PatchNorm tables must be contiguous float32")
+    cells = n.numel()
+    PP = table.numel() // max(1, cells)
+    ctx = _lib.context(dev)
+    rc = ctx.lib.dctae_norm_merge(ctx.h, cells, PP, ptr(table), ptr(batch), ptr(n), ptr(batch_n), int(n_update),
+                                  _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_norm_merge")
+
+
+def norm_train_step(x, channels, positions, key_pad, n, median, b, p: FEParams, want_output=True):
+    """patchnorm.py:101-155 in one call: updates n / median / b in place,
+    returns x with the pad rows zeroed (or None)."""
+    dev, xs, ch, pos, kp, ntok = _stats_inputs(x, channels, positions, key_pad, p)
+    _check_dev(n, median, b)
+    ctx = _lib.context(dev)
+    y = torch.empty_like(xs) if want_output else None
+    st = NormState(median, b)
+    rc = ctx.lib.dctae_norm_train_step(ctx.h, C.byref(st.c()), ptr(n), p.patch_size, p.channels, p.max_patch_h,
+                                       p.max_patch_w, ptr(xs), ptr(ch), ptr(pos), ptr(kp), ntok, ptr(y),
+                                       _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_norm_train_step")
+    return y
+
+
 def check_device_errors(dev):
     ctx = _lib.context(dev)
     ctx.check(ctx.lib.dctae_check_device_errors(ctx.h, _lib.stream_ptr(dev)), "device index check")

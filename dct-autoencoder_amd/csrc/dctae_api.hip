@@ -62,6 +62,9 @@ struct dctae_ctx {
   int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
+  // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
+  uint8_t* st_ws = nullptr;
+  size_t st_bytes = 0;
   // cached encode plan
   std::vector<int64_t> enc_key;
   struct EncPlan* enc_plan = nullptr;
@@ -509,6 +512,7 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->plan_dev) hipFree(ctx->plan_dev);
   if (ctx->err_dev) hipFree(ctx->err_dev);
   if (ctx->fft_tab) hipFree(ctx->fft_tab);
+  if (ctx->st_ws) hipFree(ctx->st_ws);
   delete ctx->enc_plan;
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
@@ -1058,6 +1062,133 @@ int dctae_norm_forward(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_
 int dctae_norm_inverse(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t mh, int32_t mw, const float* y,
                        const int64_t* ch, const int64_t* pos, int64_t n, float* x, void* stream) {
   return norm_impl(ctx, norm, P, mh, mw, y, ch, pos, n, x, 1, stream);
+}
+
+// ---- PatchNorm training (patchnorm.py:101-155), kernels in dctae_stats.hip ----
+namespace {
+
+struct StatsScratch {
+  int32_t *cell, *count, *start, *list;
+  float* bn;       // (n_cells) batch counts
+  float *t0, *t1;  // two (n_cells, PP) tables (batch median / batch b)
+};
+
+int stats_scratch(dctae_ctx* ctx, int64_t n_tok, int n_cells, int PP, bool tables, hipStream_t s,
+                  StatsScratch* o) {
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t b_tok = al(sizeof(int32_t) * std::max<int64_t>(n_tok, 1));
+  const size_t b_cell = al(sizeof(int32_t) * n_cells);
+  const size_t b_tab = tables ? al(sizeof(float) * (size_t)n_cells * PP) : 0;
+  const size_t need = 2 * b_tok + 3 * b_cell + 2 * b_tab;
+  if (need > ctx->st_bytes) {
+    if (ctx->st_ws) {
+      HIPCHK(ctx, hipStreamSynchronize(s));
+      HIPCHK(ctx, hipFree(ctx->st_ws));
+      ctx->st_ws = nullptr;
+      ctx->st_bytes = 0;
+    }
+    HIPCHK(ctx, hipMalloc((void**)&ctx->st_ws, need));
+    ctx->st_bytes = need;
+  }
+  uint8_t* p = ctx->st_ws;
+  o->cell = (int32_t*)p;
+  p += b_tok;
+  o->list = (int32_t*)p;
+  p += b_tok;
+  o->count = (int32_t*)p;
+  p += b_cell;
+  o->start = (int32_t*)p;
+  p += b_cell;
+  o->bn = (float*)p;
+  p += b_cell;
+  o->t0 = tables ? (float*)p : nullptr;
+  p += b_tab;
+  o->t1 = tables ? (float*)p : nullptr;
+  return 0;
+}
+
+int stats_check(dctae_ctx* ctx, int32_t P, int32_t C, int32_t mh, int32_t mw, int64_t n_tok, const float* x,
+                const int64_t* ch, const int64_t* pos) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (P < 1 || C < 1 || mh < 1 || mw < 1 || n_tok < 0) return fail(ctx, DCTAE_EINVAL, "bad PatchNorm shape");
+  if ((int64_t)C * mh * mw > (1 << 30)) return fail(ctx, DCTAE_EINVAL, "PatchNorm table too large");
+  if (n_tok > (int64_t)INT32_MAX) return fail(ctx, DCTAE_EINVAL, "too many tokens for one statistics batch");
+  if (n_tok > 0 && (!x || !ch || !pos)) return fail(ctx, DCTAE_EINVAL, "NULL tensor");
+  return 0;
+}
+
+}  // namespace
+
+int dctae_norm_batch_stats(dctae_ctx* ctx, int32_t P, int32_t C, int32_t mh, int32_t mw, const float* x,
+                           const int64_t* ch, const int64_t* pos, const uint8_t* key_pad, int64_t n_tok,
+                           float* batch_n, float* batch_median, void* stream) {
+  if (int rc = stats_check(ctx, P, C, mh, mw, n_tok, x, ch, pos)) return rc;
+  if (!batch_n || !batch_median) return fail(ctx, DCTAE_EINVAL, "NULL output table");
+  hipStream_t s = (hipStream_t)stream;
+  const int n_cells = C * mh * mw, PP = P * P;
+  StatsScratch w;
+  if (int rc = stats_scratch(ctx, n_tok, n_cells, PP, false, s, &w)) return rc;
+  Timer t(ctx, s, "norm_batch_stats");
+  launch_stats_lists(ch, pos, key_pad, n_tok, C, mh, mw, w.cell, w.count, w.start, w.list, ctx->err_dev, s);
+  launch_stats_median(x, PP, n_cells, w.start, w.count, w.list, batch_median, batch_n, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_norm_batch_mad(dctae_ctx* ctx, int32_t P, int32_t C, int32_t mh, int32_t mw, const float* x,
+                         const int64_t* ch, const int64_t* pos, const uint8_t* key_pad, int64_t n_tok,
+                         const float* median, float* batch_b, void* stream) {
+  if (int rc = stats_check(ctx, P, C, mh, mw, n_tok, x, ch, pos)) return rc;
+  if (!median || !batch_b) return fail(ctx, DCTAE_EINVAL, "NULL table");
+  hipStream_t s = (hipStream_t)stream;
+  const int n_cells = C * mh * mw, PP = P * P;
+  StatsScratch w;
+  if (int rc = stats_scratch(ctx, n_tok, n_cells, PP, false, s, &w)) return rc;
+  Timer t(ctx, s, "norm_batch_mad");
+  launch_stats_lists(ch, pos, key_pad, n_tok, C, mh, mw, w.cell, w.count, w.start, w.list, ctx->err_dev, s);
+  launch_stats_batch_b(x, PP, n_cells, w.start, w.count, w.list, median, batch_b, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_norm_merge(dctae_ctx* ctx, int32_t n_cells, int32_t PP, float* table, const float* batch, float* n,
+                     const float* batch_n, int32_t n_update, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (n_cells < 0 || PP < 1) return fail(ctx, DCTAE_EINVAL, "bad PatchNorm shape");
+  if (n_cells == 0) return 0;
+  if (!n || !batch_n || ((!table || !batch) && PP > 0)) return fail(ctx, DCTAE_EINVAL, "NULL table");
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "norm_merge");
+  launch_stats_merge(table, batch, n, batch_n, n_cells, PP, s);
+  if (n_update) launch_stats_add(n, batch_n, n_cells, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_norm_train_step(dctae_ctx* ctx, const dctae_norm* norm, float* n_dev, int32_t P, int32_t C, int32_t mh,
+                          int32_t mw, const float* x, const int64_t* ch, const int64_t* pos, const uint8_t* key_pad,
+                          int64_t n_tok, float* y, void* stream) {
+  if (int rc = stats_check(ctx, P, C, mh, mw, n_tok, x, ch, pos)) return rc;
+  if (!norm || !norm->median_dev || !norm->b_dev || !n_dev) return fail(ctx, DCTAE_EINVAL, "PatchNorm tables are NULL");
+  hipStream_t s = (hipStream_t)stream;
+  const int n_cells = C * mh * mw, PP = P * P;
+  float* median = const_cast<float*>(norm->median_dev);
+  float* b = const_cast<float*>(norm->b_dev);
+  StatsScratch w;
+  if (int rc = stats_scratch(ctx, n_tok, n_cells, PP, true, s, &w)) return rc;
+  Timer t(ctx, s, "norm_train_step");
+  launch_stats_lists(ch, pos, key_pad, n_tok, C, mh, mw, w.cell, w.count, w.start, w.list, ctx->err_dev, s);
+  launch_stats_median(x, PP, n_cells, w.start, w.count, w.list, w.t0, w.bn, s);      // :112-130
+  launch_stats_merge(median, w.t0, n_dev, w.bn, n_cells, PP, s);                     // :135-138
+  launch_stats_batch_b(x, PP, n_cells, w.start, w.count, w.list, median, w.t1, s);   // :140-144
+  launch_stats_merge(b, w.t1, n_dev, w.bn, n_cells, PP, s);                          // :146-148
+  launch_stats_add(n_dev, w.bn, n_cells, s);                                         // :150
+  if (y && n_tok > 0) {                                                              // :153-155
+    if (key_pad) launch_zero_pads(x, key_pad, n_tok, PP, y, s);
+    else if (y != x) HIPCHK(ctx, hipMemcpyAsync(y, x, sizeof(float) * n_tok * PP, hipMemcpyDeviceToDevice, s));
+  }
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
 }
 
 int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, float* q, int64_t* idx,

@@ -26,6 +26,18 @@ void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float sc
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
 void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s);
 
+// PatchNorm training statistics (dctae_stats.hip)
+void launch_stats_lists(const int64_t* ch, const int64_t* pos, const uint8_t* key_pad, int64_t n_tok, int C, int mh,
+                        int mw, int32_t* cell, int32_t* count, int32_t* start, int32_t* list, int* err, hipStream_t s);
+void launch_stats_median(const float* x, int PP, int n_cells, const int32_t* start, const int32_t* count,
+                         const int32_t* list, float* batch_median, float* batch_n, hipStream_t s);
+void launch_stats_batch_b(const float* x, int PP, int n_cells, const int32_t* start, const int32_t* count,
+                          const int32_t* list, const float* median, float* batch_b, hipStream_t s);
+void launch_stats_merge(float* t, const float* src, const float* n, const float* bn, int n_cells, int PP,
+                        hipStream_t s);
+void launch_stats_add(float* n, const float* bn, int n_cells, hipStream_t s);
+void launch_zero_pads(const float* x, const uint8_t* key_pad, int64_t n_tok, int PP, float* y, hipStream_t s);
+
 size_t fft_kernel_setup(int device);
 void launch_fft_rows(const ImgDesc* imgs, const FftPlan* plans, const int2* blocks, int n_blocks, size_t lds,
                      const float* rgb, float* ws, const float2* tabs, const ColorMats& cm, hipStream_t s);

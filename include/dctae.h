@@ -150,6 +150,38 @@ int dctae_norm_inverse(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_
                        int32_t max_patch_w, const float* y_dev, const int64_t* channels_dev,
                        const int64_t* positions_dev, int64_t n, float* x_dev, void* stream);
 
+/* PatchNorm training statistics of one packed batch of n_tok tokens
+ * (patchnorm.py:101-130; replaces the reference's scatter_add_3d + per-cell
+ * torch.median loop).  key_pad_dev (n_tok bytes, nullable) marks padding.
+ * batch_n_dev: (C*mh*mw) fp32 token counts; batch_median_dev: (C*mh*mw, P*P)
+ * lower median per cell (0 for empty cells).  Bit-exact with the reference. */
+int dctae_norm_batch_stats(dctae_ctx* ctx, int32_t P, int32_t C, int32_t max_patch_h, int32_t max_patch_w,
+                           const float* x_dev, const int64_t* channels_dev, const int64_t* positions_dev,
+                           const uint8_t* key_pad_dev, int64_t n_tok, float* batch_n_dev,
+                           float* batch_median_dev, void* stream);
+
+/* Mean absolute deviation of the batch around the (already merged) running
+ * median (patchnorm.py:140-144): batch_b = sum_{tokens, batch order}
+ * |x - median| / clamp(batch_n, 1). */
+int dctae_norm_batch_mad(dctae_ctx* ctx, int32_t P, int32_t C, int32_t max_patch_h, int32_t max_patch_w,
+                         const float* x_dev, const int64_t* channels_dev, const int64_t* positions_dev,
+                         const uint8_t* key_pad_dev, int64_t n_tok, const float* median_dev, float* batch_b_dev,
+                         void* stream);
+
+/* Running merge (patchnorm.py:135-138 / 146-148): per cell,
+ * table <- (table*n + batch*batch_n) / clamp(n + batch_n, 1); then, if
+ * n_update, n <- n + batch_n (patchnorm.py:150). */
+int dctae_norm_merge(dctae_ctx* ctx, int32_t n_cells, int32_t PP, float* table_dev, const float* batch_dev,
+                     float* n_dev, const float* batch_n_dev, int32_t n_update, void* stream);
+
+/* One PatchNorm training forward (patchnorm.py:101-155, not frozen):
+ * updates norm->median_dev, norm->b_dev and n_dev (C*mh*mw) in place;
+ * y_dev (nullable) = x with padding rows zeroed. */
+int dctae_norm_train_step(dctae_ctx* ctx, const dctae_norm* norm, float* n_dev, int32_t P, int32_t C,
+                          int32_t max_patch_h, int32_t max_patch_w, const float* x_dev, const int64_t* channels_dev,
+                          const int64_t* positions_dev, const uint8_t* key_pad_dev, int64_t n_tok, float* y_dev,
+                          void* stream);
+
 /* LFQ.forward eval (lfq.py:136-227): quantized (n, dim) = +-scale (nullable)
  * and indices (n, num_codebooks) int64. */
 int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, int64_t n,

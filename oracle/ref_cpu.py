@@ -417,14 +417,15 @@ def _scatter_cells(acc: torch.Tensor, ch, hi, wi, vals: Optional[torch.Tensor] =
     acc.view(c * h * w, z).scatter_add_(0, idx, vals)
 
 
-def norm_train_step(t: NormTables, patches, channels, h_idx, w_idx, key_pad_mask) -> NormTables:
-    """patchnorm.py:101-155: one training-mode update of n / median / b."""
+def norm_batch_stats(shape, patches, channels, h_idx, w_idx, key_pad_mask):
+    """patchnorm.py:104-130: (batch_n, batch_median) of the non-pad tokens;
+    batch_median is torch.median(0) (lower median) per occupied cell."""
     keep = ~key_pad_mask
     ch, hi, wi, x = channels[keep], h_idx[keep], w_idx[keep], patches[keep]
-    c, h, w = t.n.shape
+    c, h, w, z = shape
     batch_n = torch.zeros(c, h, w, dtype=x.dtype)
     _scatter_cells(batch_n.unsqueeze(-1), ch, hi, wi)
-    batch_median = torch.zeros_like(t.median)
+    batch_median = torch.zeros(c, h, w, z, dtype=x.dtype)
     cell = ch * h * w + hi * w + wi
     order = torch.sort(cell, stable=True).indices
     cs = cell[order]
@@ -436,15 +437,31 @@ def norm_train_step(t: NormTables, patches, channels, h_idx, w_idx, key_pad_mask
         cc, rem = divmod(u, h * w)
         hh, ww = divmod(rem, w)
         batch_median[cc, hh, ww] = rows.median(0).values                   # lower median
-    n_old = t.n
-    denom = (n_old + batch_n).clamp(1).unsqueeze(-1)
-    median = (t.median * n_old.unsqueeze(-1) + batch_median * batch_n.unsqueeze(-1)) / denom
+    return batch_n, batch_median
+
+
+def norm_batch_mad(median, patches, channels, h_idx, w_idx, key_pad_mask, batch_n):
+    """patchnorm.py:140-144: scatter_add of |x - median| / clamp(batch_n, 1)."""
+    keep = ~key_pad_mask
+    ch, hi, wi, x = channels[keep], h_idx[keep], w_idx[keep], patches[keep]
     dist = (x - median[ch, hi, wi]).abs()
-    batch_b = torch.zeros_like(t.b)
+    batch_b = torch.zeros_like(median)
     _scatter_cells(batch_b, ch, hi, wi, dist)
-    batch_b = batch_b / batch_n.unsqueeze(-1).clamp(1)
-    b = (t.b * n_old.unsqueeze(-1) + batch_b * batch_n.unsqueeze(-1)) / denom
-    return NormTables(n_old + batch_n, median, b, t.eps, t.max_val, t.min_val)
+    return batch_b / batch_n.unsqueeze(-1).clamp(1)
+
+
+def norm_merge(table, n, batch, batch_n):
+    """patchnorm.py:135-138 / 146-148: (t*n + s*bn) / clamp(n + bn, 1)."""
+    return (table * n.unsqueeze(-1) + batch * batch_n.unsqueeze(-1)) / (n + batch_n).clamp(1).unsqueeze(-1)
+
+
+def norm_train_step(t: NormTables, patches, channels, h_idx, w_idx, key_pad_mask) -> NormTables:
+    """patchnorm.py:101-155: one training-mode update of n / median / b."""
+    batch_n, batch_median = norm_batch_stats(tuple(t.median.shape), patches, channels, h_idx, w_idx, key_pad_mask)
+    median = norm_merge(t.median, t.n, batch_median, batch_n)
+    batch_b = norm_batch_mad(median, patches, channels, h_idx, w_idx, key_pad_mask, batch_n)
+    b = norm_merge(t.b, t.n, batch_b, batch_n)
+    return NormTables(t.n + batch_n, median, b, t.eps, t.max_val, t.min_val)
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,149 @@
+"""Multi-process (gloo, CPU) tests of the data-parallel PatchNorm fit
+(dct-autoencoder_amd/distributed.py).
+
+Contract checked: R ranks, each holding one shard of a packed batch, end
+with tables bit-identical to the reference's single-process training update
+(patchnorm.py:101-155, restated by oracle.ref_cpu.norm_train_step) applied to
+the shards as consecutive batches in rank order.  The per-shard statistics
+come from an oracle-backed StatsOps here (no GPU in this container); on the
+GPU the same exchange runs with the HIP kernels (test_gpu_stats.py checks
+those kernels against the same oracle functions bit-exactly).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ref_cpu
+
+SHAPE = (3, 6, 5, 16)   # C, mh, mw, P*P (P = 4)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batch(seed, rows, seq, integer=False):
+    """Packed batch: random cells, duplicate cells within and across rows,
+    padding at row tails; integer-valued patches give many median ties."""
+    g = torch.Generator().manual_seed(seed)
+    c, mh, mw, z = SHAPE
+    ch = torch.randint(0, c, (rows, seq), generator=g)
+    h = torch.randint(0, mh, (rows, seq), generator=g)
+    w = torch.randint(0, mw, (rows, seq), generator=g)
+    x = torch.randn(rows, seq, z, generator=g) * 3
+    if integer:
+        x = torch.round(x)
+    kp = torch.zeros(rows, seq, dtype=torch.bool)
+    for r in range(rows):
+        n_pad = int(torch.randint(0, seq // 2, (1,), generator=g))
+        if n_pad:
+            kp[r, seq - n_pad:] = True
+    x[kp] = 0
+    return x, ch, h, w, kp
+
+
+def _oracle_ops():
+    from importlib import import_module
+    import _pkgload
+    _pkgload.load()
+    D = import_module("dct_autoencoder_amd.distributed")
+
+    def batch_stats(x, ch, pos, kp):
+        return ref_cpu.norm_batch_stats(SHAPE, x, ch, pos[..., 0], pos[..., 1], kp)
+
+    def batch_mad(x, ch, pos, kp, med, bn):
+        return ref_cpu.norm_batch_mad(med, x, ch, pos[..., 0], pos[..., 1], kp, bn)
+
+    def merge_(table, batch, n, bn, n_update):
+        table.copy_(ref_cpu.norm_merge(table, n, batch, bn))
+        if n_update:
+            n.copy_(n + bn)
+
+    return D, D.StatsOps(batch_stats, batch_mad, merge_)
+
+
+def _start_tables(seed):
+    c, mh, mw, z = SHAPE
+    if seed is None:
+        return torch.zeros(c, mh, mw), torch.zeros(SHAPE), torch.ones(SHAPE)
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randint(0, 5, (c, mh, mw), generator=g).float(), torch.randn(SHAPE, generator=g),
+            torch.rand(SHAPE, generator=g) + 0.5)
+
+
+def _worker(rank, world, port, case, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        D, ops = _oracle_ops()
+        seed, rows, seq, integer, start = case
+        x, ch, h, w, kp = _batch(seed, rows * world, seq, integer)
+        sl = slice(rank * rows, (rank + 1) * rows)
+        pos = torch.stack([h, w], -1)
+        n, med, b = _start_tables(start)
+        n2, med2, b2 = D.fit_tables(n, med, b, x[sl], ch[sl], pos[sl], kp[sl], ops)
+        q.put((rank, n2, med2, b2))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, *t = q.get(timeout=240)
+        res[r] = t
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+CASES = {
+    "fresh": (1, 3, 40, False, None),
+    "running_ties": (2, 2, 64, True, 7),
+}
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name", list(CASES))
+def test_distributed_fit_equals_sequential_reference(world, name):
+    case = CASES[name]
+    seed, rows, seq, integer, start = case
+    res = _run(world, case)
+    x, ch, h, w, kp = _batch(seed, rows * world, seq, integer)
+    n, med, b = _start_tables(start)
+    t = ref_cpu.NormTables(n, med, b)
+    for r in range(world):
+        sl = slice(r * rows, (r + 1) * rows)
+        t = ref_cpu.norm_train_step(t, x[sl], ch[sl], h[sl], w[sl], kp[sl])
+    for r in range(world):
+        n2, med2, b2 = res[r]
+        assert torch.equal(n2, t.n)
+        assert torch.equal(med2, t.median), f"rank {r} median differs"
+        assert torch.equal(b2, t.b), f"rank {r} b differs"
+
+
+def test_single_process_composition_equals_train_step():
+    """The three oracle sub-steps composed like dctae_norm_train_step give the
+    oracle's (reference-pinned) training update."""
+    x, ch, h, w, kp = _batch(5, 4, 50, True)
+    n, med, b = _start_tables(3)
+    t = ref_cpu.norm_train_step(ref_cpu.NormTables(n, med, b), x, ch, h, w, kp)
+    bn, bm = ref_cpu.norm_batch_stats(SHAPE, x, ch, h, w, kp)
+    med2 = ref_cpu.norm_merge(med, n, bm, bn)
+    bb = ref_cpu.norm_batch_mad(med2, x, ch, h, w, kp, bn)
+    b2 = ref_cpu.norm_merge(b, n, bb, bn)
+    assert torch.equal(med2, t.median) and torch.equal(b2, t.b) and torch.equal(n + bn, t.n)
