@@ -59,7 +59,10 @@ struct dctae_ctx {
   bool fft_spec_enabled = true;
   int rows_prefetch = 0;
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
-  int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)              // k_fft_rows2: prefetch the next row (more VGPRs, fewer waves)       // use the compile-time specialised kernels when a plan matches
+  int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)
+  int cols_kernel = 4;                // specialised column kernel: 2 (LDS scatter), 3 (persistent), 4 (linear addresses)
+  int cols_persist = 4;               // cols_kernel 3: blocks per CU
+  int n_cu = 256;                     // compute units of the device
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
@@ -496,6 +499,11 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
     return DCTAE_EHIP;
   }
   c->lds_limit = fft_kernel_setup(device);
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->n_cu = cu;
+    hipGetLastError();
+  }
   hipEventRecord(c->plan_evt, 0);
   *out = c;
   return 0;
@@ -565,6 +573,8 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
   else if (k == "t_layout" && value >= 0 && value <= 2) ctx->t_layout = (int)value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
+  else if (k == "cols_persist" && value >= 1 && value <= 16) ctx->cols_persist = (int)value;
+  else if (k == "cols_kernel" && value >= 2 && value <= 4) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -1010,7 +1020,11 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       if (j.n_fc[v]) {
         Timer t(ctx, s, "fft_cols");
         launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
-                             ctx->fft_tab + j.post_off_c[v], epj, sk, s);
+                             ctx->fft_tab + j.post_off_c[v], epj, sk, s,
+                             ctx->t_layout == 2 || ctx->cols_kernel == 2 ? 0
+                             : ctx->cols_kernel == 3                     ? ctx->cols_persist * ctx->n_cu
+                                                                         : -1,
+                             ctx->t_layout);
       }
   }
   if (full && E.n_img > 0) {

@@ -1,4 +1,5 @@
 // Compile-time specialised two-pass FFT-DCT kernels (M = N/2 = R1 * R2,
+#include <type_traits>
 // at most 64/3 butterflies per job and pass) for the headline image sizes:
 //   N = 512: M = 256 = 16 x 16        N = 224: M = 112 = 16 x 7
 // Same maths as dctae_fft.hip (Makhoul + Stockham), but every index is a
@@ -344,6 +345,374 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// cols, linear-address form: every LDS address is (lane base) + (compile-time
+// constant), so address arithmetic folds into the ds_read / ds_write offset
+// fields instead of costing VALU (the column kernel is VALU-issue bound).
+//  * the T slice is copied to LDS in natural row order (row y at y*KSP);
+//  * Makhoul's reorder v[n] = x[2n] / x[2N-1-2n] is applied by pass 1's read
+//    addresses: z[m] = (v[2m], v[2m+1]) with m = jj + B1 r is rows
+//    4jj + 4B1 r (+2) for r < 8 and 2N-1-4jj-4B1 r (-2) for r >= 8;
+//  * passes and post-processing use the padded complex layout pad16(m),
+//    which is linear in the unrolled index for every access made here.
+// Row-major T only (t_layout 0); P = 14 tile columns per block.
+// ---------------------------------------------------------------------------
+template <int N, int R2, int KS>
+__global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+#pragma clang fp contract(fast)
+  constexpr int R1 = 16;
+  constexpr int M = N / 2;
+  constexpr int B1 = M / R1, B2 = M / R2;
+  constexpr int KSP = KS | 1;
+  constexpr int ZROWS = 2 * (pad16(M - 1) + 1);
+  constexpr int M16 = M / 16;
+  static_assert(M % 16 == 0 && B2 == 16 && B1 <= 16 && KS == 14, "plan shape");
+  static_assert(N * KSP <= ZROWS * KSP, "natural rows fit the complex layout");
+  __shared__ float zs[ZROWS * KSP];
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
+  const int tid = threadIdx.x;
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const int c = jb.y, strip = jb.z;
+  // LFQ-bit thresholds of this thread's epilogue rows (latency hidden behind the transform)
+  constexpr int EPR = 2;
+  const int g16 = tid >> 4, jl = tid & 15;
+  const bool use_thr = ep.median && ep.thr && !sk.norm;
+  float2 thr_r[EPR][KS / 2];
+#pragma unroll
+  for (int r = 0; r < EPR; ++r)
+#pragma unroll
+    for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = make_float2(0.0f, 0.0f);
+  if (use_thr) {
+#pragma unroll
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh && jl < KS) {
+        const float2* t2 = reinterpret_cast<const float2*>(
+            ep.thr + ((((int64_t)c * ep.maxph + h) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jl * KS);
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
+      }
+    }
+  }
+  for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
+  for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
+  // ---- T slice -> LDS, natural row order: thread (y0 = t / 7, p = t % 7) copies rows y0 + 32k
+  if (tid < 32 * (KS / 2)) {
+    const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
+    const float2* src = reinterpret_cast<const float2*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
+    const int64_t rstep = (int64_t)16 * d.Kw;   // 32 rows, in float2
+    float* dst = zs + y0 * KSP + 2 * p;
+    float2 tv[N / 32];
+#pragma unroll
+    for (int k = 0; k < N / 32; ++k) tv[k] = src[k * rstep];
+#pragma unroll
+    for (int k = 0; k < N / 32; ++k) {
+      dst[32 * KSP * k] = tv[k].x;
+      dst[32 * KSP * k + 1] = tv[k].y;
+    }
+  }
+  __syncthreads();
+  const int jj = tid & 15, col = tid >> 4;
+  const bool on_col = col < KS;
+  // ---- pass 1 (Ns = 1), Makhoul reorder folded into the read addresses
+  {
+    float2 v[R1];
+    const bool on = on_col && jj < B1;
+    if (on) {
+      const float* lo = zs + 4 * jj * KSP + col;                  // rows 4jj + 4B1 r (+2 KSP: row + 2)
+      const float* hi = zs + (2 * N - 1 - 4 * jj) * KSP + col;    // rows 2N-1-4jj-4B1 r (-2)
+#pragma unroll
+      for (int r = 0; r < R1 / 2; ++r) v[r] = make_float2(lo[4 * B1 * r * KSP], lo[(4 * B1 * r + 2) * KSP]);
+#pragma unroll
+      for (int r = R1 / 2; r < R1; ++r)
+        v[r] = make_float2(hi[-4 * B1 * r * KSP], hi[-(4 * B1 * r + 2) * KSP]);
+      DFT<R1>::run(v);
+    }
+    __syncthreads();
+    if (on) {
+      float* o = zs + 2 * 17 * jj * KSP + col;                     // z[16 jj + r]: pad16 = 17 jj + r
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        o[2 * r * KSP] = v[r].x;
+        o[(2 * r + 1) * KSP] = v[r].y;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- pass 2 (Ns = 16): z[jj + 16 r], pad16 = jj + 17 r
+  {
+    float2 v[R2];
+    const bool on = on_col;
+    float* z = zs + 2 * jj * KSP + col;
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R2; ++r) v[r] = make_float2(z[2 * 17 * r * KSP], z[(2 * 17 * r + 1) * KSP]);
+#pragma unroll
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
+      DFT<R2>::run(v);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < R2; ++r) {
+        z[2 * 17 * r * KSP] = v[r].x;
+        z[(2 * 17 * r + 1) * KSP] = v[r].y;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- Makhoul post-processing: k = jj + 16 i, A = Z[k] (pad16 = jj + 17 i),
+  //      B = conj Z[M - k] (pad16 = bb - 17 i); k = 0 and k = M use Z[0]
+  constexpr int KPL = M16 + 1;
+  float2 wv[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) wv[i] = make_float2(0.0f, 0.0f);
+  if (on_col) {
+    const float* za = zs + 2 * jj * KSP + col;
+    const int bb = M + M16 - 1 - jj + (jj == 0 ? 1 : 0);
+    const float* zb = zs + 2 * bb * KSP + col;
+    const float2* ps = post_s + 2 * jj;
+#pragma unroll
+    for (int i = 0; i < M16; ++i) {
+      const float2 A = make_float2(za[2 * 17 * i * KSP], za[(2 * 17 * i + 1) * KSP]);
+      float2 B;
+      if (i == 0) {
+        const float* zb0 = jj == 0 ? zs + col : zb;
+        B = make_float2(zb0[0], -zb0[KSP]);
+      } else {
+        B = make_float2(zb[-2 * 17 * i * KSP], -zb[(-2 * 17 * i + 1) * KSP]);
+      }
+      const float2 al = ps[32 * i], be = ps[32 * i + 1];
+      wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+    }
+    if (jj == 0) {  // k = M
+      const float2 A = make_float2(zs[col], zs[KSP + col]);
+      const float2 B = make_float2(A.x, -A.y);
+      wv[M16] = cadd(cmul(post_s[2 * M], cadd(A, B)), cmul(post_s[2 * M + 1], csub(A, B)));
+    }
+  }
+  __syncthreads();
+  const int Kh = d.Kh;
+  if (on_col) {
+    float* xo = zs + jj * KSP + col;                 // X[k] at row k (natural layout)
+    float* xn = zs + (N - jj) * KSP + col;           // X[N - k]
+#pragma unroll
+    for (int i = 0; i < M16; ++i) {
+      const int k = jj + 16 * i;
+      if (k < Kh) xo[16 * i * KSP] = wv[i].x;
+      if (k >= 1 && N - k < Kh) xn[-16 * i * KSP] = -wv[i].y;
+    }
+    if (jj == 0 && M < Kh) zs[M * KSP + col] = wv[M16].x;
+  }
+  __syncthreads();
+  // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
+  if (use_thr && d.qh <= 16 * EPR) {
+#pragma unroll
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh) {
+        float vals[KS];
+        const float* row = zs + (KS * h + jl) * KSP;
+#pragma unroll
+        for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? row[p2] : 0.0f;
+        const int f = (h * d.qw + strip) * ep.C + c;
+        token_epilogue_thr<KS>(ep, c, h, strip, jl, vals, thr_r[r], d.tok_off + f, sk);
+      }
+    }
+  } else {
+    for (int h = g16; h < d.qh; h += 16) {
+      float vals[KS];
+#pragma unroll
+      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
+      const int f = (h * d.qw + strip) * ep.C + c;
+      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cols, persistent: a grid of about 4 blocks per CU walks the same item list
+// (image, channel, tile column); the T slice of the block's NEXT item is
+// loaded into registers while the current one is transformed, so the HBM
+// latency of the 28 KB slice hides behind the FFT / epilogue of the previous
+// item instead of stalling each block's start.  LAY 0: row-major T (KS/2
+// float2 per row), LAY 1: contiguous strips (float4).
+// ---------------------------------------------------------------------------
+template <int N, int R1, int R2, int KS, int LAY>
+__global__ __launch_bounds__(256) void k_fft_cols3(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                   int n_items, const float* __restrict__ ws,
+                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                   EncParams ep, TokenSinks sk) {
+  constexpr int M = N / 2;
+  constexpr int B1 = M / R1, B2 = M / R2;
+  constexpr int KSP = KS | 1;
+  constexpr int ZROWS = 2 * (pad16(M - 1) + 1);
+  static_assert(KS * 16 <= 256 && (KS % 2) == 0, "16 butterfly lanes per column, even tile");
+  static_assert(B1 <= 16 && B2 <= 16 && R1 == 16, "plan shape");
+  using PF = typename std::conditional<LAY == 1, float4, float2>::type;
+  constexpr int PER = LAY == 1 ? 4 : 2;              // floats per prefetch element
+  constexpr int NQ = N * KS / PER;                   // prefetch elements per item
+  constexpr int NPF = (NQ + 255) / 256;
+  __shared__ float zs[ZROWS * KSP];
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
+  for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
+  auto zre = [&](int m, int col) -> float& { return zs[2 * pad16(m) * KSP + col]; };
+  auto zim = [&](int m, int col) -> float& { return zs[(2 * pad16(m) + 1) * KSP + col]; };
+  auto put = [&](int y, int j, float v) {
+    const int vv = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
+    zs[(2 * pad16(vv >> 1) + (vv & 1)) * KSP + j] = v;
+  };
+  PF pf[NPF];
+  auto prefetch = [&](int it, int tid) {
+    const int4 jb = blocks[it];
+    const ImgDesc& d = imgs[jb.x];
+    const float* base = ws + d.ws_t + (int64_t)jb.y * d.H * d.Kw;
+    if (LAY == 1) {
+      const float4* T4 = reinterpret_cast<const float4*>(base + (int64_t)jb.z * N * KS);
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int q = tid + 256 * u;
+        if (NQ % 256 == 0 || q < NQ) pf[u] = *reinterpret_cast<const PF*>(T4 + q);
+      }
+    } else {
+      const float2* T2 = reinterpret_cast<const float2*>(base + jb.z * KS);
+      const int rs = d.Kw / 2;
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int q = tid + 256 * u;
+        const int y = q / (KS / 2), p = q - y * (KS / 2);
+        if (NQ % 256 == 0 || q < NQ) pf[u] = *reinterpret_cast<const PF*>(T2 + (int64_t)y * rs + p);
+      }
+    }
+  };
+  auto scatter = [&](int tid) {
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int q = tid + 256 * u;
+      if (NQ % 256 == 0 || q < NQ) {
+        if (LAY == 1) {
+          const float* tv = reinterpret_cast<const float*>(&pf[u]);
+#pragma unroll
+          for (int v = 0; v < PER; ++v) {
+            const int e = PER * q + v;
+            const int y = e / KS, j = e - y * KS;
+            put(y, j, tv[v]);
+          }
+        } else {
+          const int y = q / (KS / 2), p = q - y * (KS / 2);
+          const float* tv = reinterpret_cast<const float*>(&pf[u]);
+          put(y, 2 * p, tv[0]);
+          put(y, 2 * p + 1, tv[1]);
+        }
+      }
+    }
+  };
+  int it = blockIdx.x;
+  if (it < n_items) prefetch(it, tid);
+#pragma unroll 1
+  for (; it < n_items; it += gridDim.x) {
+    // opaque per-iteration copy of the thread id: keeps the compiler from
+    // hoisting every derived LDS / global address out of the loop (which
+    // costs more registers than recomputing them)
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    const int jj = t & 15, col = t >> 4;
+    const bool on_col = col < KS;
+    const int g16 = t >> 4, jl = t & 15;
+    const int4 jb = blocks[it];
+    const ImgDesc d = imgs[jb.x];
+    const int c = jb.y, strip = jb.z;
+    __syncthreads();  // zs free again (previous epilogue), tables in LDS (first item)
+    scatter(t);
+    if (it + (int)gridDim.x < n_items) prefetch(it + gridDim.x, t);
+    __syncthreads();
+    {  // pass 1 (Ns = 1)
+      // every array below is fully initialised inside the loop: a
+      // conditionally assigned one becomes a loop-carried register set
+      float2 v[R1];
+#pragma unroll
+      for (int r = 0; r < R1; ++r) v[r] = make_float2(0.0f, 0.0f);
+      const bool on = on_col && jj < B1;
+      if (on) {
+#pragma unroll
+        for (int r = 0; r < R1; ++r) v[r] = make_float2(zre(jj + r * B1, col), zim(jj + r * B1, col));
+        DFT<R1>::run(v);
+      }
+      __syncthreads();
+      if (on) {
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+          zre(jj * R1 + r, col) = v[r].x;
+          zim(jj * R1 + r, col) = v[r].y;
+        }
+      }
+      __syncthreads();
+    }
+    {  // pass 2 (Ns = R1)
+      float2 v[R2];
+#pragma unroll
+      for (int r = 0; r < R2; ++r) v[r] = make_float2(0.0f, 0.0f);
+      const bool on = on_col && jj < B2;
+      if (on) {
+#pragma unroll
+        for (int r = 0; r < R2; ++r) v[r] = make_float2(zre(jj + r * B2, col), zim(jj + r * B2, col));
+#pragma unroll
+        for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
+        DFT<R2>::run(v);
+      }
+      __syncthreads();
+      if (on) {
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {
+          zre(jj + r * R1, col) = v[r].x;
+          zim(jj + r * R1, col) = v[r].y;
+        }
+      }
+      __syncthreads();
+    }
+    constexpr int KPL = (M + 1 + 15) / 16;
+    float2 wv[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) wv[i] = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = jj + 16 * i;
+      if (on_col && k <= M) {
+        const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
+        const float2 A = make_float2(zre(ka, col), zim(ka, col));
+        const float2 B = make_float2(zre(kb, col), -zim(kb, col));
+        const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
+        wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+      }
+    }
+    __syncthreads();
+    const int Kh = d.Kh;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = jj + 16 * i;
+      if (on_col && k <= M) {
+        if (k < Kh) zs[k * KSP + col] = wv[i].x;
+        if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KSP + col] = -wv[i].y;
+      }
+    }
+    __syncthreads();
+    for (int h = g16; h < d.qh; h += 16) {
+      float vals[KS];
+#pragma unroll
+      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
+      const int f = (h * d.qw + strip) * ep.C + c;
+      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
 
@@ -371,8 +740,28 @@ void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int
 
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
-                          hipStream_t s) {
+                          hipStream_t s, int persist_grid, int layout) {
   if (n_blocks <= 0) return;
+  if (persist_grid < 0 && layout != 0) persist_grid = 0;  // linear kernel: row-major T only
+  if (persist_grid < 0) {
+    if (spec == 1)
+      hipLaunchKernelGGL((k_fft_cols4<512, 16, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
+    else if (spec == 2)
+      hipLaunchKernelGGL((k_fft_cols4<224, 7, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
+    return;
+  }
+  if (persist_grid > 0) {
+    const int g = std::min(n_blocks, persist_grid);
+    if (spec == 1 && layout == 1)
+      hipLaunchKernelGGL((k_fft_cols3<512, 16, 16, 14, 1>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
+    else if (spec == 1)
+      hipLaunchKernelGGL((k_fft_cols3<512, 16, 16, 14, 0>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
+    else if (spec == 2 && layout == 1)
+      hipLaunchKernelGGL((k_fft_cols3<224, 16, 7, 14, 1>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
+    else if (spec == 2)
+      hipLaunchKernelGGL((k_fft_cols3<224, 16, 7, 14, 0>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
+    return;
+  }
   if (spec == 1)
     hipLaunchKernelGGL((k_fft_cols2<512, 16, 16, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
   else if (spec == 2)

@@ -362,13 +362,30 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
+SPEC_VARIANTS = {  # option sets of the specialised kernels, with the defaults they are reset to
+    "default": ({}, {}),
+    "cols_lds_scatter": ({"cols_kernel": 2}, {"cols_kernel": 4}),
+    "cols_persistent": ({"cols_kernel": 3}, {"cols_kernel": 4}),
+    "t_strips": ({"t_layout": 1}, {"t_layout": 0}),
+    "t_strips16": ({"t_layout": 2}, {"t_layout": 0}),
+}
+
+
+@pytest.mark.parametrize("variant", list(SPEC_VARIANTS))
 @pytest.mark.parametrize("shape", [(512, 512), (224, 224)])
-def test_specialised_kernels_match_generic(fe, pn, lfq, shape):
+def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
     """dctae_fft2.hip (compile-time plans) vs dctae_fft.hip (runtime plans):
     same algorithm, different op order -> tokens within 1e-6 * max|Y|."""
     ops = _ops()
     x = torch.from_numpy(np.stack(rng.synth_images(53, [shape] * 3))).to(DEV)
-    ((dp_s, c_s),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
+    on, off = SPEC_VARIANTS[variant]
+    for k, v in on.items():
+        ops.set_option(k, v)
+    try:
+        ((dp_s, c_s),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
+    finally:
+        for k, v in off.items():
+            ops.set_option(k, v)
     ops.set_option("fft_spec", 0)
     try:
         ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
