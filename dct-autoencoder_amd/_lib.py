@@ -13,7 +13,8 @@ from typing import Dict, Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdctae.so")
+# DCTAE_LIBRARY: another build of the same ABI (e.g. a profiling variant)
+LIB_PATH = os.environ.get("DCTAE_LIBRARY") or os.path.join(_HERE, "libdctae.so")
 ABI_VERSION = 1
 
 

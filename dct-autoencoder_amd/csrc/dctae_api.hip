@@ -59,10 +59,9 @@ struct dctae_ctx {
   bool fft_spec_enabled = true;
   int rows_prefetch = 0;
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
-  int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16)
-  int cols_kernel = 4;                // specialised column kernel: 2 (LDS scatter), 3 (persistent), 4 (linear addresses)
-  int cols_persist = 4;               // cols_kernel 3: blocks per CU
-  int n_cu = 256;                     // compute units of the device
+  int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16),
+                                      // 3 row-major with each tile column padded to 16 floats (64-B segments)
+  int cols_kernel = 4;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses)
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
@@ -499,11 +498,6 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
     return DCTAE_EHIP;
   }
   c->lds_limit = fft_kernel_setup(device);
-  {
-    int cu = 0;
-    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->n_cu = cu;
-    hipGetLastError();
-  }
   hipEventRecord(c->plan_evt, 0);
   *out = c;
   return 0;
@@ -571,10 +565,9 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "fft_spec") ctx->fft_spec_enabled = value != 0;
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
-  else if (k == "t_layout" && value >= 0 && value <= 2) ctx->t_layout = (int)value;
+  else if (k == "t_layout" && value >= 0 && value <= 3) ctx->t_layout = (int)value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
-  else if (k == "cols_persist" && value >= 1 && value <= 16) ctx->cols_persist = (int)value;
-  else if (k == "cols_kernel" && value >= 2 && value <= 4) ctx->cols_kernel = (int)value;
+  else if (k == "cols_kernel" && (value == 2 || value == 4)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -748,7 +741,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     for (int i = j.i0; i < j.i1; ++i) {
       ImgDesc& d = D[i];
       d.ws_t = wsf;
-      wsf += up(3ll * (d.t_strips == 2 ? (d.Kw / 14) * 16 : d.Kw) * d.H);
+      wsf += up(3ll * (d.t_strips >= 2 ? (d.Kw / 14) * 16 : d.Kw) * d.H);
       d.ws_p = wsf;
       if (d.plan_w < 0) wsf += up(3ll * d.H * d.W);
       d.ws_y = wsf;
@@ -1021,10 +1014,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         Timer t(ctx, s, "fft_cols");
         launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
                              ctx->fft_tab + j.post_off_c[v], epj, sk, s,
-                             ctx->t_layout == 2 || ctx->cols_kernel == 2 ? 0
-                             : ctx->cols_kernel == 3                     ? ctx->cols_persist * ctx->n_cu
-                                                                         : -1,
-                             ctx->t_layout);
+                             ctx->cols_kernel, ctx->t_layout);
       }
   }
   if (full && E.n_img > 0) {

@@ -1,5 +1,4 @@
 // Compile-time specialised two-pass FFT-DCT kernels (M = N/2 = R1 * R2,
-#include <type_traits>
 // at most 64/3 butterflies per job and pass) for the headline image sizes:
 //   N = 512: M = 256 = 16 x 16        N = 224: M = 112 = 16 x 7
 // Same maths as dctae_fft.hip (Makhoul + Stockham), but every index is a
@@ -8,6 +7,11 @@
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
 #include "dctae_launch.h"
+
+// profiling builds only (tools/gpu_ablate.sh): skip parts of the column kernel
+#ifndef DCTAE_ABLATE
+#define DCTAE_ABLATE 0
+#endif
 
 namespace dctae {
 
@@ -49,8 +53,8 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   const int64_t hw = (int64_t)H * N;
   const float* src = rgb + d.rgb_off;
   const float gam = 0.430000007152557373046875f;
-  const int lay = d.t_strips;               // 0 row-major, 1 strips of 14, 2 strips padded to 16
-  const int SW = (lay == 2) ? 16 : 14;       // strip row width (floats)
+  const int lay = d.t_strips;               // 0 row-major, 1 strips of 14, 2 strips padded to 16, 3 padded row-major
+  const int SW = (lay >= 2) ? 16 : 14;       // strip row width (floats)
   // ---- lane-invariant index maps (the same for every row)
   int zo[PX];                               // Makhoul slot of pixel lane + 64 i
 #pragma unroll
@@ -65,12 +69,13 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   for (int i = 0; i < KI; ++i) {
     const int k = lane + 64 * i;
     const int kx2 = N - k;
-    oa[i] = (k < Kw) ? (lay ? (k / 14) * H * SW + k % 14 : k) : -1;
-    ob[i] = (k >= 1 && kx2 < Kw) ? (lay ? (kx2 / 14) * H * SW + kx2 % 14 : kx2) : -1;
+    oa[i] = (k < Kw) ? (lay == 3 ? (k / 14) * 16 + k % 14 : lay ? (k / 14) * H * SW + k % 14 : k) : -1;
+    ob[i] = (k >= 1 && kx2 < Kw) ? (lay == 3 ? (kx2 / 14) * 16 + kx2 % 14 : lay ? (kx2 / 14) * H * SW + kx2 % 14 : kx2)
+                                 : -1;
   }
-  const int oM = (M < Kw) ? (lay ? (M / 14) * H * SW + M % 14 : M) : -1;
-  const int ystride = lay ? SW : Kw;        // T offset step per row
-  const int64_t cstride = lay == 2 ? (int64_t)H * (Kw / 14) * 16 : (int64_t)H * Kw;  // per channel
+  const int oM = (M < Kw) ? (lay == 3 ? (M / 14) * 16 + M % 14 : lay ? (M / 14) * H * SW + M % 14 : M) : -1;
+  const int ystride = lay == 3 ? (Kw / 14) * 16 : lay ? SW : Kw;   // T offset step per row
+  const int64_t cstride = lay >= 2 ? (int64_t)H * (Kw / 14) * 16 : (int64_t)H * Kw;  // per channel
   float pr[PX], pg[PX], pb[PX];
   auto fetch = [&](int y) {
 #pragma unroll
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
 //    which is linear in the unrolled index for every access made here.
 // Row-major T only (t_layout 0); P = 14 tile columns per block.
 // ---------------------------------------------------------------------------
-template <int N, int R2, int KS>
+template <int N, int R2, int KS, bool THR>
 __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
                                                    const float* __restrict__ ws, const float2* __restrict__ tw,
                                                    const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
@@ -372,6 +377,7 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   __shared__ float zs[ZROWS * KSP];
   __shared__ float2 post_s[2 * (M + 1)];
   __shared__ float2 tw_s[M];
+  __shared__ float sbias[32];   // -(h + strip) / ci[c] per tile row h (fp32 division, FE:411-416)
   const int tid = threadIdx.x;
   const int4 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
@@ -379,13 +385,8 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   // LFQ-bit thresholds of this thread's epilogue rows (latency hidden behind the transform)
   constexpr int EPR = 2;
   const int g16 = tid >> 4, jl = tid & 15;
-  const bool use_thr = ep.median && ep.thr && !sk.norm;
   float2 thr_r[EPR][KS / 2];
-#pragma unroll
-  for (int r = 0; r < EPR; ++r)
-#pragma unroll
-    for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = make_float2(0.0f, 0.0f);
-  if (use_thr) {
+  if (THR) {
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
       const int h = g16 + 16 * r;
@@ -399,8 +400,32 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   }
   for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
   for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
-  // ---- T slice -> LDS, natural row order: thread (y0 = t / 7, p = t % 7) copies rows y0 + 32k
-  if (tid < 32 * (KS / 2)) {
+  if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
+  // ---- T slice -> LDS, natural row order
+  if (d.t_strips == 3) {
+    // padded row-major: the slice row is one aligned 64-B segment (14 of 16 floats used);
+    // thread (y0 = t / 4, q = t % 4) copies float4 q of rows y0 + 64 k
+    const int q = tid & 3, y0 = tid >> 2;
+    const int64_t rs = (int64_t)(d.Kw / KS) * 16;
+    const float4* src = reinterpret_cast<const float4*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * rs + strip * 16) + q;
+    constexpr int NK4 = (N + 63) / 64;
+    float4 tv[NK4];
+#pragma unroll
+    for (int k = 0; k < NK4; ++k)
+      if (N % 64 == 0 || y0 + 64 * k < N) tv[k] = src[k * 16 * rs];
+    float* dst = zs + y0 * KSP + 4 * q;
+#pragma unroll
+    for (int k = 0; k < NK4; ++k) {
+      if (N % 64 != 0 && y0 + 64 * k >= N) continue;
+      dst[64 * KSP * k] = tv[k].x;
+      dst[64 * KSP * k + 1] = tv[k].y;
+      if (q < 3) {
+        dst[64 * KSP * k + 2] = tv[k].z;
+        dst[64 * KSP * k + 3] = tv[k].w;
+      }
+    }
+  } else if (!(DCTAE_ABLATE & 1) && tid < 32 * (KS / 2)) {
+    // row-major: thread (y0 = t / 7, p = t % 7) copies float2 p of rows y0 + 32k
     const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
     const float2* src = reinterpret_cast<const float2*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
     const int64_t rstep = (int64_t)16 * d.Kw;   // 32 rows, in float2
@@ -419,17 +444,19 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   const bool on_col = col < KS;
   // ---- pass 1 (Ns = 1), Makhoul reorder folded into the read addresses
   {
-    float2 v[R1];
-    const bool on = on_col && jj < B1;
+    cf v[R1];
+    const bool on = on_col && jj < B1 && !(DCTAE_ABLATE & 2);
     if (on) {
-      const float* lo = zs + 4 * jj * KSP + col;                  // rows 4jj + 4B1 r (+2 KSP: row + 2)
-      const float* hi = zs + (2 * N - 1 - 4 * jj) * KSP + col;    // rows 2N-1-4jj-4B1 r (-2)
+      // rows 4jj + 4B1 r (+2) for r < 8; rows 2N-1-4jj-4B1 r (-2) for r >= 8, addressed
+      // upwards from the lowest one (LDS offsets are unsigned immediates)
+      const float* lo = zs + 4 * jj * KSP + col;
+      const float* hi = zs + (2 * N - 3 - 4 * jj - 4 * B1 * (R1 - 1)) * KSP + col;
 #pragma unroll
-      for (int r = 0; r < R1 / 2; ++r) v[r] = make_float2(lo[4 * B1 * r * KSP], lo[(4 * B1 * r + 2) * KSP]);
+      for (int r = 0; r < R1 / 2; ++r) v[r] = (cf){lo[4 * B1 * r * KSP], lo[(4 * B1 * r + 2) * KSP]};
 #pragma unroll
       for (int r = R1 / 2; r < R1; ++r)
-        v[r] = make_float2(hi[-4 * B1 * r * KSP], hi[-(4 * B1 * r + 2) * KSP]);
-      DFT<R1>::run(v);
+        v[r] = (cf){hi[(4 * B1 * (R1 - 1 - r) + 2) * KSP], hi[4 * B1 * (R1 - 1 - r) * KSP]};
+      DFTV<R1>::run(v);
     }
     __syncthreads();
     if (on) {
@@ -444,15 +471,18 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   }
   // ---- pass 2 (Ns = 16): z[jj + 16 r], pad16 = jj + 17 r
   {
-    float2 v[R2];
-    const bool on = on_col;
+    cf v[R2];
+    const bool on = on_col && !(DCTAE_ABLATE & 4);
     float* z = zs + 2 * jj * KSP + col;
     if (on) {
 #pragma unroll
-      for (int r = 0; r < R2; ++r) v[r] = make_float2(z[2 * 17 * r * KSP], z[(2 * 17 * r + 1) * KSP]);
+      for (int r = 0; r < R2; ++r) v[r] = (cf){z[2 * 17 * r * KSP], z[(2 * 17 * r + 1) * KSP]};
 #pragma unroll
-      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
-      DFT<R2>::run(v);
+      for (int r = 1; r < R2; ++r) {
+        const float2 w = tw_s[r * jj];
+        v[r] = cmulv(v[r], (cf){w.x, w.y});
+      }
+      DFTV<R2>::run(v);
     }
     __syncthreads();
     if (on) {
@@ -467,245 +497,83 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   // ---- Makhoul post-processing: k = jj + 16 i, A = Z[k] (pad16 = jj + 17 i),
   //      B = conj Z[M - k] (pad16 = bb - 17 i); k = 0 and k = M use Z[0]
   constexpr int KPL = M16 + 1;
-  float2 wv[KPL];
-#pragma unroll
-  for (int i = 0; i < KPL; ++i) wv[i] = make_float2(0.0f, 0.0f);
-  if (on_col) {
+  cf wv[KPL];
+  if (on_col && !(DCTAE_ABLATE & 8)) {
     const float* za = zs + 2 * jj * KSP + col;
     const int bb = M + M16 - 1 - jj + (jj == 0 ? 1 : 0);
-    const float* zb = zs + 2 * bb * KSP + col;
-    const float2* ps = post_s + 2 * jj;
+    const float* zb = zs + 2 * (bb - 17 * (M16 - 1)) * KSP + col;   // Z[M - k] for i = M16 - 1; others above it
+    const cf* ps = reinterpret_cast<const cf*>(post_s) + 2 * jj;
 #pragma unroll
     for (int i = 0; i < M16; ++i) {
-      const float2 A = make_float2(za[2 * 17 * i * KSP], za[(2 * 17 * i + 1) * KSP]);
-      float2 B;
+      const cf A = (cf){za[2 * 17 * i * KSP], za[(2 * 17 * i + 1) * KSP]};
+      cf B;
       if (i == 0) {
-        const float* zb0 = jj == 0 ? zs + col : zb;
-        B = make_float2(zb0[0], -zb0[KSP]);
+        const float* zb0 = jj == 0 ? zs + col : zb + 2 * 17 * (M16 - 1) * KSP;
+        B = (cf){zb0[0], -zb0[KSP]};
       } else {
-        B = make_float2(zb[-2 * 17 * i * KSP], -zb[(-2 * 17 * i + 1) * KSP]);
+        B = (cf){zb[2 * 17 * (M16 - 1 - i) * KSP], -zb[(2 * 17 * (M16 - 1 - i) + 1) * KSP]};
       }
-      const float2 al = ps[32 * i], be = ps[32 * i + 1];
-      wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
+      // W = al (A + B) + be (A - B), as (re, im) pairs: one pk_mul + pk_fma per product
+      const cf s1 = A + B, d1 = A - B, al = ps[32 * i], be = ps[32 * i + 1];
+      wv[i] = s1.xx * al + s1.yy * (cf){-al.y, al.x} + d1.xx * be + d1.yy * (cf){-be.y, be.x};
     }
     if (jj == 0) {  // k = M
-      const float2 A = make_float2(zs[col], zs[KSP + col]);
-      const float2 B = make_float2(A.x, -A.y);
-      wv[M16] = cadd(cmul(post_s[2 * M], cadd(A, B)), cmul(post_s[2 * M + 1], csub(A, B)));
+      const cf A = (cf){zs[col], zs[KSP + col]};
+      const cf B = (cf){A.x, -A.y};
+      const cf* pm = reinterpret_cast<const cf*>(post_s) + 2 * M;
+      wv[M16] = cmulv(A + B, pm[0]) + cmulv(A - B, pm[1]);
     }
   }
   __syncthreads();
   const int Kh = d.Kh;
-  if (on_col) {
+  if (on_col && !(DCTAE_ABLATE & 8)) {
     float* xo = zs + jj * KSP + col;                 // X[k] at row k (natural layout)
-    float* xn = zs + (N - jj) * KSP + col;           // X[N - k]
+    float* xn = zs + (N - jj - 16 * (M16 - 1)) * KSP + col;   // X[N - k], addressed from the lowest row
 #pragma unroll
     for (int i = 0; i < M16; ++i) {
       const int k = jj + 16 * i;
       if (k < Kh) xo[16 * i * KSP] = wv[i].x;
-      if (k >= 1 && N - k < Kh) xn[-16 * i * KSP] = -wv[i].y;
+      if (k >= 1 && N - k < Kh) xn[16 * (M16 - 1 - i) * KSP] = -wv[i].y;
     }
     if (jj == 0 && M < Kh) zs[M * KSP + col] = wv[M16].x;
   }
   __syncthreads();
   // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
-  if (use_thr && d.qh <= 16 * EPR) {
+  if (DCTAE_ABLATE & 16) return;
+  if (THR) {
+    // codes from the exact LFQ thresholds; amax as an integer max of |x| bit
+    // patterns (NaN patterns order above inf: NaN-propagating like torch.amax)
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
       const int h = g16 + 16 * r;
       if (h < d.qh) {
-        float vals[KS];
-        const float* row = zs + (KS * h + jl) * KSP;
+        const float* row = zs + (KS * h + jl) * KSP;   // lanes jl >= KS read in-bounds junk, masked below
+        uint32_t am = 0, code = 0;
 #pragma unroll
-        for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? row[p2] : 0.0f;
-        const int f = (h * d.qw + strip) * ep.C + c;
-        token_epilogue_thr<KS>(ep, c, h, strip, jl, vals, thr_r[r], d.tok_off + f, sk);
+        for (int p = 0; p < KS / 2; ++p) {
+          const float v0 = row[2 * p], v1 = row[2 * p + 1];
+          am = max(am, max(__float_as_uint(v0) & 0x7fffffffu, __float_as_uint(v1) & 0x7fffffffu));
+          code |= (v0 >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
+          code |= (v1 >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
+        }
+        am = jl < KS ? am : 0u;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
+        const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
+        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
+        if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
+        if (sk.raw && jl < KS) {
+#pragma unroll
+          for (int p2 = 0; p2 < KS; ++p2) sk.raw[tok * KS * KS + jl * KS + p2] = row[p2];
+        }
       }
     }
   } else {
     for (int h = g16; h < d.qh; h += 16) {
       float vals[KS];
+      const float* row = zs + (KS * h + jl) * KSP;
 #pragma unroll
-      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
-      const int f = (h * d.qw + strip) * ep.C + c;
-      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// cols, persistent: a grid of about 4 blocks per CU walks the same item list
-// (image, channel, tile column); the T slice of the block's NEXT item is
-// loaded into registers while the current one is transformed, so the HBM
-// latency of the 28 KB slice hides behind the FFT / epilogue of the previous
-// item instead of stalling each block's start.  LAY 0: row-major T (KS/2
-// float2 per row), LAY 1: contiguous strips (float4).
-// ---------------------------------------------------------------------------
-template <int N, int R1, int R2, int KS, int LAY>
-__global__ __launch_bounds__(256) void k_fft_cols3(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
-                                                   int n_items, const float* __restrict__ ws,
-                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
-                                                   EncParams ep, TokenSinks sk) {
-  constexpr int M = N / 2;
-  constexpr int B1 = M / R1, B2 = M / R2;
-  constexpr int KSP = KS | 1;
-  constexpr int ZROWS = 2 * (pad16(M - 1) + 1);
-  static_assert(KS * 16 <= 256 && (KS % 2) == 0, "16 butterfly lanes per column, even tile");
-  static_assert(B1 <= 16 && B2 <= 16 && R1 == 16, "plan shape");
-  using PF = typename std::conditional<LAY == 1, float4, float2>::type;
-  constexpr int PER = LAY == 1 ? 4 : 2;              // floats per prefetch element
-  constexpr int NQ = N * KS / PER;                   // prefetch elements per item
-  constexpr int NPF = (NQ + 255) / 256;
-  __shared__ float zs[ZROWS * KSP];
-  __shared__ float2 post_s[2 * (M + 1)];
-  __shared__ float2 tw_s[M];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
-  for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
-  auto zre = [&](int m, int col) -> float& { return zs[2 * pad16(m) * KSP + col]; };
-  auto zim = [&](int m, int col) -> float& { return zs[(2 * pad16(m) + 1) * KSP + col]; };
-  auto put = [&](int y, int j, float v) {
-    const int vv = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
-    zs[(2 * pad16(vv >> 1) + (vv & 1)) * KSP + j] = v;
-  };
-  PF pf[NPF];
-  auto prefetch = [&](int it, int tid) {
-    const int4 jb = blocks[it];
-    const ImgDesc& d = imgs[jb.x];
-    const float* base = ws + d.ws_t + (int64_t)jb.y * d.H * d.Kw;
-    if (LAY == 1) {
-      const float4* T4 = reinterpret_cast<const float4*>(base + (int64_t)jb.z * N * KS);
-#pragma unroll
-      for (int u = 0; u < NPF; ++u) {
-        const int q = tid + 256 * u;
-        if (NQ % 256 == 0 || q < NQ) pf[u] = *reinterpret_cast<const PF*>(T4 + q);
-      }
-    } else {
-      const float2* T2 = reinterpret_cast<const float2*>(base + jb.z * KS);
-      const int rs = d.Kw / 2;
-#pragma unroll
-      for (int u = 0; u < NPF; ++u) {
-        const int q = tid + 256 * u;
-        const int y = q / (KS / 2), p = q - y * (KS / 2);
-        if (NQ % 256 == 0 || q < NQ) pf[u] = *reinterpret_cast<const PF*>(T2 + (int64_t)y * rs + p);
-      }
-    }
-  };
-  auto scatter = [&](int tid) {
-#pragma unroll
-    for (int u = 0; u < NPF; ++u) {
-      const int q = tid + 256 * u;
-      if (NQ % 256 == 0 || q < NQ) {
-        if (LAY == 1) {
-          const float* tv = reinterpret_cast<const float*>(&pf[u]);
-#pragma unroll
-          for (int v = 0; v < PER; ++v) {
-            const int e = PER * q + v;
-            const int y = e / KS, j = e - y * KS;
-            put(y, j, tv[v]);
-          }
-        } else {
-          const int y = q / (KS / 2), p = q - y * (KS / 2);
-          const float* tv = reinterpret_cast<const float*>(&pf[u]);
-          put(y, 2 * p, tv[0]);
-          put(y, 2 * p + 1, tv[1]);
-        }
-      }
-    }
-  };
-  int it = blockIdx.x;
-  if (it < n_items) prefetch(it, tid);
-#pragma unroll 1
-  for (; it < n_items; it += gridDim.x) {
-    // opaque per-iteration copy of the thread id: keeps the compiler from
-    // hoisting every derived LDS / global address out of the loop (which
-    // costs more registers than recomputing them)
-    int t = tid;
-    asm volatile("" : "+v"(t));
-    const int jj = t & 15, col = t >> 4;
-    const bool on_col = col < KS;
-    const int g16 = t >> 4, jl = t & 15;
-    const int4 jb = blocks[it];
-    const ImgDesc d = imgs[jb.x];
-    const int c = jb.y, strip = jb.z;
-    __syncthreads();  // zs free again (previous epilogue), tables in LDS (first item)
-    scatter(t);
-    if (it + (int)gridDim.x < n_items) prefetch(it + gridDim.x, t);
-    __syncthreads();
-    {  // pass 1 (Ns = 1)
-      // every array below is fully initialised inside the loop: a
-      // conditionally assigned one becomes a loop-carried register set
-      float2 v[R1];
-#pragma unroll
-      for (int r = 0; r < R1; ++r) v[r] = make_float2(0.0f, 0.0f);
-      const bool on = on_col && jj < B1;
-      if (on) {
-#pragma unroll
-        for (int r = 0; r < R1; ++r) v[r] = make_float2(zre(jj + r * B1, col), zim(jj + r * B1, col));
-        DFT<R1>::run(v);
-      }
-      __syncthreads();
-      if (on) {
-#pragma unroll
-        for (int r = 0; r < R1; ++r) {
-          zre(jj * R1 + r, col) = v[r].x;
-          zim(jj * R1 + r, col) = v[r].y;
-        }
-      }
-      __syncthreads();
-    }
-    {  // pass 2 (Ns = R1)
-      float2 v[R2];
-#pragma unroll
-      for (int r = 0; r < R2; ++r) v[r] = make_float2(0.0f, 0.0f);
-      const bool on = on_col && jj < B2;
-      if (on) {
-#pragma unroll
-        for (int r = 0; r < R2; ++r) v[r] = make_float2(zre(jj + r * B2, col), zim(jj + r * B2, col));
-#pragma unroll
-        for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * jj]);
-        DFT<R2>::run(v);
-      }
-      __syncthreads();
-      if (on) {
-#pragma unroll
-        for (int r = 0; r < R2; ++r) {
-          zre(jj + r * R1, col) = v[r].x;
-          zim(jj + r * R1, col) = v[r].y;
-        }
-      }
-      __syncthreads();
-    }
-    constexpr int KPL = (M + 1 + 15) / 16;
-    float2 wv[KPL];
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) wv[i] = make_float2(0.0f, 0.0f);
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      const int k = jj + 16 * i;
-      if (on_col && k <= M) {
-        const int ka = (k == M) ? 0 : k, kb = (k == 0) ? 0 : M - k;
-        const float2 A = make_float2(zre(ka, col), zim(ka, col));
-        const float2 B = make_float2(zre(kb, col), -zim(kb, col));
-        const float2 al = post_s[2 * k], be = post_s[2 * k + 1];
-        wv[i] = cadd(cmul(al, cadd(A, B)), cmul(be, csub(A, B)));
-      }
-    }
-    __syncthreads();
-    const int Kh = d.Kh;
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) {
-      const int k = jj + 16 * i;
-      if (on_col && k <= M) {
-        if (k < Kh) zs[k * KSP + col] = wv[i].x;
-        if (k >= 1 && k < M && N - k < Kh) zs[(N - k) * KSP + col] = -wv[i].y;
-      }
-    }
-    __syncthreads();
-    for (int h = g16; h < d.qh; h += 16) {
-      float vals[KS];
-#pragma unroll
-      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = (jl < KS) ? zs[(KS * h + jl) * KSP + p2] : 0.0f;
+      for (int p2 = 0; p2 < KS; ++p2) vals[p2] = row[p2];
       const int f = (h * d.qw + strip) * ep.C + c;
       token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
     }
@@ -740,26 +608,18 @@ void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int
 
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
-                          hipStream_t s, int persist_grid, int layout) {
+                          hipStream_t s, int kernel, int layout) {
   if (n_blocks <= 0) return;
-  if (persist_grid < 0 && layout != 0) persist_grid = 0;  // linear kernel: row-major T only
-  if (persist_grid < 0) {
-    if (spec == 1)
-      hipLaunchKernelGGL((k_fft_cols4<512, 16, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
-    else if (spec == 2)
-      hipLaunchKernelGGL((k_fft_cols4<224, 7, 14>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
-    return;
-  }
-  if (persist_grid > 0) {
-    const int g = std::min(n_blocks, persist_grid);
-    if (spec == 1 && layout == 1)
-      hipLaunchKernelGGL((k_fft_cols3<512, 16, 16, 14, 1>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
-    else if (spec == 1)
-      hipLaunchKernelGGL((k_fft_cols3<512, 16, 16, 14, 0>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
-    else if (spec == 2 && layout == 1)
-      hipLaunchKernelGGL((k_fft_cols3<224, 16, 7, 14, 1>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
-    else if (spec == 2)
-      hipLaunchKernelGGL((k_fft_cols3<224, 16, 7, 14, 0>), dim3(g), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw, post, ep, sk);
+  if (kernel == 4 && (layout == 0 || layout == 3)) {
+    // thresholds path: codes (+ raw) only; every image's qh within the 32 tile rows the kernel walks
+    const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
+#define DCTAE_COLS4(NN, RR, T)                                                                                  \
+  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk)
+    if (spec == 1 && thr) DCTAE_COLS4(512, 16, true);
+    else if (spec == 1) DCTAE_COLS4(512, 16, false);
+    else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true);
+    else if (spec == 2) DCTAE_COLS4(224, 7, false);
+#undef DCTAE_COLS4
     return;
   }
   if (spec == 1)

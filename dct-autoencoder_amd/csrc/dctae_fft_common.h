@@ -148,4 +148,101 @@ struct DFT<7> {
   static __device__ __forceinline__ void run(float2* v) { dft_odd<7>(v, kCos7, kSin7); }
 };
 
+// ---------------------------------------------------------------------------
+// The same codelets on a native 2-float vector (re, im): every complex add is
+// one v_pk_add_f32 on an aligned register pair and multiplies become
+// v_pk_mul / v_pk_fma with op_sel swizzles, instead of scalar ops that the
+// SLP vectoriser re-pairs with register moves.  FMA contraction is allowed
+// here (the DCT is compared with a tolerance; PatchNorm / LFQ / score code
+// lives elsewhere and keeps -ffp-contract=off).
+// ---------------------------------------------------------------------------
+typedef float cf __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ cf cmulv(cf a, cf w) {
+#pragma clang fp contract(fast)
+  return a.xx * w + a.yy * (cf){-w.y, w.x};
+}
+__device__ __forceinline__ cf mul_mi_v(cf a) { return (cf){a.y, -a.x}; }  // -i * a
+
+template <int R>
+struct DFTV;
+
+template <>
+struct DFTV<4> {
+  static __device__ __forceinline__ void run(cf* v) {
+    const cf t0 = v[0] + v[2], t1 = v[0] - v[2];
+    const cf t2 = v[1] + v[3], t3 = mul_mi_v(v[1] - v[3]);
+    v[0] = t0 + t2;
+    v[2] = t0 - t2;
+    v[1] = t1 + t3;
+    v[3] = t1 - t3;
+  }
+};
+
+template <>
+struct DFTV<16> {
+  static __device__ __forceinline__ void run(cf* v) {
+#pragma clang fp contract(fast)
+    cf a[4][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+#pragma unroll
+      for (int n1 = 0; n1 < 4; ++n1) a[n2][n1] = v[4 * n1 + n2];
+      DFTV<4>::run(a[n2]);
+    }
+    // twiddles W16^(n2 k1): m = 4 -> -i (free), m = 2, 6 -> (1 -+ i)/sqrt2 forms
+#pragma unroll
+    for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+      for (int k1 = 1; k1 < 4; ++k1) {
+        const int m = n2 * k1;
+        if (m == 4) a[n2][k1] = mul_mi_v(a[n2][k1]);
+        else a[n2][k1] = cmulv(a[n2][k1], (cf){kCos16[m], -kSin16[m]});
+      }
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) {
+      cf b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
+      DFTV<4>::run(b);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
+    }
+  }
+};
+
+template <int R>
+__device__ __forceinline__ void dftv_odd(cf* v, const float* C, const float* S) {
+#pragma clang fp contract(fast)
+  constexpr int H = (R - 1) / 2;
+  cf s[H], d[H];
+  const cf x0 = v[0];
+  cf sum = v[0];
+#pragma unroll
+  for (int n = 1; n <= H; ++n) {
+    s[n - 1] = v[n] + v[R - n];
+    d[n - 1] = v[n] - v[R - n];
+    sum = sum + s[n - 1];
+  }
+  cf out[R];
+  out[0] = sum;
+#pragma unroll
+  for (int k = 1; k <= H; ++k) {
+    cf a = x0, b = (cf){0.0f, 0.0f};
+#pragma unroll
+    for (int n = 1; n <= H; ++n) {
+      const int m = (n * k) % R;
+      a = a + s[n - 1] * C[m];
+      b = b + d[n - 1].yx * S[m];      // (d.y S, d.x S)
+    }
+    out[k] = (cf){a.x + b.x, a.y - b.y};
+    out[R - k] = (cf){a.x - b.x, a.y + b.y};
+  }
+#pragma unroll
+  for (int k = 0; k < R; ++k) v[k] = out[k];
+}
+
+template <>
+struct DFTV<7> {
+  static __device__ __forceinline__ void run(cf* v) { dftv_odd<7>(v, kCos7, kSin7); }
+};
+
 }  // namespace dctae

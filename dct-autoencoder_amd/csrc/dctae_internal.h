@@ -30,7 +30,8 @@ struct ImgDesc {
   int32_t T;         // tokens = C*qh*qw
   int32_t row, col, k, local_id;  // packing
   int32_t plan_w, plan_h;         // FFT plan index for rows (length W) / cols (length H); -1 = GEMM
-  int32_t t_strips;               // T layout: 0 = [c][y][Kw] row-major, 1 = [c][w][y][P] strips
+  int32_t t_strips;               // T layout: 0 = [c][y][Kw] row-major, 1 = [c][w][y][P] strips,
+                                  // 2 = [c][w][y][16] padded strips, 3 = [c][y][w][16] padded row-major
   int32_t t_pad;
 };
 

@@ -52,6 +52,6 @@ void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int
                           const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int prefetch);
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
-                          hipStream_t s, int persist_grid, int layout);
+                          hipStream_t s, int kernel, int layout);
 
 }  // namespace dctae

@@ -364,8 +364,11 @@ def test_thresholds_are_exact(pn):
 
 SPEC_VARIANTS = {  # option sets of the specialised kernels, with the defaults they are reset to
     "default": ({}, {}),
-    "cols_lds_scatter": ({"cols_kernel": 2}, {"cols_kernel": 4}),
-    "cols_persistent": ({"cols_kernel": 3}, {"cols_kernel": 4}),
+    "cols_lds_scatter": ({"cols_kernel": 2}, {"cols_kernel": 5}),
+    "cols_persistent": ({"cols_kernel": 3}, {"cols_kernel": 5}),
+    "cols_linear": ({"cols_kernel": 4}, {"cols_kernel": 5}),
+    "cols_no_prefetch": ({"cols_prefetch": 0}, {"cols_prefetch": 1}),
+    "cols_group3": ({"cols_group": 3}, {"cols_group": 16}),
     "t_strips": ({"t_layout": 1}, {"t_layout": 0}),
     "t_strips16": ({"t_layout": 2}, {"t_layout": 0}),
 }
