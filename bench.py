@@ -48,6 +48,7 @@ def kernel_models(h, w, p, maxp, ncb, s, images_per_row):
         "gemm_cols": ("mfma", 3 * 2.0 * kh * kw * h, "flop"),
         "fft_rows": ("hbm", 12 * h * w + inter, "B"),            # RGB in, T out
         "fft_cols": ("hbm", inter + stage, "B"),                  # T in, token staging out
+        "enc_fused": ("hbm", 12 * h * w + stage, "B"),            # RGB in, token staging out (T on chip)
         "tile_epilogue": ("hbm", 12 * kh * kw + stage, "B"),
         "sort_pack": ("hbm", stage + t * (8 * ncb + 32) + s / images_per_row, "B"),
         "pad_fill": ("hbm", s / images_per_row, "B"),
@@ -140,6 +141,7 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
+    ops.check_device_errors(dev)   # raises if a fused-kernel dependence wait timed out
     if timing:
         ctx.lib.dctae_set_timing(ctx.h, 0)
         ctx.lib.dctae_timing_collect(ctx.h)

@@ -81,6 +81,7 @@ _SIGS = {
                       C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32), _P, _P, _P, _P,
                       C.POINTER(Norm), C.POINTER(LFQCfg), _P, _P, _P, _P], C.c_int),
     "dctae_check_device_errors": ([_P, _P], C.c_int),
+    "dctae_fused_debug_counters": ([_P, C.POINTER(C.c_int32), C.c_int64, _P], C.c_int64),
     "dctae_synth_images": ([_P, C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, _P], C.c_int),
     "dctae_set_timing": ([_P, C.c_int], C.c_int),
     "dctae_timing_collect": ([_P], C.c_int),

@@ -64,6 +64,14 @@ struct dctae_ctx {
   int cols_kernel = 4;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses)
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
+  // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
+  int fused = 0;                      // measured slower than the two kernels so far (profile: DESIGN.md)
+  int fused_slots = 2;                // T slots per XCD (lookahead = slots - 1 images)
+  int fused_bpc = 4;                  // resident workgroups per CU
+  int fused_spin = 1 << 20;           // poll bound of a dependence wait (~1 s), then err |= 8
+  int fused_rows_pct = 50;            // share of row workers
+  int fused_debug = 0;                // 1: skip dependence waits; 2: collect per-XCD tick profile
+  int n_cu = 256;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   size_t st_bytes = 0;
@@ -455,6 +463,10 @@ struct EncPlan {
   size_t rowlen_off = 0, plans_off = 0;
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
+  // fused path (fused_spec != 0): ring of T slots at ws[0], sync ints after it
+  int fused_spec = 0, fused_nr = 0, fused_nc = 0, fused_qw = 0, n_xcd = 1;
+  int64_t slot_floats = 0, sync_off = 0;   // floats
+  int64_t fused_tw_off = 0, fused_post_off = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -498,6 +510,11 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
     return DCTAE_EHIP;
   }
   c->lds_limit = fft_kernel_setup(device);
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->n_cu = cu;
+    hipGetLastError();
+  }
   hipEventRecord(c->plan_evt, 0);
   *out = c;
   return 0;
@@ -569,6 +586,12 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
   else if (k == "cols_kernel" && (value == 2 || value == 4)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
+  else if (k == "fused") ctx->fused = value != 0;
+  else if (k == "fused_slots" && value >= 1 && value <= 16) ctx->fused_slots = (int)value;
+  else if (k == "fused_bpc" && value >= 1 && value <= 8) ctx->fused_bpc = (int)value;
+  else if (k == "fused_rows_pct" && value >= 1 && value <= 99) ctx->fused_rows_pct = (int)value;
+  else if (k == "fused_debug" && value >= 0 && value <= 3) ctx->fused_debug = (int)value;
+  else if (k == "fused_spin" && value >= 1024) ctx->fused_spin = (int)std::min<int64_t>(value, 1ll << 30);
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -643,7 +666,22 @@ int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
   if (h & 1) return fail(ctx, DCTAE_EINVAL, "channel/position index out of range of the PatchNorm tables");
   if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
   if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
+  if (h & 8) return fail(ctx, DCTAE_EHIP, "fused encode: a dependence wait timed out (outputs invalid)");
   return 0;
+}
+
+int64_t dctae_fused_debug_counters(dctae_ctx* ctx, int32_t* host_out, int64_t cap, void* stream) {
+  if (!ctx || !ctx->enc_plan || !ctx->enc_plan->fused_spec) return 0;
+  const EncPlan& E = *ctx->enc_plan;
+  const int64_t n = ((24 + 2ll * E.n_img + 1) & ~1ll) + 128;   // + 64 profile u64 (fused_debug 2)
+  if (host_out && cap > 0) {
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemcpyAsync(host_out, ctx->ws + E.sync_off, sizeof(int32_t) * std::min(n, cap), hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail(ctx, DCTAE_EHIP, "fused counters copy failed");
+  }
+  return n;
 }
 
 int dctae_synth_images(dctae_ctx* ctx, uint64_t seed, int64_t first_index, int32_t n_img, int32_t H, int32_t W,
@@ -704,6 +742,26 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
       if (pack->row_len[r] < 0 || pack->row_len[r] > S) return fail(ctx, DCTAE_EINVAL, "row_len out of range");
+  // fused path: every image square N x N on one specialised plan, row-major T
+  {
+    bool ok = ctx->fused && n > 0 && P == 14 && ctx->t_layout == 0 && ctx->cols_kernel == 4;
+    for (int i = 0; ok && i < n; ++i) {
+      const ImgDesc& d = D[i];
+      ok = d.plan_w >= 0 && d.plan_w == d.plan_h && plans[d.plan_w].spec != 0 && d.H == d.W && d.H == D[0].H &&
+           d.qh <= 32;
+    }
+    if (ok) {
+      E.fused_spec = plans[D[0].plan_w].spec;
+      E.fused_nr = (D[0].H + fused_rows_per_item() - 1) / fused_rows_per_item();
+      E.fused_nc = 3 * D[0].qw;
+      E.fused_qw = D[0].qw;
+      E.fused_tw_off = plans[D[0].plan_w].tw_off;
+      E.fused_post_off = plans[D[0].plan_w].post_off;
+      E.n_xcd = std::max(1, std::min(8, ctx->n_cu / 32));
+      E.slot_floats = (3ll * D[0].Kw * D[0].H + 63) & ~63ll;
+      E.sync_off = E.n_xcd * (int64_t)ctx->fused_slots * E.slot_floats;
+    }
+  }
   // chunks: FFT images are grouped so the intermediate T of a chunk stays in
   // the 256 MiB Infinity Cache between the row and column kernels
   auto ws_of = [&](const ImgDesc& d) {
@@ -722,7 +780,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     while (i < n) {
       const int64_t w = ws_of(D[i]);
       const bool fft = D[i].plan_w >= 0 && D[i].plan_h >= 0;
-      const int64_t cap = fft ? std::min<int64_t>(ctx->chunk_bytes, ctx->ws_limit) : ctx->ws_limit;
+      const int64_t cap = E.fused_spec ? INT64_MAX : fft ? std::min<int64_t>(ctx->chunk_bytes, ctx->ws_limit) : ctx->ws_limit;
       if (i > j.i0 && wsb + w > cap) break;
       wsb += w;
       ++i;
@@ -751,7 +809,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.max_T = std::max(j.max_T, d.T);
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
-    E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
+    E.ws_need = E.fused_spec ? (size_t)(E.sync_off + 24 + 2ll * n + 2 + 128) * 4 : std::max<size_t>(E.ws_need, (size_t)wsf * 4);
     E.max_T = std::max(E.max_T, j.max_T);
   }
   E.n_tok = tok;
@@ -896,7 +954,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout +
-                             1024 * ctx->xcd_order,
+                             1024 * ctx->xcd_order + 4096 * ctx->fused + 8192 * ctx->fused_slots +
+                             (1 << 20) * ctx->cols_kernel,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -973,7 +1032,36 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   }
   EncParams epj = ep;
   if (!full) epj.median = nullptr;
+  if (E.fused_spec) {
+    FusedArgs fa{};
+    fa.imgs = (const ImgDesc*)(pd + E.all_desc_off);
+    fa.rgb = imgs->rgb_dev;
+    fa.ring = ctx->ws;
+    fa.slot_floats = E.slot_floats;
+    fa.sync = (int*)(ctx->ws + E.sync_off);
+    fa.err = ctx->err_dev;
+    fa.tw = ctx->fft_tab + E.fused_tw_off;
+    fa.post = ctx->fft_tab + E.fused_post_off;
+    fa.n_img = E.n_img;
+    fa.n_xcd = E.n_xcd;
+    fa.slots = ctx->fused_slots;
+    fa.look = std::max(1, ctx->fused_slots - 1);
+    fa.nr = E.fused_nr;
+    fa.nc = E.fused_nc;
+    fa.qw = E.fused_qw;
+    fa.spin_limit = ctx->fused_spin;
+    fa.rows_pct = ctx->fused_rows_pct;
+    fa.debug = ctx->fused_debug & 1;
+    const size_t n_sync = 24 + 2 * (size_t)E.n_img;
+    fa.prof = (ctx->fused_debug & 2) ? (unsigned long long*)(ctx->ws + E.sync_off + ((n_sync + 1) & ~size_t(1)))
+                                     : nullptr;
+    const bool thr = epj.median && epj.thr && !sk.norm && epj.maxph <= 32 && epj.cb_dim == 14 && epj.ncb == 14;
+    HIPCHK(ctx, hipMemsetAsync(fa.sync, 0, (((n_sync + 1) & ~size_t(1)) + 128) * sizeof(int), s));
+    Timer t(ctx, s, "enc_fused");
+    launch_enc_fused(E.fused_spec, thr, ctx->n_cu * ctx->fused_bpc, fa, ctx->cm, epj, sk, s);
+  }
   for (auto& j : E.jobs) {
+    if (E.fused_spec) break;
     const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     if (j.any_gemm_rows) {

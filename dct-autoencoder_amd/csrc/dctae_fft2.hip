@@ -9,6 +9,9 @@
 #include "dctae_launch.h"
 
 // profiling builds only (tools/gpu_ablate.sh): skip parts of the column kernel
+#ifndef DCTAE_THR_AT
+#define DCTAE_THR_AT 2
+#endif
 #ifndef DCTAE_ABLATE
 #define DCTAE_ABLATE 0
 #endif
@@ -20,15 +23,38 @@ namespace dctae {
 __device__ __forceinline__ constexpr int pad16(int m) { return m + (m >> 4); }
 
 // ---------------------------------------------------------------------------
-// rows: one wave = one image row, its 3 IPT channels are 3 jobs
+// rows: one wave = one image row, its 3 IPT channels are 3 jobs.  A row item
+// is 16 rows (4 waves x RPW rows); T points at channel 0, row 0 of the
+// image's row-pass output.  NT: RGB read with non-temporal loads (streamed
+// once; keeps the XCD's L2 for T in the fused kernel).
 // ---------------------------------------------------------------------------
-template <int N, int R1, int R2, bool PF>
-__global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
-                                                   const float* __restrict__ rgb, float* __restrict__ ws,
-                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
-                                                   ColorMats cm) {
+template <int N>
+struct RowsLds {
+  static constexpr int M = N / 2;
+  static constexpr int MP = pad16(M - 1) + 2;
+  float2 z[4][3][MP];
+};
+
+// threadIdx.x through a volatile asm: not loop-invariant to the compiler, so
+// the lane-derived LDS addresses of an item body are rebuilt per item instead
+// of being hoisted out of the fused kernel's item loop (and kept live in VGPRs)
+__device__ __forceinline__ int opaque_tid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  return t;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+
+template <int N, int R1, int R2, bool PF, bool NT>
+__device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const float* __restrict__ rgb,
+                                           float* __restrict__ T, RowsLds<N>& L, const float2* post_s,
+                                           const float2* tw_s, const ColorMats& cm) {
   constexpr int M = N / 2;
-  constexpr int MP = pad16(M - 1) + 2;
+  constexpr int MP = RowsLds<N>::MP;
   constexpr int B1 = M / R1, B2 = M / R2;
   constexpr int PX = (N + 63) / 64;        // pixels per lane and row
   constexpr int KI = (M + 63) / 64;        // k = lane + 64 i, i < KI, covers k < M (k = M by lane 0)
@@ -36,16 +62,9 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
   static_assert(R1 * R2 == M, "two-pass plan");
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
-  __shared__ float2 zs[4][3][MP];
-  __shared__ float2 post_s[2 * (M + 1)];
-  __shared__ float2 tw_s[M];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
-  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
-  __syncthreads();
-  const int2 jb = blocks[blockIdx.x];
-  const ImgDesc d = imgs[jb.x];
-  float2(*z)[MP] = zs[wave];
+  const int tid = opaque_tid();
+  const int wave = tid >> 6, lane = tid & 63;
+  float2(*z)[MP] = L.z[wave];
   float* zf0 = reinterpret_cast<float*>(z[0]);
   float* zf1 = reinterpret_cast<float*>(z[1]);
   float* zf2 = reinterpret_cast<float*>(z[2]);
@@ -83,13 +102,19 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
       const int px = lane + 64 * i;
       if (px < N && y < H) {
         const int64_t o = (int64_t)y * N + px;
-        pr[i] = src[o];
-        pg[i] = src[hw + o];
-        pb[i] = src[2 * hw + o];
+        if (NT) {
+          pr[i] = ld_nt(src + o);
+          pg[i] = ld_nt(src + hw + o);
+          pb[i] = ld_nt(src + 2 * hw + o);
+        } else {
+          pr[i] = src[o];
+          pg[i] = src[hw + o];
+          pb[i] = src[2 * hw + o];
+        }
       }
     }
   };
-  int y = jb.y + wave;
+  int y = y_first + wave;
   if (PF) fetch(y);
 #pragma unroll 1
   for (int rr = 0; rr < RPW; ++rr, y += 4) {
@@ -136,7 +161,7 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
     // ---- Makhoul post-processing -> T (k = lane + 64 i; X[k] = Re W_k, X[N-k] = -Im W_k)
 #pragma unroll 1
     for (int c = 0; c < 3; ++c) {
-      float* tb = ws + d.ws_t + c * cstride + (int64_t)y * ystride;
+      float* tb = T + c * cstride + (int64_t)y * ystride;
 #pragma unroll
       for (int i = 0; i < KI; ++i) {
         const int k = lane + 64 * i;
@@ -159,6 +184,23 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
       }
     }
   }
+}
+
+template <int N, int R1, int R2, bool PF>
+__global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                                                   const float* __restrict__ rgb, float* __restrict__ ws,
+                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                   ColorMats cm) {
+  constexpr int M = N / 2;
+  __shared__ RowsLds<N> L;
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
+  for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  __syncthreads();
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  rows2_item<N, R1, R2, PF, false>(d, jb.y, rgb, ws + d.ws_t, L, post_s, tw_s, cm);
 }
 
 // ---------------------------------------------------------------------------
@@ -361,10 +403,23 @@ __global__ __launch_bounds__(256) void k_fft_cols2(const ImgDesc* __restrict__ i
 //    which is linear in the unrolled index for every access made here.
 // Row-major T only (t_layout 0); P = 14 tile columns per block.
 // ---------------------------------------------------------------------------
-template <int N, int R2, int KS, bool THR>
-__global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
-                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
-                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+template <int N>
+struct ColsLds {
+  static constexpr int M = N / 2;
+  static constexpr int KSP = 15;
+  static constexpr int ZROWS = 2 * (pad16(M - 1) + 1);
+  float z[ZROWS * KSP];
+};
+
+// one column item: (image d, channel c, tile column strip); T = the image's
+// row-pass output (channel 0, row 0).  NTL: T read with non-temporal loads,
+// which bypass the CU's L1 (the fused kernel reads T that other CUs of the
+// XCD have just written).  Caller: post_s / tw_s loaded, a block barrier
+// since the previous use of zs.
+template <int N, int R2, int KS, bool THR, bool NTL, int THR_AT = 0>
+__device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, const float* __restrict__ T, float* zs,
+                                           const float2* post_s, const float2* tw_s, float* sbias,
+                                           const EncParams& ep, const TokenSinks& sk) {
 #pragma clang fp contract(fast)
   constexpr int R1 = 16;
   constexpr int M = N / 2;
@@ -374,19 +429,13 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   constexpr int M16 = M / 16;
   static_assert(M % 16 == 0 && B2 == 16 && B1 <= 16 && KS == 14, "plan shape");
   static_assert(N * KSP <= ZROWS * KSP, "natural rows fit the complex layout");
-  __shared__ float zs[ZROWS * KSP];
-  __shared__ float2 post_s[2 * (M + 1)];
-  __shared__ float2 tw_s[M];
-  __shared__ float sbias[32];   // -(h + strip) / ci[c] per tile row h (fp32 division, FE:411-416)
-  const int tid = threadIdx.x;
-  const int4 jb = blocks[blockIdx.x];
-  const ImgDesc d = imgs[jb.x];
-  const int c = jb.y, strip = jb.z;
+  static_assert(KSP == ColsLds<N>::KSP, "LDS image");
+  const int tid = opaque_tid();
   // LFQ-bit thresholds of this thread's epilogue rows (latency hidden behind the transform)
   constexpr int EPR = 2;
   const int g16 = tid >> 4, jl = tid & 15;
   float2 thr_r[EPR][KS / 2];
-  if (THR) {
+  auto load_thr = [&]() {
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
       const int h = g16 + 16 * r;
@@ -397,9 +446,8 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
         for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
       }
     }
-  }
-  for (int i = tid; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
-  for (int i = tid; i < M; i += 256) tw_s[i] = tw[i];
+  };
+  if (THR && THR_AT == 0) load_thr();
   if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
   // ---- T slice -> LDS, natural row order
   if (d.t_strips == 3) {
@@ -407,7 +455,7 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
     // thread (y0 = t / 4, q = t % 4) copies float4 q of rows y0 + 64 k
     const int q = tid & 3, y0 = tid >> 2;
     const int64_t rs = (int64_t)(d.Kw / KS) * 16;
-    const float4* src = reinterpret_cast<const float4*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * rs + strip * 16) + q;
+    const float4* src = reinterpret_cast<const float4*>(T + ((int64_t)c * d.H + y0) * rs + strip * 16) + q;
     constexpr int NK4 = (N + 63) / 64;
     float4 tv[NK4];
 #pragma unroll
@@ -427,12 +475,13 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   } else if (!(DCTAE_ABLATE & 1) && tid < 32 * (KS / 2)) {
     // row-major: thread (y0 = t / 7, p = t % 7) copies float2 p of rows y0 + 32k
     const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
-    const float2* src = reinterpret_cast<const float2*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v* src = reinterpret_cast<const f2v*>(T + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
     const int64_t rstep = (int64_t)16 * d.Kw;   // 32 rows, in float2
     float* dst = zs + y0 * KSP + 2 * p;
-    float2 tv[N / 32];
+    f2v tv[N / 32];
 #pragma unroll
-    for (int k = 0; k < N / 32; ++k) tv[k] = src[k * rstep];
+    for (int k = 0; k < N / 32; ++k) tv[k] = NTL ? ld_nt(src + k * rstep) : src[k * rstep];
 #pragma unroll
     for (int k = 0; k < N / 32; ++k) {
       dst[32 * KSP * k] = tv[k].x;
@@ -494,6 +543,7 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
     }
     __syncthreads();
   }
+  if (THR && THR_AT == 1) load_thr();
   // ---- Makhoul post-processing: k = jj + 16 i, A = Z[k] (pad16 = jj + 17 i),
   //      B = conj Z[M - k] (pad16 = bb - 17 i); k = 0 and k = M use Z[0]
   constexpr int KPL = M16 + 1;
@@ -538,6 +588,7 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
     if (jj == 0 && M < Kh) zs[M * KSP + col] = wv[M16].x;
   }
   __syncthreads();
+  if (THR && THR_AT == 2) load_thr();
   // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile
   if (DCTAE_ABLATE & 16) return;
   if (THR) {
@@ -578,6 +629,212 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
       token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
     }
   }
+}
+
+template <int N, int R2, int KS, bool THR>
+__global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+  constexpr int M = N / 2;
+  __shared__ ColsLds<N> L;
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
+  __shared__ float sbias[32];   // -(h + strip) / ci[c] per tile row h (fp32 division, FE:411-416)
+  for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  cols4_item<N, R2, KS, THR, false>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk);
+}
+
+// ---------------------------------------------------------------------------
+// Fused encode: rows and columns of the same images in ONE persistent launch,
+// the intermediate T kept on chip.  Every workgroup reads its XCD id and
+// serves that XCD's images q, q + n_xcd, ... (j-th image of the queue =
+// image q + n_xcd j); it is a ROW worker or a COLUMN worker for its whole
+// life (two loops: each keeps the register allocation of its own body), the
+// share of row workers set by rows_pct; worker 0 of an XCD rows, worker 1
+// columns.  Items are claimed in order from per-XCD counters:
+//   row item (j, s):    rows 16 s .. 16 s + 15 of image j -> T slot j % slots
+//   column item (j, s): channel s / qw, tile column s % qw of image j
+// Dependences (each on items that are claimed in order and never wait on
+// the waiter, so they always drain):
+//   column items of j wait for all nr row items of j (rows_done[img] == nr);
+//   row items of j wait for all nc column items of j - slots (slot reuse).
+// Producer and consumer are on the same XCD by construction (queue =
+// XCC_ID), so the hand-off goes through that XCD's L2: producers wait for
+// their stores (vmcnt(0)) before one relaxed agent-scope counter add per
+// workgroup; consumers poll the counter and read T with non-temporal loads,
+// which bypass the (stale-prone) CU L1.  No release fence writes the ring
+// back: n_xcd * slots slots of 2.75 MB (512^2) stay in L2 / Infinity Cache.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int xcc_id() {
+  int v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 0xf;
+}
+
+// The dependence helpers below keep every branch WAVE-uniform (wave 0 of the
+// workgroup does the work, the branch tested on readfirstlane(threadIdx.x)):
+// a `threadIdx.x == 0` region inside the persistent loop is a divergent
+// branch to the compiler, whose CFG structurizer then builds a loop around
+// the barriers that does not re-run the claim (a hang on gfx950 / ROCm 7.2).
+__device__ __forceinline__ bool is_wave0() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x) == 0; }
+
+// wave 0: spin until *p >= target (bounded; false on time-out); uniform result
+__device__ __forceinline__ bool wait_count(const int* p, int target, int limit) {
+  for (int n = 0;; ++n) {
+    const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (v >= target) return true;
+    if (n >= limit) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// one add of 1 from wave 0 (lane 0's term; the other lanes add 0)
+__device__ __forceinline__ int wave_add1(int* p) {
+  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int old = __hip_atomic_fetch_add(p, lane == 0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane(old);
+}
+
+// every thread: own stores complete, then one counter add for the workgroup
+__device__ __forceinline__ void signal_done(int* p) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (is_wave0()) wave_add1(p);
+}
+
+// wait (wave 0 polls) then release the workgroup; err |= 8 on time-out
+__device__ __forceinline__ void wait_all(const int* p, int target, int limit, int* err) {
+  if (is_wave0()) {
+    if (!wait_count(p, target, limit)) atomicOr(err, 8);
+  }
+  __syncthreads();
+}
+
+// claim the next item of a counter (block-uniform result)
+__device__ __forceinline__ int claim(int* ctr, int* s_slot) {
+  if (is_wave0()) *s_slot = wave_add1(ctr);
+  __syncthreads();
+  const int it = __builtin_amdgcn_readfirstlane(*s_slot);
+  __syncthreads();
+  return it;
+}
+
+template <int N, int R2, bool THR>
+__global__ __launch_bounds__(256, 4) void k_enc_fused(FusedParams p_, const ImgDesc* __restrict__ imgs) {
+  const FusedArgs& a = p_.a;
+  constexpr int M = N / 2;
+  union Lds {
+    RowsLds<N> r;
+    ColsLds<N> c;
+  };
+  __shared__ Lds L;
+  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float2 tw_s[M];
+  __shared__ float sbias[32];
+  __shared__ int s_int;
+  const FusedArgs& a0 = a;
+  for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = a0.post[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = a0.tw[i];
+  const int n_xcd = a0.n_xcd, n_img = a0.n_img, nr = a0.nr, nc = a0.nc, slots = a0.slots;
+  int* const sync = a0.sync;
+  const int q = n_xcd > 1 ? xcc_id() % n_xcd : 0;
+  const int nj = n_img > q ? (n_img - q + n_xcd - 1) / n_xcd : 0;
+  int* rows_done = sync + 24;
+  int* cols_done = sync + 24 + n_img;
+  // one claim sequence per XCD: R(0) .. R(look - 1), then [C(j), R(j + look)] per image j
+  const int look = min(a0.look, nj);
+  const int per = nr + nc;
+  const int n_full = nj - look;
+  const int head = look * nr;
+  const int total = head + n_full * per + look * nc;
+  uint64_t prof_w = 0, prof_r = 0, prof_c = 0, n_r = 0, n_c = 0;
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+  for (;;) {
+    const int it = claim(sync + q, &s_int);
+    if (it >= total) break;
+    bool row;
+    int j, sub;
+    if (it < head) {
+      row = true;
+      j = it / nr;
+      sub = it - j * nr;
+    } else {
+      int u = it - head;
+      if (u < n_full * per) {
+        const int blk = u / per, off = u - blk * per;
+        row = off >= nc;
+        j = row ? blk + look : blk;
+        sub = row ? off - nc : off;
+      } else {
+        u -= n_full * per;
+        row = false;
+        j = n_full + u / nc;
+        sub = u - (j - n_full) * nc;
+      }
+    }
+    const int img = q + n_xcd * j;
+    const ImgDesc d = imgs[img];
+    float* T = a.ring + (int64_t)(q * slots + j % slots) * a.slot_floats;
+    if (row) {
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      if (j >= slots && !(a.debug & 1))   // the slot's previous image: all its columns read
+        wait_all(cols_done + img - n_xcd * slots, nc, a.spin_limit, a.err);
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      const ColorMats& cm = p_.cm;
+      rows2_item<N, 16, R2, false, true>(d, 16 * sub, a.rgb, T, L.r, post_s, tw_s, cm);
+      signal_done(rows_done + img);
+      if (a.prof) {
+        prof_w += t1 - t0;
+        prof_r += __builtin_amdgcn_s_memtime() - t1;
+        ++n_r;
+      }
+    } else {
+      const uint64_t t0 = __builtin_amdgcn_s_memtime();
+      if (!(a.debug & 1)) wait_all(rows_done + img, nr, a.spin_limit, a.err);
+      const uint64_t t1 = __builtin_amdgcn_s_memtime();
+      const int qw = a.qw;
+      const int c = sub / qw, strip = sub - c * qw;
+      const EncParams& ep = p_.ep;
+      const TokenSinks& sk = p_.sk;
+      cols4_item<N, R2, 14, THR, true, DCTAE_THR_AT>(d, c, strip, T, L.c.z, post_s, tw_s, sbias, ep, sk);
+      signal_done(cols_done + img);
+      if (a.prof) {
+        prof_w += t1 - t0;
+        prof_c += __builtin_amdgcn_s_memtime() - t1;
+        ++n_c;
+      }
+    }
+  }
+  if (a.prof && is_wave0()) {   // per-XCD totals: wait, row work, column work (s_memtime ticks), items
+    const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    if (lane == 0) {
+      unsigned long long* pr = a.prof + 8 * q;
+      atomicAdd(pr + 0, (unsigned long long)prof_w);
+      atomicAdd(pr + 1, (unsigned long long)prof_r);
+      atomicAdd(pr + 2, (unsigned long long)prof_c);
+      atomicAdd(pr + 3, (unsigned long long)n_r);
+      atomicAdd(pr + 4, (unsigned long long)n_c);
+      atomicAdd(pr + 5, (unsigned long long)(__builtin_amdgcn_s_memtime() - t_start));
+      atomicAdd(pr + 6, 1ull);
+    }
+  }
+}
+
+int fused_rows_per_item() { return 16; }
+
+void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,
+                      const TokenSinks& sk, hipStream_t s) {
+  if (a.n_img <= 0 || grid <= 0) return;
+  FusedParams fp{a, cm, ep, sk};
+#define DCTAE_FUSED(NN, RR, T) hipLaunchKernelGGL((k_enc_fused<NN, RR, T>), dim3(grid), dim3(256), 0, s, fp, a.imgs)
+  if (spec == 1 && thr) DCTAE_FUSED(512, 16, true);
+  else if (spec == 1) DCTAE_FUSED(512, 16, false);
+  else if (spec == 2 && thr) DCTAE_FUSED(224, 7, true);
+  else if (spec == 2) DCTAE_FUSED(224, 7, false);
+#undef DCTAE_FUSED
 }
 
 // ---------------------------------------------------------------------------

@@ -54,4 +54,8 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
                           hipStream_t s, int kernel, int layout);
 
+int fused_rows_per_item();
+void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,
+                      const TokenSinks& sk, hipStream_t s);
+
 }  // namespace dctae

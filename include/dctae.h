@@ -234,6 +234,13 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
  * IndexError there).  Synchronises `stream`. */
 int dctae_check_device_errors(dctae_ctx* ctx, void* stream);
 
+/* Diagnostics of the fused encode (k_enc_fused): copies the last launch's
+ * dependence counters (24 queue/worker ints, then rows_done[n], cols_done[n])
+ * into host_out (up to cap ints, synchronising the stream).  Returns the
+ * number of ints available, 0 if the last encode was not fused.  No reference
+ * counterpart (test / profiling aid). */
+int64_t dctae_fused_debug_counters(dctae_ctx* ctx, int32_t* host_out, int64_t cap, void* stream);
+
 /* Counter-based synthetic RGB images (same hash as oracle/rng.py):
  * value(seed, first_index + i, e) for i < n_img, images of (3, H, W)
  * contiguous. */

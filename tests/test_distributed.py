@@ -94,7 +94,7 @@ def _worker(rank, world, port, case, q):
         dist.destroy_process_group()
 
 
-def _run(world, case):
+def _run_once(world, case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -102,12 +102,24 @@ def _run(world, case):
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r, *t = q.get(timeout=240)
-        res[r] = t
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        for _ in range(world):
+            r, *t = q.get(timeout=240)
+            res[r] = t
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    ok = all(p.exitcode == 0 for p in procs) and len(res) == world
+    return res if ok else None
+
+
+def _run(world, case):
+    # one retry with a fresh port: the free-port probe can race with another
+    # process binding the port between probe and rendezvous
+    res = _run_once(world, case) or _run_once(world, case)
+    assert res is not None, "gloo workers failed twice"
     return res
 
 

@@ -364,13 +364,12 @@ def test_thresholds_are_exact(pn):
 
 SPEC_VARIANTS = {  # option sets of the specialised kernels, with the defaults they are reset to
     "default": ({}, {}),
-    "cols_lds_scatter": ({"cols_kernel": 2}, {"cols_kernel": 5}),
-    "cols_persistent": ({"cols_kernel": 3}, {"cols_kernel": 5}),
-    "cols_linear": ({"cols_kernel": 4}, {"cols_kernel": 5}),
-    "cols_no_prefetch": ({"cols_prefetch": 0}, {"cols_prefetch": 1}),
-    "cols_group3": ({"cols_group": 3}, {"cols_group": 16}),
+    "fused": ({"fused": 1}, {"fused": 0}),
+    "cols_lds_scatter": ({"cols_kernel": 2}, {"cols_kernel": 4}),
     "t_strips": ({"t_layout": 1}, {"t_layout": 0}),
     "t_strips16": ({"t_layout": 2}, {"t_layout": 0}),
+    "t_rowmajor_pad16": ({"t_layout": 3}, {"t_layout": 0}),
+    "fused_1slot": ({"fused": 1, "fused_slots": 1}, {"fused": 0, "fused_slots": 2}),
 }
 
 
@@ -405,3 +404,35 @@ def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
         a, b = dp_s.patches.cpu()[r, sj], dp_g.patches.cpu()[r, gj]
         assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item()
         assert (c_s.cpu()[r, sj] != c_g.cpu()[r, gj]).sum().item() <= 4
+
+
+@pytest.mark.parametrize("slots", [1, 2, 3])
+@pytest.mark.parametrize("shape,n", [((512, 512), 27), ((224, 224), 70)])
+def test_fused_matches_unfused_bitwise(fe, pn, lfq, shape, n, slots):
+    """k_enc_fused (rows and columns in one persistent launch, T handed over
+    through the XCD's L2 ring slots) runs the same arithmetic as the two
+    separate kernels: every output bit-identical.  n > 8 XCD queues x slots,
+    so every ring slot is reused (write-after-read hand-off) several times."""
+    ops = _ops()
+    x = torch.from_numpy(np.stack(rng.synth_images(61 + slots, [shape] * n))).to(DEV)
+    ops.set_option("fused_slots", slots)
+    try:
+        outs = {}
+        for fused in (1, 0):
+            ops.set_option("fused", fused)
+            outs[fused] = [fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True),
+                           fe.encode_batch(x, pn, lfq)]
+        ops.check_device_errors(x.device)
+    finally:
+        ops.set_option("fused", 0)
+        ops.set_option("fused_slots", 2)
+    for (a_list, b_list) in zip(outs[1], outs[0]):
+        for (dp_a, c_a), (dp_b, c_b) in zip(a_list, b_list):
+            assert torch.equal(c_a, c_b)
+            assert torch.equal(dp_a.patch_positions, dp_b.patch_positions)
+            assert torch.equal(dp_a.patch_channels, dp_b.patch_channels)
+            assert torch.equal(dp_a.batched_image_ids, dp_b.batched_image_ids)
+            assert torch.equal(dp_a.key_pad_mask, dp_b.key_pad_mask)
+            assert torch.equal(dp_a.patches.view(torch.int32), dp_b.patches.view(torch.int32))
+            if dp_a._data:
+                assert torch.equal(dp_a._data["scores"].view(torch.int32), dp_b._data["scores"].view(torch.int32))
