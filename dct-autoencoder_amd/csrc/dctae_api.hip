@@ -61,7 +61,9 @@ struct dctae_ctx {
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16),
                                       // 3 row-major with each tile column padded to 16 floats (64-B segments)
-  int cols_kernel = 4;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses)
+  int cols_kernel = 6;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses),
+                                      // 5 (complex-pair LDS, N = 512), 6 (5 with several images per block)
+  int cols_ipb = 2, cols_pf = 1;      // cols_kernel 6: images per block, prefetch of the next slice
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
@@ -448,6 +450,8 @@ struct ChunkJob {
   int n_fr[kVariants], n_fc[kVariants];
   int64_t tw_off[kVariants], post_off_r[kVariants], tw_off_c[kVariants], post_off_c[kVariants];
   int n_rows_tiles, n_cols_tiles;
+  size_t pc_off;      // persistent column kernel (cols_kernel 6): spec-1 images of the job, uniform qw
+  int n_pc, pc_qw;
   int max_T, any_gemm_rows, any_gemm_cols;
   int64_t max_hw;
   size_t lds_rows, lds_cols;
@@ -584,9 +588,11 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
   else if (k == "t_layout" && value >= 0 && value <= 3) ctx->t_layout = (int)value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
-  else if (k == "cols_kernel" && (value == 2 || value == 4)) ctx->cols_kernel = (int)value;
+  else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
+  else if (k == "cols_ipb" && (value == 2 || value == 4)) ctx->cols_ipb = (int)value;
+  else if (k == "cols_pf") ctx->cols_pf = value != 0;
   else if (k == "fused_slots" && value >= 1 && value <= 16) ctx->fused_slots = (int)value;
   else if (k == "fused_bpc" && value >= 1 && value <= 8) ctx->fused_bpc = (int)value;
   else if (k == "fused_rows_pct" && value >= 1 && value <= 99) ctx->fused_rows_pct = (int)value;
@@ -744,7 +750,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       if (pack->row_len[r] < 0 || pack->row_len[r] > S) return fail(ctx, DCTAE_EINVAL, "row_len out of range");
   // fused path: every image square N x N on one specialised plan, row-major T
   {
-    bool ok = ctx->fused && n > 0 && P == 14 && ctx->t_layout == 0 && ctx->cols_kernel == 4;
+    bool ok = ctx->fused && n > 0 && P == 14 && ctx->t_layout == 0;
     for (int i = 0; ok && i < n; ++i) {
       const ImgDesc& d = D[i];
       ok = d.plan_w >= 0 && d.plan_w == d.plan_h && plans[d.plan_w].spec != 0 && d.H == d.W && d.H == D[0].H &&
@@ -827,6 +833,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     std::vector<TileRef> rt, ct;
     std::vector<int2> fr[kVariants];
     std::vector<int4> fc[kVariants];
+    std::vector<int32_t> pc;
+    int pc_qw = 0;
+    bool pc_ok = true;
     j.lds_rows = j.lds_cols = 0;
     for (int i = j.i0; i < j.i1; ++i) {
       const ImgDesc& d = D[i];
@@ -866,6 +875,11 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         const int G = 1;
         for (int c = 0; c < 3; ++c)
           for (int w = 0; w < d.qw; w += G) fc[p.spec].push_back(make_int4(li, c, w, std::min(G, d.qw - w)));
+        if (p.spec == 1 && d.t_strips == 0) {
+          pc_ok = pc_ok && (pc.empty() || d.qw == pc_qw);
+          pc_qw = d.qw;
+          pc.push_back(li);
+        }
         if (p.spec) {
           j.tw_off_c[p.spec] = p.tw_off;
           j.post_off_c[p.spec] = p.post_off;
@@ -914,6 +928,10 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     }
     j.n_rows_tiles = (int)rt.size();
     j.n_cols_tiles = (int)ct.size();
+    // all spec-1 column items of the job in one persistent launch, when their qw agree
+    j.n_pc = (pc_ok && (int)pc.size() * 3 * pc_qw == (int)fc[1].size()) ? (int)pc.size() : 0;
+    j.pc_qw = pc_qw;
+    j.pc_off = E.pb.add(pc.data(), pc.size());
   }
   E.plans_off = E.pb.add(plans.data(), plans.size());
   E.all_desc_off = E.pb.add(D.data(), D.size());
@@ -1102,7 +1120,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         Timer t(ctx, s, "fft_cols");
         launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
                              ctx->fft_tab + j.post_off_c[v], epj, sk, s,
-                             ctx->cols_kernel, ctx->t_layout);
+                             ctx->cols_kernel, ctx->t_layout, v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr,
+                             v == 1 ? j.n_pc : 0, j.pc_qw, ctx->cols_ipb, ctx->cols_pf);
       }
   }
   if (full && E.n_img > 0) {

@@ -631,6 +631,318 @@ __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, c
   }
 }
 
+// ---------------------------------------------------------------------------
+// cols, complex-pair LDS form (N = 512, P = 14): every complex value is one
+// 8-byte LDS word, so each butterfly operand is one ds_read_b64 / ds_write_b64
+// (half the LDS instructions of the split re/im rows of cols4).
+//   z[m][col] at float2 index pad16(m) * 14 + col: the stride-16 Stockham
+//   accesses of a half-wave (16 butterflies x 2 columns) hit 32 distinct
+//   8-byte bank pairs (14 jj mod 32 distinct and even, col parity odd/even);
+//   the Makhoul reorder is applied while copying T in: z[m] = (x[4m], x[4m+2])
+//   for m < M/2, (x[2N-1-4m], x[2N-3-4m]) above;
+//   X[k][col] (real, after the post-processing) at float index k * 14 + col,
+//   in place; the epilogue reads a tile row as 7 ds_read_b64.
+// ---------------------------------------------------------------------------
+// float2 slot of complex element m of column 0 (column col at + col):
+//   zaddr(m) = 15 (m % 16) + 257 (m / 16)
+// * stride-16 reads z[jj + 16 r] (16 butterflies x 2 columns per half-wave):
+//   15 jj + col distinct mod 32 but for one pair -> ds_read_b64 ~conflict-free;
+// * pass-1 writes z[16 jj + r] (257 jj = jj mod 16) and pass-2 writes
+//   z[jj + 16 r] (15 jj) hit 16 distinct 8-byte slots per 16-lane store group;
+// * the m + 16 step (257 x 8 bytes) is beyond ds_read2_b64's 8-bit offset, so
+//   butterfly operands are not paired into ds_read2_b64 (8 LDS cycles for the
+//   pair against 2 + 2 for two ds_read_b64).
+__device__ __forceinline__ constexpr int zaddr(int m) { return 15 * (m & 15) + 257 * (m >> 4); }
+
+struct Cols5Lds {
+  static constexpr int KS = 14;
+  float2 z[zaddr(255) + KS];
+};
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// cols5 pieces.  Thresholds of this thread's epilogue rows: tiles h = g16 + 16 r, row jl.
+template <bool THR>
+__device__ __forceinline__ void cols5_thresholds(const ImgDesc& d, int c, int strip, const EncParams& ep,
+                                                 float2 (&thr_r)[2][7], float* sbias) {
+  constexpr int KS = 14, EPR = 2;
+  const int tid = opaque_tid();
+  const int g16 = tid >> 4, jl = tid & 15;
+  if (THR) {
+#pragma unroll
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh && jl < KS) {
+        const float2* t2 = reinterpret_cast<const float2*>(
+            ep.thr + ((((int64_t)c * ep.maxph + h) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jl * KS);
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
+      }
+    }
+  }
+  if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
+}
+
+// the T slice (512 rows x 14 columns) of (c, strip) into registers: item i = (m, p)
+template <bool NTL>
+__device__ __forceinline__ void cols5_load(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
+                                           f2v (&va)[7], f2v (&vb)[7]) {
+  constexpr int N = 512, M = 256, KS = 14;
+  const int tid = opaque_tid();
+  const f2v* base = reinterpret_cast<const f2v*>(T + (int64_t)c * d.H * d.Kw + strip * KS);
+  const int rs = d.Kw >> 1;
+#pragma unroll
+  for (int u = 0; u < 7; ++u) {
+    if (DCTAE_ABLATE & 1) { va[u] = vb[u] = (f2v){1.0f, 2.0f}; continue; }
+    const int i = tid + 256 * u;
+    const int m = i / 7, p = i - m * 7;
+    const int ya = m < M / 2 ? 4 * m : 2 * N - 1 - 4 * m;
+    const f2v* pa = base + ya * rs + p;
+    const f2v* pb = base + (m < M / 2 ? ya + 2 : ya - 2) * rs + p;
+    va[u] = NTL ? ld_nt(pa) : *pa;
+    vb[u] = NTL ? ld_nt(pb) : *pb;
+  }
+}
+
+// registers -> z, Makhoul reorder: z[m] = (x[4m], x[4m+2]) / (x[2N-1-4m], x[2N-3-4m])
+__device__ __forceinline__ void cols5_stage(float2* zc, const f2v (&va)[7], const f2v (&vb)[7]) {
+  constexpr int KS = 14;
+  const int tid = opaque_tid();
+#pragma unroll
+  for (int u = 0; u < 7; ++u) {
+    const int i = tid + 256 * u;
+    const int m = i / 7, p = i - m * 7;
+    f2v* z = reinterpret_cast<f2v*>(zc + zaddr(m) + 2 * p);
+    z[0] = (f2v){va[u].x, vb[u].x};
+    z[1] = (f2v){va[u].y, vb[u].y};
+  }
+}
+
+// z staged (and a barrier since): column FFT-DCT, post-processing, token epilogue
+template <bool THR>
+__device__ __forceinline__ void cols5_compute(const ImgDesc& d, int c, int strip, float2* zc, const float4* post4,
+                                              const float2* tw_s, const float* sbias, const float2 (&thr_r)[2][7],
+                                              const EncParams& ep, const TokenSinks& sk) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14, M16 = 16, EPR = 2;
+  const int tid = opaque_tid();
+  const int jj = tid & 15, col = tid >> 4;
+  const bool on_col = col < KS;
+  const int g16 = tid >> 4, jl = tid & 15;
+  constexpr int S16 = 257;   // float2 step of m + 16 (zaddr)
+  const cf* zr = reinterpret_cast<const cf*>(zc) + 15 * jj + col;   // z[jj + 16 r] = 15 jj + 257 r
+  // ---- pass 1 (Ns = 1): z[jj + 16 r] -> DFT16 -> z[16 jj + r]
+  if (!(DCTAE_ABLATE & 2)) {
+    cf v[16];
+    if (on_col) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = zr[S16 * r];
+      DFTV<16>::run(v);
+    }
+    __syncthreads();
+    if (on_col) {
+      cf* zw = reinterpret_cast<cf*>(zc) + S16 * jj + col;      // zaddr(16 jj + r) = 257 jj + 15 r
+#pragma unroll
+      for (int r = 0; r < 16; ++r) zw[15 * r] = v[r];
+    }
+    __syncthreads();
+  }
+  // ---- pass 2 (Ns = 16): z[jj + 16 r] * W_M^{r jj} -> DFT16 -> in place
+  if (!(DCTAE_ABLATE & 4)) {
+    cf v[16];
+    if (on_col) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = zr[S16 * r];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        const float2 w = tw_s[r * jj];
+        v[r] = cmulv(v[r], (cf){w.x, w.y});
+      }
+      DFTV<16>::run(v);
+    }
+    __syncthreads();
+    if (on_col) {
+      cf* zw = reinterpret_cast<cf*>(zc) + 15 * jj + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) zw[S16 * r] = v[r];
+    }
+    __syncthreads();
+  }
+  // ---- Makhoul post-processing: k = jj + 16 i; A = Z[k], B = conj Z[M - k] (Z[0] at k = 0, M)
+  cf wv[M16 + 1];
+  if (on_col && !(DCTAE_ABLATE & 8)) {
+    // Z[M - k]: zaddr = 257 (15 - i) + 15 (16 - jj) (jj >= 1), 257 (16 - i) (jj = 0)
+    const cf* zb = reinterpret_cast<const cf*>(zc) + (jj == 0 ? S16 : 15 * (16 - jj)) + col;
+    const float4* ps = post4 + jj;
+#pragma unroll
+    for (int i = 0; i < M16; ++i) {
+      const cf A = zr[S16 * i];
+      cf Bc;
+      if (i == 0) Bc = jj == 0 ? A : zb[S16 * 15];
+      else Bc = zb[S16 * (15 - i)];
+      const cf B = (cf){Bc.x, -Bc.y};
+      const float4 ab = ps[16 * i];
+      const cf al = (cf){ab.x, ab.y}, be = (cf){ab.z, ab.w};
+      const cf s1 = A + B, d1 = A - B;
+      wv[i] = s1.xx * al + s1.yy * (cf){-al.y, al.x} + d1.xx * be + d1.yy * (cf){-be.y, be.x};
+    }
+    if (jj == 0) {   // k = M
+      const cf A = zr[0];
+      const cf B = (cf){A.x, -A.y};
+      const float4 ab = post4[M];
+      wv[M16] = cmulv(A + B, (cf){ab.x, ab.y}) + cmulv(A - B, (cf){ab.z, ab.w});
+    }
+  }
+  __syncthreads();
+  const int Kh = d.Kh;
+  float* X = reinterpret_cast<float*>(zc);
+  if (on_col && !(DCTAE_ABLATE & 8)) {
+    float* xo = X + jj * KS + col;                             // X[k], k = jj + 16 i
+    float* xn = X + (N - jj - 16 * (M16 - 1)) * KS + col;      // X[N - k], from the lowest row
+#pragma unroll
+    for (int i = 0; i < M16; ++i) {
+      const int k = jj + 16 * i;
+      if (k < Kh) xo[16 * KS * i] = wv[i].x;
+      if (k >= 1 && N - k < Kh) xn[16 * KS * (M16 - 1 - i)] = -wv[i].y;
+    }
+    if (jj == 0 && M < Kh) X[M * KS + col] = wv[M16].x;
+  }
+  __syncthreads();
+  // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile, row jl
+  const f2v* X2 = reinterpret_cast<const f2v*>(zc);
+  if (DCTAE_ABLATE & 16) return;
+  if (THR) {
+#pragma unroll
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh) {
+        const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
+        uint32_t am = 0, code = 0;
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) {
+          const f2v v2 = row[p];
+          am = max(am, max(__float_as_uint(v2.x) & 0x7fffffffu, __float_as_uint(v2.y) & 0x7fffffffu));
+          code |= (v2.x >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
+          code |= (v2.y >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
+        }
+        am = jl < KS ? am : 0u;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
+        const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
+        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
+        if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
+        if (sk.raw && jl < KS) {
+#pragma unroll
+          for (int p = 0; p < KS / 2; ++p) {
+            const f2v v2 = row[p];
+            sk.raw[tok * KS * KS + jl * KS + 2 * p] = v2.x;
+            sk.raw[tok * KS * KS + jl * KS + 2 * p + 1] = v2.y;
+          }
+        }
+      }
+    }
+  } else {
+    for (int h = g16; h < d.qh; h += 16) {
+      float vals[KS];
+      const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
+#pragma unroll
+      for (int p = 0; p < KS / 2; ++p) {
+        const f2v v2 = row[p];
+        vals[2 * p] = v2.x;
+        vals[2 * p + 1] = v2.y;
+      }
+      const int f = (h * d.qw + strip) * ep.C + c;
+      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+    }
+  }
+}
+
+
+template <bool THR, bool NTL>
+__device__ __forceinline__ void cols5_item(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
+                                           float2* zc, const float4* post4, const float2* tw_s, float* sbias,
+                                           const EncParams& ep, const TokenSinks& sk) {
+  float2 thr_r[2][7];
+  cols5_thresholds<THR>(d, c, strip, ep, thr_r, sbias);
+  f2v va[7], vb[7];
+  cols5_load<NTL>(d, c, strip, T, va, vb);
+  cols5_stage(zc, va, vb);
+  __syncthreads();
+  cols5_compute<THR>(d, c, strip, zc, post4, tw_s, sbias, thr_r, ep, sk);
+}
+
+template <bool THR>
+__global__ __launch_bounds__(256) void k_fft_cols5(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+  constexpr int M = 256;
+  __shared__ Cols5Lds L;
+  __shared__ float4 post4[M + 1];
+  __shared__ float2 tw_s[M];
+  __shared__ float sbias[32];
+  const float4* p4 = reinterpret_cast<const float4*>(post);
+  for (int i = threadIdx.x; i < M + 1; i += 256) post4[i] = p4[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  cols5_item<THR, false>(d, jb.y, jb.z, ws + d.ws_t, L.z, post4, tw_s, sbias, ep, sk);
+}
+
+// ---------------------------------------------------------------------------
+// cols, several images per block (N = 512): block b owns ONE (channel, tile
+// column) item t and IPB consecutive images: the LDS tables and the item's
+// LFQ thresholds (2.4 MB per image over all items) are loaded once per IPB
+// images, and with PF the next image's T slice is loaded into registers while
+// the current one is transformed.  The image loop is fully unrolled: as a
+// run-time loop the compiler's allocation of the same body needs ~180 VGPRs
+// (82 straight-line).  Items are dealt so that the 8 XCD groups (b % 8) own
+// contiguous runs of tile columns: the 56-byte row slices of neighbouring
+// items share L2 lines on one XCD.
+// ---------------------------------------------------------------------------
+template <bool THR, int IPB, bool PF>
+__global__ __launch_bounds__(256) void k_fft_cols6(const ImgDesc* __restrict__ imgs, const int* __restrict__ list,
+                                                   int n_list, int n_items, int qw,
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+  constexpr int M = 256;
+  __shared__ Cols5Lds L;
+  __shared__ float4 post4[M + 1];
+  __shared__ float2 tw_s[M];
+  __shared__ float sbias[32];
+  const int per_x = (n_items + 7) / 8;
+  const int b = blockIdx.x, slot = b >> 3;
+  const int t = (b & 7) * per_x + slot % per_x, g = slot / per_x;
+  const int k0 = g * IPB;
+  if (t >= n_items || k0 >= n_list) return;
+  const int c = t / qw, strip = t - c * qw;
+  const float4* p4 = reinterpret_cast<const float4*>(post);
+  for (int i = threadIdx.x; i < M + 1; i += 256) post4[i] = p4[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  float2 thr_r[2][7];
+  cols5_thresholds<THR>(imgs[list[k0]], c, strip, ep, thr_r, sbias);
+  f2v va[7], vb[7];
+  if (PF) {
+    const ImgDesc d0 = imgs[list[k0]];
+    cols5_load<false>(d0, c, strip, ws + d0.ws_t, va, vb);
+  }
+#pragma unroll
+  for (int u = 0; u < IPB; ++u) {
+    const int k = k0 + u;
+    if (k < n_list) {
+      const ImgDesc dk = imgs[list[k]];
+      if (!PF) cols5_load<false>(dk, c, strip, ws + dk.ws_t, va, vb);
+      cols5_stage(L.z, va, vb);
+      __syncthreads();
+      if (PF && u + 1 < IPB && k + 1 < n_list) {
+        const ImgDesc dn = imgs[list[k + 1]];
+        cols5_load<false>(dn, c, strip, ws + dn.ws_t, va, vb);   // in flight during the transform
+      }
+      cols5_compute<THR>(dk, c, strip, L.z, post4, tw_s, sbias, thr_r, ep, sk);
+      __syncthreads();
+    }
+  }
+}
+
 template <int N, int R2, int KS, bool THR>
 __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
                                                    const float* __restrict__ ws, const float2* __restrict__ tw,
@@ -865,9 +1177,36 @@ void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int
 
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
-                          hipStream_t s, int kernel, int layout) {
+                          hipStream_t s, int kernel, int layout, const int* cols6_list, int cols6_n, int cols6_qw,
+                          int cols6_ipb, int cols6_pf) {
   if (n_blocks <= 0) return;
-  if (kernel == 4 && (layout == 0 || layout == 3)) {
+  if (kernel == 6 && layout == 0 && spec == 1 && cols6_list && cols6_n > 0) {
+    const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
+    const int n_items = 3 * cols6_qw;
+    const int per_x = (n_items + 7) / 8;
+    const int ipb = cols6_ipb;
+    const int grid = 8 * per_x * ((cols6_n + ipb - 1) / ipb);
+#define DCTAE_COLS6(T, I, P)                                                                                  \
+  hipLaunchKernelGGL((k_fft_cols6<T, I, P>), dim3(grid), dim3(256), 0, s, imgs, cols6_list, cols6_n, n_items, \
+                     cols6_qw, ws, tw, post, ep, sk)
+    if (thr && ipb == 2 && cols6_pf) DCTAE_COLS6(true, 2, true);
+    else if (thr && ipb == 2) DCTAE_COLS6(true, 2, false);
+    else if (thr && ipb == 4 && cols6_pf) DCTAE_COLS6(true, 4, true);
+    else if (thr && ipb == 4) DCTAE_COLS6(true, 4, false);
+    else if (ipb == 2) DCTAE_COLS6(false, 2, false);
+    else DCTAE_COLS6(false, 4, false);
+#undef DCTAE_COLS6
+    return;
+  }
+  if ((kernel == 5 || kernel == 6) && layout == 0 && spec == 1) {
+    const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
+    if (thr)
+      hipLaunchKernelGGL((k_fft_cols5<true>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
+    else
+      hipLaunchKernelGGL((k_fft_cols5<false>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);
+    return;
+  }
+  if (kernel >= 4 && (layout == 0 || layout == 3)) {
     // thresholds path: codes (+ raw) only; every image's qh within the 32 tile rows the kernel walks
     const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
 #define DCTAE_COLS4(NN, RR, T)                                                                                  \

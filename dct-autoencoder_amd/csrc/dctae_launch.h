@@ -52,7 +52,8 @@ void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int
                           const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int prefetch);
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
-                          hipStream_t s, int kernel, int layout);
+                          hipStream_t s, int kernel, int layout, const int* cols6_list = nullptr, int cols6_n = 0,
+                          int cols6_qw = 0, int cols6_ipb = 4, int cols6_pf = 1);
 
 int fused_rows_per_item();
 void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,

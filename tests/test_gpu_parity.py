@@ -362,14 +362,19 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-SPEC_VARIANTS = {  # option sets of the specialised kernels, with the defaults they are reset to
-    "default": ({}, {}),
-    "fused": ({"fused": 1}, {"fused": 0}),
-    "cols_lds_scatter": ({"cols_kernel": 2}, {"cols_kernel": 4}),
-    "t_strips": ({"t_layout": 1}, {"t_layout": 0}),
-    "t_strips16": ({"t_layout": 2}, {"t_layout": 0}),
-    "t_rowmajor_pad16": ({"t_layout": 3}, {"t_layout": 0}),
-    "fused_1slot": ({"fused": 1, "fused_slots": 1}, {"fused": 0, "fused_slots": 2}),
+DEFAULTS = {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2}
+SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
+    "default": {},
+    "fused": {"fused": 1},
+    "fused_1slot": {"fused": 1, "fused_slots": 1},
+    "cols_lds_scatter": {"cols_kernel": 2},
+    "cols_linear": {"cols_kernel": 4},
+    "cols_pairs": {"cols_kernel": 5},
+    "cols_multi4_pf": {"cols_kernel": 6, "cols_ipb": 4, "cols_pf": 1},
+    "cols_multi2_nopf": {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 0},
+    "t_strips": {"t_layout": 1},
+    "t_strips16": {"t_layout": 2},
+    "t_rowmajor_pad16": {"t_layout": 3},
 }
 
 
@@ -380,13 +385,12 @@ def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
     same algorithm, different op order -> tokens within 1e-6 * max|Y|."""
     ops = _ops()
     x = torch.from_numpy(np.stack(rng.synth_images(53, [shape] * 3))).to(DEV)
-    on, off = SPEC_VARIANTS[variant]
-    for k, v in on.items():
+    for k, v in SPEC_VARIANTS[variant].items():
         ops.set_option(k, v)
     try:
         ((dp_s, c_s),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
     finally:
-        for k, v in off.items():
+        for k, v in DEFAULTS.items():
             ops.set_option(k, v)
     ops.set_option("fft_spec", 0)
     try:

@@ -15,7 +15,7 @@ if [ "${BUILD:-0}" = 1 ]; then
 fi
 for m in "$@"; do
   echo "=== ablate $m"
-  DCTAE_LIBRARY=$PWD/_ablate/libdctae_$m.so timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/ablate.log 2>&1
+  DCTAE_LIBRARY=$PWD/_ablate/libdctae_$m.so timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ${ABL_OPTS:-} > gpurun_out/ablate.log 2>&1
   rc=$?
   grep '^{' gpurun_out/ablate.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], json.dumps({k:v['avg_ms'] for k,v in d['kernels'].items()}))"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/ablate.log; fi
