@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the config-3 decode timing")
     ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
 
@@ -197,6 +198,54 @@ def main():
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                         "per_launch": f"{per_launch:.4g} B ({imgs_per_launch:g} images)"}
 
+    # config 3: decode of this step's codes back to RGB, timed the same way
+    decode = None
+    if not args.no_decode:
+        try:
+            dec = fe_mod.BatchDecoder(enc, pn, lfq)
+            packed = enc(x)
+            for _ in range(args.warmup):
+                dec(packed)
+            torch.cuda.synchronize(dev)
+            if timing:
+                ctx.lib.dctae_timing_reset(ctx.h)
+                ctx.lib.dctae_set_timing(ctx.h, 1)
+            if dist:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                dec(packed)
+            torch.cuda.synchronize(dev)
+            if dist:
+                dist.barrier()
+            el_d = time.perf_counter() - t0
+            ops.check_device_errors(dev)
+            dk = {}
+            if timing:
+                import ctypes as C
+                ctx.lib.dctae_set_timing(ctx.h, 0)
+                ctx.lib.dctae_timing_collect(ctx.h)
+                i = 0
+                while True:
+                    name, ms, n = C.c_char_p(), C.c_double(), C.c_int64()
+                    if ctx.lib.dctae_timing_get(ctx.h, i, C.byref(name), C.byref(ms), C.byref(n)) != 0:
+                        break
+                    dk[name.value.decode()] = {"avg_ms": round(ms.value / max(1, n.value), 5)}
+                    i += 1
+            el_t = torch.tensor([el_d], dtype=torch.float64, device=dev)
+            if dist:
+                dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+            el_d = float(el_t.item())
+            dec_bytes = t_tok * (8 * 14 + 32) + S / imgs_per_row + 12 * H * H   # read codes + meta, write RGB
+            decode = {"workload": f"config 3 decode: LFQ codes -> inverse PatchNorm -> IDCT -> RGB, {B} x {H}x{H}",
+                      "value": round(args.steps * B * H * H * world / el_d / 1e6, 2), "unit": "Mpix/s",
+                      "ms_per_step": round(el_d / args.steps * 1e3, 4),
+                      "hbm_roofline_frac": round(dec_bytes * B * world * args.steps / el_d / (HBM_PEAK_GBS * 1e9 * world), 5),
+                      "kernels": dk}
+        except Exception as e:  # noqa: BLE001 — the encode line must still print
+            decode = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import ref_cpu
@@ -228,6 +277,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": kernels,
+            "decode": decode,
             "options": args.opt,
         }
         print(json.dumps(line))

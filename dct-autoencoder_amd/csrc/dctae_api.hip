@@ -67,6 +67,7 @@ struct dctae_ctx {
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
+  int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int fused = 0;                      // measured slower than the two kernels so far (profile: DESIGN.md)
   int fused_slots = 2;                // T slots per XCD (lookahead = slots - 1 images)
   int fused_bpc = 4;                  // resident workgroups per CU
@@ -400,7 +401,7 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   p.npass = np;
   // rows per block of k_fft_rows: 2 (ping-pong) x rows x 3 jobs x (2M+1) floats <= 52 KiB
   p.rows_per_block = std::max(1, std::min(8, (int)(53248 / (24 * (2 * p.M + 1)))));
-  const int64_t need = p.M + 2ll * (p.M + 1);
+  const int64_t need = p.M + 2ll * (p.M + 1) + 2ll * p.M;
   if (ctx->fft_tab_used + need > ctx->fft_tab_cap) {
     p.npass = 0;
     ctx->fft_plans[N] = p;
@@ -422,6 +423,18 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
     h[p.M + 2 * k] = make_float2((float)ar, (float)ai);
     h[p.M + 2 * k + 1] = make_float2((float)bi, (float)-br);  // -i * (br + i bi) = bi - i br
   }
+  for (int k = 0; k < p.M; ++k) {
+    // DCT-III pre-processing (dctae_idct.hip): Z_k = a_k A_k + b_k B_k; stored conjugated
+    const double g = std::sqrt(N / 2.0) / p.M;
+    const double e = 2.0 * pi * k / N;                       // i e^{i e} = (-sin e, cos e)
+    const double t1 = pi * k / (2.0 * N), t2 = pi * (k + p.M) / (2.0 * N);
+    const double pr = 1.0 - std::sin(e), pi_ = std::cos(e);  // 1 + i e^{i e}
+    const double qr = 1.0 + std::sin(e), qi = -std::cos(e);  // 1 - i e^{i e}
+    const double ar = 0.5 * g * (pr * std::cos(t1) - pi_ * std::sin(t1)), ai = 0.5 * g * (pr * std::sin(t1) + pi_ * std::cos(t1));
+    const double br = 0.5 * g * (qr * std::cos(t2) - qi * std::sin(t2)), bi = 0.5 * g * (qr * std::sin(t2) + qi * std::cos(t2));
+    h[p.M + 2 * (p.M + 1) + 2 * k] = make_float2((float)ar, (float)-ai);
+    h[p.M + 2 * (p.M + 1) + 2 * k + 1] = make_float2((float)br, (float)-bi);
+  }
   if (hipMemcpy(ctx->fft_tab + ctx->fft_tab_used, h.data(), need * sizeof(float2), hipMemcpyHostToDevice) !=
       hipSuccess) {
     p.npass = 0;
@@ -430,6 +443,7 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   }
   p.tw_off = ctx->fft_tab_used;
   p.post_off = ctx->fft_tab_used + p.M;
+  p.ipre_off = ctx->fft_tab_used + p.M + 2ll * (p.M + 1);
   ctx->fft_tab_used += need;
   ctx->fft_plans[N] = p;
   *out = p;
@@ -591,6 +605,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
+  else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "cols_ipb" && (value == 2 || value == 4)) ctx->cols_ipb = (int)value;
   else if (k == "cols_pf") ctx->cols_pf = value != 0;
   else if (k == "fused_slots" && value >= 1 && value <= 16) ctx->fused_slots = (int)value;
@@ -1330,6 +1345,83 @@ int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64
   return 0;
 }
 
+// decode of 512 x 512 images on the FFT path: token map -> column DCT-III
+// (tokens expanded in the kernel) -> U -> row DCT-III + IPT -> RGB
+static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDesc>& D, const FftPlan& fpl,
+                      int32_t n_rows, const int32_t* img_lut, int32_t lut_w, const int64_t* ids,
+                      const uint8_t* key_pad, const int64_t* pos, const int64_t* ch, const dctae_norm* norm,
+                      const dctae_lfq* lfq, const int64_t* codes, const float* patches, float* rgb, hipStream_t s) {
+  const int n_img = (int)D.size();
+  const int S = cfg->max_seq_len, P = cfg->patch_size;
+  int64_t wsf = 0;
+  std::vector<int4> cb;
+  std::vector<int2> rb;
+  for (int i = 0; i < n_img; ++i) {
+    ImgDesc& d = D[i];
+    d.ws_t = wsf;
+    wsf += (3ll * d.H * d.Kw + 63) & ~63ll;
+    for (int c = 0; c < 3; ++c)
+      for (int w = 0; w < d.qw; ++w) cb.push_back(make_int4(i, c, w, 0));
+    for (int y0 = 0; y0 < d.H; y0 += 16) rb.push_back(make_int2(i, y0));
+  }
+  const int64_t map_off = wsf;
+  const int64_t map_n = (int64_t)n_img * 3 * cfg->max_patch_h * cfg->max_patch_w;
+  wsf += map_n;
+  int rc;
+  if ((rc = ensure_ws(ctx, (size_t)wsf * 4, 256))) return rc;
+  PlanBuf pb;
+  const size_t d_off = pb.add(D.data(), D.size());
+  const size_t cb_off = pb.add(cb.data(), cb.size());
+  const size_t rb_off = pb.add(rb.data(), rb.size());
+  const size_t lut_off = pb.add(img_lut, (size_t)n_rows * lut_w);
+  order_after_previous(ctx, s);
+  if ((rc = upload_plan(ctx, pb, s))) return rc;
+  uint8_t* pd = ctx->plan_dev;
+  const ImgDesc* dd = (const ImgDesc*)(pd + d_off);
+  int32_t* map = (int32_t*)(ctx->ws + map_off);
+  HIPCHK(ctx, hipMemsetAsync(map, 0xFF, (size_t)map_n * 4, s));
+  DecodeArgs a{};
+  a.ids = ids;
+  a.key_pad = key_pad;
+  a.pos = pos;
+  a.ch = ch;
+  a.codes = codes;
+  a.patches = patches;
+  a.lut = (const int32_t*)(pd + lut_off);
+  a.lut_w = lut_w;
+  a.S = S;
+  a.P = P;
+  a.use_codes = codes ? 1 : 0;
+  if (codes) {
+    a.cb_dim = lfq->codebook_dim;
+    a.ncb = lfq->num_codebooks;
+    a.scale = lfq->codebook_scale;
+    a.median = norm->median_dev;
+    a.b = norm->b_dev;
+    a.eps = norm->eps;
+  }
+  a.maxph = cfg->max_patch_h;
+  a.maxpw = cfg->max_patch_w;
+  a.err = ctx->err_dev;
+  const float2* tw = ctx->fft_tab + fpl.tw_off;
+  const float4* pre = reinterpret_cast<const float4*>(ctx->fft_tab + fpl.ipre_off);
+  {
+    Timer t(ctx, s, "dec_map");
+    launch_dec_map((int64_t)n_rows * S, dd, a, map, s);
+  }
+  {
+    Timer t(ctx, s, "idct_cols");
+    launch_idct_cols512(dd, (const int4*)(pd + cb_off), (int)cb.size(), ctx->ws, map, tw, pre, a, s);
+  }
+  {
+    Timer t(ctx, s, "idct_rows");
+    launch_idct_rows_spec(1, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
+  }
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
+  return 0;
+}
+
 int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut, int32_t lut_w,
                  int32_t n_img, const int32_t* out_hw, const int64_t* out_off, const int32_t* patch_hw,
                  const int64_t* ids, const uint8_t* key_pad, const int64_t* pos, const int64_t* ch,
@@ -1378,6 +1470,14 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
     wsf += 3ll * d.H * d.W;
     max_hw = std::max<int64_t>(max_hw, (int64_t)d.H * d.W);
   }
+  // FFT path (dctae_idct.hip): every image 512 x 512 on the specialised plan, recommended LFQ
+  bool fftdec = ctx->fft_decode && P == 14 && (!codes || (lfq->codebook_dim == 14 && lfq->num_codebooks == 14));
+  for (int i = 0; fftdec && i < n_img; ++i)
+    fftdec = D[i].H == 512 && D[i].W == 512 && D[i].qh <= 32 && D[i].qw <= 32;
+  FftPlan fpl{};
+  if (fftdec) fftdec = fft_plan_for(ctx, 512, P, &fpl) == 0 && fpl.spec == 1;
+  if (fftdec) return decode_fft(ctx, cfg, D, fpl, n_rows, img_lut, lut_w, ids, key_pad, pos, ch, norm, lfq, codes,
+                                patches, rgb, s);
   if ((rc = ensure_ws(ctx, (size_t)wsf * 4, 256))) return rc;
   const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
   std::vector<GemmProblem> probs;

@@ -1,0 +1,378 @@
+// Decode on the FFT path: the inverse of dctae_fft2.hip's encode, for the
+// specialised square sizes (N = 512; rows also N = 224).
+//
+//   codes -> (+-1, inverse PatchNorm) -> spectrum corner Y (3, Kh, Kw)
+//         -> DCT-III along y (column kernel)  -> U (3, H, Kw)  [row-major, like T]
+//         -> DCT-III along x (row kernel) -> IPT -> RGB (3, H, W)
+//
+// The orthonormal DCT-III of length N (torch_dct.idct(norm='ortho'),
+// util.py:337-338 <- FE:149) through one N/2-point complex FFT, the inverse of
+// Makhoul's encode post-processing:
+//   A_k = Ys[k] - i Ys[N-k],  B_k = Ys[M+k] - i Ys[M-k]   (Ys[N] = 0, Ys[0] *= sqrt 2)
+//   Z_k = a_k A_k + b_k B_k,  k < M = N/2,
+//   a_k = g (1 + i e^{2 pi i k/N}) e^{i pi k/(2N)} / 2,  b_k = g (1 - i e^{2 pi i k/N}) e^{i pi (k+M)/(2N)} / 2,
+//   g = sqrt(N/2) / M;  z = sum_k Z_k e^{+2 pi i m k/M}  (computed as conj(FFT(conj Z)));
+//   x[4m] = Re z[m], x[4m+2] = Im z[m] (m < M/2);  x[2N-1-4m] = Re z[m], x[2N-3-4m] = Im z[m] (above).
+// The tables hold conj(a_k), conj(b_k) (float4 per k), so the kernels build
+// conj Z_k = conj(a) (Ys[k] + i Ys[N-k]) + conj(b) (Ys[M+k] + i Ys[M-k]).
+#include "dctae_device.h"
+#include "dctae_fft_common.h"
+#include "dctae_launch.h"
+
+namespace dctae {
+
+namespace {
+
+__device__ __forceinline__ constexpr int ipad16(int m) { return m + (m >> 4); }
+__device__ __forceinline__ constexpr int izaddr(int m) { return 15 * (m & 15) + 257 * (m >> 4); }
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int itid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  return t;
+}
+
+// conj Z_k from the four real inputs
+__device__ __forceinline__ cf pre_z(float yk, float ynk, float ymk, float ymk2, float4 ab) {
+#pragma clang fp contract(fast)
+  const cf A = (cf){yk, ynk}, B = (cf){ymk, ymk2};
+  return cmulv(A, (cf){ab.x, ab.y}) + cmulv(B, (cf){ab.z, ab.w});
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// token map: map[img][c][h][w] = packed slot r * S + j of the token (or -1)
+// (the inverse of the encode's sort/pack; FE:607-656 revert_patching places
+// token (c, h, w) at image[c, h, w]).  Same argument checks as k_scatter_tokens.
+// ---------------------------------------------------------------------------
+__global__ void k_dec_map(int64_t n_tok, const ImgDesc* __restrict__ imgs, DecodeArgs a, int32_t* __restrict__ map) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tok; t += (int64_t)gridDim.x * blockDim.x) {
+    if (a.key_pad[t]) continue;
+    const int64_t r = t / a.S;
+    const int64_t id = a.ids[t];
+    if (id < 0 || id >= a.lut_w) {
+      atomicOr(a.err, 2);
+      continue;
+    }
+    const int im = a.lut[r * a.lut_w + id];
+    if (im < 0) {
+      atomicOr(a.err, 2);
+      continue;
+    }
+    const ImgDesc d = imgs[im];
+    const int64_t c = a.ch[t], h = a.pos[2 * t], w = a.pos[2 * t + 1];
+    if (c < 0 || c >= 3 || h < 0 || h >= d.qh || w < 0 || w >= d.qw) {
+      atomicOr(a.err, 4);
+      continue;
+    }
+    map[(((int64_t)im * 3 + c) * a.maxph + h) * a.maxpw + w] = (int32_t)t;
+  }
+}
+
+void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int32_t* map, hipStream_t s) {
+  const int gx = (int)std::min<int64_t>((n_tok + 255) / 256, 8192);
+  if (gx > 0) hipLaunchKernelGGL(k_dec_map, dim3(gx), dim3(256), 0, s, n_tok, imgs, a, map);
+}
+
+// ---------------------------------------------------------------------------
+// columns (N = H = 512, P = 14): one block = (image, channel, tile column).
+//   1. tokens of the tile column -> X[ky][col] (float, natural rows, zero rows
+//      for ky >= Kh and for tokens not present);
+//   2. conj Z_k for k = jj + 16 i (lane jj of column col) into registers;
+//   3. complex z (zaddr layout, as the encode's cols5) -> radix-16 x 2 FFT;
+//   4. z[m] -> x[y] (natural rows) -> U[c][y][14 strip + col] (56-byte rows).
+// ---------------------------------------------------------------------------
+struct IColsLds {
+  union {
+    float x[512 * 14];
+    float2 z[izaddr(255) + 14];
+  };
+};
+
+__global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                      float* __restrict__ ws, const int32_t* __restrict__ map,
+                                                      const float2* __restrict__ tw, const float4* __restrict__ pre,
+                                                      DecodeArgs a) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14, S16 = 257;
+  __shared__ IColsLds L;
+  __shared__ float4 pre_s[M];
+  __shared__ float2 tw_s[M];
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const int c = jb.y, strip = jb.z;
+  for (int i = threadIdx.x; i < M; i += 256) {
+    pre_s[i] = pre[i];
+    tw_s[i] = tw[i];
+  }
+  const int tid = itid();
+  // ---- 1. tokens -> X rows 14 h + jl (tile h = g16 + 16 r)
+  {
+    const int g16 = tid >> 4, jl = tid & 15;
+    const int PP = KS * KS;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int h = g16 + 16 * r;
+      if (jl < KS && h < 32) {
+        float v[KS];
+#pragma unroll
+        for (int p = 0; p < KS; ++p) v[p] = 0.0f;
+        const int32_t slot = h < d.qh ? map[(((int64_t)jb.x * 3 + c) * a.maxph + h) * a.maxpw + strip] : -1;
+        if (slot >= 0 && !a.use_codes) {   // decode of PatchNorm-space patches (no LFQ)
+          const float* pt = a.patches + (int64_t)slot * PP + jl * KS;
+#pragma unroll
+          for (int p = 0; p < KS; ++p) v[p] = pt[p];
+        } else if (slot >= 0) {
+          const int32_t code = (int32_t)a.codes[(int64_t)slot * a.ncb + jl];
+          const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + jl * KS;
+          const float s2 = a.scale * 2.0f;
+#pragma unroll
+          for (int p = 0; p < KS; ++p) {
+            const float bit = ((code >> (KS - 1 - p)) & 1) ? 1.0f : 0.0f;    // lfq.py:105-134
+            const float y = __fsub_rn(__fmul_rn(bit, s2), a.scale);
+            v[p] = pn_inverse(y, a.median[tab + p], a.b[tab + p], a.eps);    // patchnorm.py:167-177
+          }
+        }
+        f2v* xr = reinterpret_cast<f2v*>(L.x + (KS * h + jl) * KS);
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) xr[p] = (f2v){v[2 * p], v[2 * p + 1]};
+      }
+    }
+    // rows 448 .. 511 (beyond Kh = 448 when qh = 32): zero
+    for (int e = tid; e < (N - KS * 32) * KS; e += 256) L.x[KS * 32 * KS + e] = 0.0f;
+  }
+  __syncthreads();
+  const int jj = tid & 15, col = tid >> 4;
+  const bool on_col = col < KS;
+  // ---- 2. conj Z_k, k = jj + 16 i
+  cf zk[16];
+  if (on_col) {
+    const float* xc = L.x + col;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = jj + 16 * i;
+      float yk = xc[k * KS];
+      const float ynk = k == 0 ? 0.0f : xc[(N - k) * KS];
+      if (k == 0) yk *= 1.41421356237309515f;
+      const float ymk = xc[(M + k) * KS], ymk2 = xc[(M - k) * KS];
+      zk[i] = pre_z(yk, ynk, ymk, ymk2, pre_s[k]);
+    }
+  }
+  __syncthreads();
+  const cf* zr = reinterpret_cast<const cf*>(L.z) + 15 * jj + col;   // z[jj + 16 r]
+  if (on_col) {
+    cf* zw = reinterpret_cast<cf*>(L.z) + 15 * jj + col;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) zw[S16 * i] = zk[i];
+  }
+  __syncthreads();
+  // ---- 3. forward FFT of conj Z (radix 16 x 16, Stockham)
+  {
+    cf v[16];
+    if (on_col) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = zr[S16 * r];
+      DFTV<16>::run(v);
+    }
+    __syncthreads();
+    if (on_col) {
+      cf* zw = reinterpret_cast<cf*>(L.z) + S16 * jj + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) zw[15 * r] = v[r];
+    }
+    __syncthreads();
+  }
+  {
+    cf v[16];
+    if (on_col) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = zr[S16 * r];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        const float2 w = tw_s[r * jj];
+        v[r] = cmulv(v[r], (cf){w.x, w.y});
+      }
+      DFTV<16>::run(v);
+    }
+    __syncthreads();
+    // ---- 4. w[jj + 16 r] -> x rows (natural), z = conj w
+    if (on_col) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = jj + 16 * r;
+        const int ya = m < M / 2 ? 4 * m : 2 * N - 1 - 4 * m;
+        const int yb = m < M / 2 ? ya + 2 : ya - 2;
+        L.x[ya * KS + col] = v[r].x;
+        L.x[yb * KS + col] = -v[r].y;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- 5. U[c][y][14 strip + 2p, +1] for rows y = y0 + 32 k
+  if (tid < 32 * (KS / 2)) {
+    const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
+    f2v* dst = reinterpret_cast<f2v*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
+    const int64_t rstep = (int64_t)16 * d.Kw;
+    const f2v* src = reinterpret_cast<const f2v*>(L.x + y0 * KS) + p;
+#pragma unroll
+    for (int k = 0; k < N / 32; ++k) dst[k * rstep] = src[k * 16 * KS];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// rows: one wave = one image row, 3 channels; 16 rows per block.
+//   U[c][y][kx] (kx < Kw, zero beyond) -> conj Z_k -> FFT -> x[px] -> IPT -> RGB
+// ---------------------------------------------------------------------------
+template <int N, int R2>
+__global__ __launch_bounds__(256) void k_idct_rows2(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                                                    const float* __restrict__ ws, float* __restrict__ rgb,
+                                                    const float2* __restrict__ tw, const float4* __restrict__ pre,
+                                                    ColorMats cm) {
+#pragma clang fp contract(fast)
+  constexpr int R1 = 16;
+  constexpr int M = N / 2;
+  constexpr int MP = ipad16(M - 1) + 2;
+  constexpr int B1 = M / R1, B2 = M / R2;
+  constexpr int PX = (N + 63) / 64;
+  constexpr int KI = (M + 63) / 64;
+  constexpr int RPW = 4;
+  static_assert(R1 * R2 == M && 3 * B1 <= 64 && 3 * B2 <= 64, "plan shape");
+  __shared__ float2 zs[4][3][MP];
+  __shared__ float4 pre_s[M];
+  __shared__ float2 tw_s[M];
+  for (int i = threadIdx.x; i < M; i += 256) {
+    pre_s[i] = pre[i];
+    tw_s[i] = tw[i];
+  }
+  __syncthreads();
+  const int tid = itid();
+  const int wave = tid >> 6, lane = tid & 63;
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  float2(*z)[MP] = zs[wave];
+  const int H = d.H, Kw = d.Kw;
+  const int64_t hw = (int64_t)H * N;
+  const float inv_gamma = 2.3255813121795654296875f;   // fp32(1/0.43), util.py:93
+  // x[px] = sign * (re or im of w[m]) at float offset xo[i] of the channel buffer
+  int xo[PX];
+  float xs[PX];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    const int px = lane + 64 * i;
+    int m, im;
+    if ((px & 1) == 0) {
+      m = px >> 2;
+      im = (px & 2) ? 1 : 0;
+    } else {
+      const int q = 2 * N - 1 - px;   // 4m or 4m + 2
+      m = q >> 2;
+      im = (q & 2) ? 1 : 0;
+    }
+    xo[i] = 2 * ipad16(m) + im;
+    xs[i] = im ? -1.0f : 1.0f;
+  }
+#pragma unroll 1
+  for (int rr = 0, y = jb.y + wave; rr < RPW && y < H; ++rr, y += 4) {
+    // ---- stage the 3 input rows (zero beyond Kw) in the channel buffers
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float* src = ws + d.ws_t + ((int64_t)c * H + y) * Kw;
+      float* zf = reinterpret_cast<float*>(z[c]);
+#pragma unroll
+      for (int i = 0; i < PX; ++i) {
+        const int kx = lane + 64 * i;
+        if (kx < N) zf[kx] = kx < Kw ? src[kx] : 0.0f;
+      }
+    }
+    // ---- conj Z_k per channel (all reads of a channel before its writes)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float* zf = reinterpret_cast<float*>(z[c]);
+      cf zk[KI];
+#pragma unroll
+      for (int i = 0; i < KI; ++i) {
+        const int k = lane + 64 * i;
+        if (k < M) {
+          float yk = zf[k];
+          const float ynk = k == 0 ? 0.0f : zf[N - k];
+          if (k == 0) yk *= 1.41421356237309515f;
+          zk[i] = pre_z(yk, ynk, zf[M + k], zf[M - k], pre_s[k]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < KI; ++i) {
+        const int k = lane + 64 * i;
+        if (k < M) z[c][ipad16(k)] = make_float2(zk[i].x, zk[i].y);
+      }
+    }
+    // ---- pass 1: radix 16, Ns = 1
+    if (lane < 3 * B1) {
+      const int c = lane / B1, j = lane - c * B1;
+      cf v[R1];
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        const float2 t = z[c][ipad16(j + r * B1)];
+        v[r] = (cf){t.x, t.y};
+      }
+      DFTV<R1>::run(v);
+#pragma unroll
+      for (int r = 0; r < R1; ++r) z[c][ipad16(j * R1 + r)] = make_float2(v[r].x, v[r].y);
+    }
+    // ---- pass 2: radix R2, Ns = R1
+    if (lane < 3 * B2) {
+      const int c = lane / B2, j = lane - c * B2;
+      cf v[R2];
+#pragma unroll
+      for (int r = 0; r < R2; ++r) {
+        const float2 t = z[c][ipad16(j + r * B2)];
+        v[r] = (cf){t.x, t.y};
+      }
+#pragma unroll
+      for (int r = 1; r < R2; ++r) {
+        const float2 w = tw_s[r * j];
+        v[r] = cmulv(v[r], (cf){w.x, w.y});
+      }
+      DFTV<R2>::run(v);
+#pragma unroll
+      for (int r = 0; r < R2; ++r) z[c][ipad16(j + r * R1)] = make_float2(v[r].x, v[r].y);
+    }
+    // ---- x -> IPT -> RGB (util.py:85-97)
+    const float* z0 = reinterpret_cast<const float*>(z[0]);
+    const float* z1 = reinterpret_cast<const float*>(z[1]);
+    const float* z2 = reinterpret_cast<const float*>(z[2]);
+    float* dst = rgb + d.rgb_off + (int64_t)y * N;
+#pragma unroll
+    for (int i = 0; i < PX; ++i) {
+      const int px = lane + 64 * i;
+      if (px < N) {
+        const float i0 = xs[i] * z0[xo[i]], i1 = xs[i] * z1[xo[i]], i2 = xs[i] * z2[xo[i]];
+        const float l0 = signed_pow_fast(mat3_row(cm.ipt2lms, 0, i0, i1, i2), inv_gamma);
+        const float l1 = signed_pow_fast(mat3_row(cm.ipt2lms, 1, i0, i1, i2), inv_gamma);
+        const float l2 = signed_pow_fast(mat3_row(cm.ipt2lms, 2, i0, i1, i2), inv_gamma);
+        dst[px] = mat3_row(cm.lms2rgb, 0, l0, l1, l2);
+        dst[hw + px] = mat3_row(cm.lms2rgb, 1, l0, l1, l2);
+        dst[2 * hw + px] = mat3_row(cm.lms2rgb, 2, l0, l1, l2);
+      }
+    }
+  }
+}
+
+void launch_idct_cols512(const ImgDesc* imgs, const int4* blocks, int n_blocks, float* ws, const int32_t* map,
+                         const float2* tw, const float4* pre, const DecodeArgs& a, hipStream_t s) {
+  if (n_blocks > 0)
+    hipLaunchKernelGGL(k_idct_cols512, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, map, tw, pre, a);
+}
+
+void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,
+                           float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s) {
+  if (n_blocks <= 0) return;
+  if (spec == 1)
+    hipLaunchKernelGGL((k_idct_rows2<512, 16>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre, cm);
+  else if (spec == 2)
+    hipLaunchKernelGGL((k_idct_rows2<224, 7>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre, cm);
+}
+
+}  // namespace dctae

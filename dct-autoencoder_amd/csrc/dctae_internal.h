@@ -56,6 +56,7 @@ struct FftPlan {
   int32_t spec, spec_pad;  // compile-time specialised kernel id (dctae_fft2.hip), 0 = generic
   int64_t tw_off;    // float2 offset of W_M^k (k < M) in the FFT table buffer
   int64_t post_off;  // float2 offset of (alpha_k, beta_k), k = 0..M
+  int64_t ipre_off;  // float2 offset of the DCT-III pre-processing table (conj a_k, conj b_k), k < M (dctae_idct.hip)
 };
 
 struct TileRef {

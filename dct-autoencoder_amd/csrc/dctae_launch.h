@@ -55,6 +55,13 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
                           hipStream_t s, int kernel, int layout, const int* cols6_list = nullptr, int cols6_n = 0,
                           int cols6_qw = 0, int cols6_ipb = 4, int cols6_pf = 1);
 
+// decode on the FFT path (dctae_idct.hip)
+void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int32_t* map, hipStream_t s);
+void launch_idct_cols512(const ImgDesc* imgs, const int4* blocks, int n_blocks, float* ws, const int32_t* map,
+                         const float2* tw, const float4* pre, const DecodeArgs& a, hipStream_t s);
+void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,
+                           float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
+
 int fused_rows_per_item();
 void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,
                       const TokenSinks& sk, hipStream_t s);

@@ -397,3 +397,44 @@ class BatchEncoder:
                                        C.byref(self._ncfg), C.byref(self.lcfg), C.byref(self.po), stream_ptr(self.dev))
         self.ctx.check(rc, "dctae_encode")
         return self.out
+
+
+class BatchDecoder:
+    """Pre-planned fused decode for a BatchEncoder's fixed geometry (config 3
+    round trip): LFQ.indices_to_codes -> PatchNorm.inverse_norm ->
+    revert_patching -> IDCT -> IPT -> RGB of the encoder's packed outputs
+    (dctae_decode), images in the reference's enumeration order (rows in
+    order, image ids ascending, FE:619-633) into one (B, 3, H, W) tensor."""
+
+    def __init__(self, enc: "BatchEncoder", patchnorm, lfq):
+        import ctypes as C
+        from ._lib import i32, i64
+        self.enc = enc
+        pl = enc.plan
+        order = sorted(range(enc.B), key=lambda i: (pl.row[i], pl.local_id[i]))
+        self.lut_w = max(pl.local_id) + 1
+        lut = [-1] * (enc.n_rows * self.lut_w)
+        for n, i in enumerate(order):
+            lut[pl.row[i] * self.lut_w + pl.local_id[i]] = n
+        H, W, p = enc.H, enc.W, enc.fe.patch_size
+        per = 3 * H * W
+        self._keep = [i32(lut), i32([H, W] * enc.B), i64([n * per for n in range(enc.B)]),
+                      i32([H // p, W // p] * enc.B)]
+        self._ptr = [C.cast(self._keep[0], C.POINTER(C.c_int32)), C.cast(self._keep[1], C.POINTER(C.c_int32)),
+                     C.cast(self._keep[2], C.POINTER(C.c_int64)), C.cast(self._keep[3], C.POINTER(C.c_int32))]
+        self.norm = patchnorm.state(thresholds=False)
+        self._ncfg = self.norm.c()
+        self.lcfg = lfq.cfg()
+        self.out = torch.empty((enc.B, 3, H, W), dtype=torch.float32, device=enc.dev)
+
+    def __call__(self, packed) -> torch.Tensor:
+        from ._lib import ptr, stream_ptr
+        import ctypes as C
+        e = self.enc
+        lut, hw, offs, phw = self._ptr
+        rc = e.ctx.lib.dctae_decode(e.ctx.h, C.byref(e._cfg), e.n_rows, lut, self.lut_w, e.B, hw, offs, phw,
+                                    ptr(packed["image_ids"]), ptr(packed["key_pad_mask"]), ptr(packed["positions"]),
+                                    ptr(packed["channels"]), C.byref(self._ncfg), C.byref(self.lcfg),
+                                    ptr(packed["codes"]), None, ptr(self.out), stream_ptr(e.dev))
+        e.ctx.check(rc, "dctae_decode")
+        return self.out

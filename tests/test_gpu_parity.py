@@ -440,3 +440,48 @@ def test_fused_matches_unfused_bitwise(fe, pn, lfq, shape, n, slots):
             assert torch.equal(dp_a.patches.view(torch.int32), dp_b.patches.view(torch.int32))
             if dp_a._data:
                 assert torch.equal(dp_a._data["scores"].view(torch.int32), dp_b._data["scores"].view(torch.int32))
+
+
+def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables):
+    """Config 3 decode (codes -> indices_to_codes -> inverse_norm -> revert ->
+    IDCT -> RGB) of 512^2 images on the FFT path (dctae_idct.hip) against the
+    oracle's decode of the same codes (<= 1e-5 x image range) and against the
+    MFMA GEMM decode (two fp32 evaluations of the same transform)."""
+    ops = _ops()
+    x = torch.from_numpy(np.stack(rng.synth_images(71, [(512, 512)] * 3))).to(DEV)
+    ((dp, codes),) = fe.encode_batch(x, pn, lfq)
+    imgs_fft = fe.decode_batch(dp, codes, pn, lfq)
+    ops.set_option("fft_decode", 0)
+    try:
+        imgs_gemm = fe.decode_batch(dp, codes, pn, lfq)
+    finally:
+        ops.set_option("fft_decode", 1)
+    ops.check_device_errors(x.device)
+    kp = dp.key_pad_mask.cpu()
+    y = ref_cpu.lfq_indices_to_codes(codes.cpu(), ref_cpu.LFQConfig())
+    pos = dp.patch_positions.cpu()
+    chs = dp.patch_channels.cpu()
+    xin = ref_cpu.norm_inverse(ref_tables, y, chs, pos[..., 0], pos[..., 1])
+    batch = ref_cpu.Batch(xin, kp, None, dp.batched_image_ids.cpu(), chs, pos, dp.patch_sizes, dp.original_sizes)
+    refs = ref_cpu.postprocess(batch, CFG)
+    assert len(refs) == len(imgs_fft) == len(imgs_gemm) == 3
+    for a, b, r in zip(imgs_fft, imgs_gemm, refs):
+        scale = max(1.0, float(r.abs().max()))
+        ok, dmax = _rgb_close(a.cpu(), r, atol=1e-5 * scale, rtol=2e-5)
+        assert ok, ("fft vs oracle", dmax, scale)
+        ok, dmax = _rgb_close(a.cpu(), b.cpu(), atol=1e-5 * scale, rtol=2e-5)
+        assert ok, ("fft vs gemm", dmax, scale)
+
+
+def test_fft_decode_patches_roundtrip_512(fe):
+    """postprocess (patch-space decode) of a 512^2 preprocess on the FFT path is
+    the inverse of the kept-corner DCT: equal to the oracle's round trip."""
+    x = torch.from_numpy(rng.synth_image(79, 0, 512, 512))
+    item = fe.preprocess(x.to(DEV))
+    (batch,) = list(fe.iter_batches(iter([{k: [v] for k, v in item.items()}]), None))
+    (img,) = fe.postprocess(batch)
+    ob = list(ref_cpu.iter_batches(iter([{k: [v] for k, v in ref_cpu.preprocess(x, CFG).items()}]), CFG, None,
+                                   build_attn_mask=False))[0]
+    (ref,) = ref_cpu.postprocess(ob, CFG)
+    ok, dmax = _rgb_close(img.cpu(), ref, atol=1e-5, rtol=1e-5)
+    assert ok, dmax
