@@ -67,6 +67,7 @@ struct dctae_ctx {
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
+  int sort_kernel = 2;                // 1: bitonic in LDS (1024 threads), 2: rocPRIM block radix sort
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int fused = 0;                      // measured slower than the two kernels so far (profile: DESIGN.md)
   int fused_slots = 2;                // T slots per XCD (lookahead = slots - 1 images)
@@ -606,6 +607,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
+  else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "cols_ipb" && (value == 2 || value == 4)) ctx->cols_ipb = (int)value;
   else if (k == "cols_pf") ctx->cols_pf = value != 0;
   else if (k == "fused_slots" && value >= 1 && value <= 16) ctx->fused_slots = (int)value;
@@ -1141,7 +1143,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   }
   if (full && E.n_img > 0) {
     Timer t(ctx, s, "sort_pack");
-    launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), ep, sk, ps, s);
+    launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), ep, sk, ps, s,
+                     ctx->sort_kernel, E.max_T);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
@@ -1411,7 +1414,7 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
   }
   {
     Timer t(ctx, s, "idct_cols");
-    launch_idct_cols512(dd, (const int4*)(pd + cb_off), (int)cb.size(), ctx->ws, map, tw, pre, a, s);
+    launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
   }
   {
     Timer t(ctx, s, "idct_rows");
@@ -1473,7 +1476,7 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   // FFT path (dctae_idct.hip): every image 512 x 512 on the specialised plan, recommended LFQ
   bool fftdec = ctx->fft_decode && P == 14 && (!codes || (lfq->codebook_dim == 14 && lfq->num_codebooks == 14));
   for (int i = 0; fftdec && i < n_img; ++i)
-    fftdec = D[i].H == 512 && D[i].W == 512 && D[i].qh <= 32 && D[i].qw <= 32;
+    fftdec = D[i].H == 512 && D[i].W == 512 && D[i].qh <= 32 && D[i].qw == D[0].qw;
   FftPlan fpl{};
   if (fftdec) fftdec = fft_plan_for(ctx, 512, P, &fpl) == 0 && fpl.spec == 1;
   if (fftdec) return decode_fft(ctx, cfg, D, fpl, n_rows, img_lut, lut_w, ids, key_pad, pos, ch, norm, lfq, codes,

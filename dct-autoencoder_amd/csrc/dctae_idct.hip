@@ -92,53 +92,56 @@ struct IColsLds {
   };
 };
 
-__global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
-                                                      float* __restrict__ ws, const int32_t* __restrict__ map,
-                                                      const float2* __restrict__ tw, const float4* __restrict__ pre,
-                                                      DecodeArgs a) {
+// one (image, channel, tile column) of the column pass; vt[r][p] = the
+// (code bit 1, code bit 0) values of this thread's tile row r, element p
+// (inverse PatchNorm of +-scale, image-independent: loaded once per block)
+__device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c, int strip, float* __restrict__ ws,
+                                               const int32_t* __restrict__ map, const DecodeArgs& a,
+                                               const float2 (&vt)[2][14], IColsLds& L, const float4* pre_s,
+                                               const float2* tw_s) {
 #pragma clang fp contract(fast)
-  constexpr int N = 512, M = 256, KS = 14, S16 = 257;
-  __shared__ IColsLds L;
-  __shared__ float4 pre_s[M];
-  __shared__ float2 tw_s[M];
-  const int4 jb = blocks[blockIdx.x];
-  const ImgDesc d = imgs[jb.x];
-  const int c = jb.y, strip = jb.z;
-  for (int i = threadIdx.x; i < M; i += 256) {
-    pre_s[i] = pre[i];
-    tw_s[i] = tw[i];
-  }
+  constexpr int N = 512, M = 256, KS = 14, S16 = 257, PP = KS * KS;
   const int tid = itid();
   // ---- 1. tokens -> X rows 14 h + jl (tile h = g16 + 16 r)
   {
     const int g16 = tid >> 4, jl = tid & 15;
-    const int PP = KS * KS;
+    int32_t sl[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int h = g16 + 16 * r;
-      if (jl < KS && h < 32) {
-        float v[KS];
+      sl[r] = map[(((int64_t)img * 3 + c) * a.maxph + (h < d.qh ? h : 0)) * a.maxpw + strip];
+      if (h >= d.qh) sl[r] = -1;
+    }
+    int32_t code[2];
+    float pv[2][KS];
 #pragma unroll
-        for (int p = 0; p < KS; ++p) v[p] = 0.0f;
-        const int32_t slot = h < d.qh ? map[(((int64_t)jb.x * 3 + c) * a.maxph + h) * a.maxpw + strip] : -1;
-        if (slot >= 0 && !a.use_codes) {   // decode of PatchNorm-space patches (no LFQ)
-          const float* pt = a.patches + (int64_t)slot * PP + jl * KS;
+    for (int r = 0; r < 2; ++r) {
+      const int64_t s0 = sl[r] >= 0 ? sl[r] : 0;   // unconditional loads
+      if (a.use_codes) {
+        code[r] = (int32_t)a.codes[s0 * a.ncb + (jl < KS ? jl : 0)];
+      } else {
+        const float* pt = a.patches + s0 * PP + (jl < KS ? jl : 0) * KS;
 #pragma unroll
-          for (int p = 0; p < KS; ++p) v[p] = pt[p];
-        } else if (slot >= 0) {
-          const int32_t code = (int32_t)a.codes[(int64_t)slot * a.ncb + jl];
-          const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + jl * KS;
-          const float s2 = a.scale * 2.0f;
+        for (int p = 0; p < KS; ++p) pv[r][p] = pt[p];
+      }
+    }
 #pragma unroll
-          for (int p = 0; p < KS; ++p) {
-            const float bit = ((code >> (KS - 1 - p)) & 1) ? 1.0f : 0.0f;    // lfq.py:105-134
-            const float y = __fsub_rn(__fmul_rn(bit, s2), a.scale);
-            v[p] = pn_inverse(y, a.median[tab + p], a.b[tab + p], a.eps);    // patchnorm.py:167-177
-          }
-        }
+    for (int r = 0; r < 2; ++r) {
+      const int h = g16 + 16 * r;
+      if (jl < KS) {
         f2v* xr = reinterpret_cast<f2v*>(L.x + (KS * h + jl) * KS);
 #pragma unroll
-        for (int p = 0; p < KS / 2; ++p) xr[p] = (f2v){v[2 * p], v[2 * p + 1]};
+        for (int p = 0; p < KS / 2; ++p) {
+          float v0, v1;
+          if (a.use_codes) {
+            v0 = ((code[r] >> (KS - 1 - 2 * p)) & 1) ? vt[r][2 * p].x : vt[r][2 * p].y;
+            v1 = ((code[r] >> (KS - 2 - 2 * p)) & 1) ? vt[r][2 * p + 1].x : vt[r][2 * p + 1].y;
+          } else {
+            v0 = pv[r][2 * p];
+            v1 = pv[r][2 * p + 1];
+          }
+          xr[p] = sl[r] >= 0 ? (f2v){v0, v1} : (f2v){0.0f, 0.0f};
+        }
       }
     }
     // rows 448 .. 511 (beyond Kh = 448 when qh = 32): zero
@@ -220,6 +223,57 @@ __global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict_
 #pragma unroll
     for (int k = 0; k < N / 32; ++k) dst[k * rstep] = src[k * 16 * KS];
   }
+  __syncthreads();
+}
+
+// block = (channel c, tile column strip) item x IPB consecutive images (the
+// image loop unrolled: straight-line register allocation); items dealt so the
+// 8 XCD groups (b % 8) own contiguous runs of tile columns
+template <int IPB>
+__global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict__ imgs, int n_img, int n_items, int qw,
+                                                      float* __restrict__ ws, const int32_t* __restrict__ map,
+                                                      const float2* __restrict__ tw, const float4* __restrict__ pre,
+                                                      DecodeArgs a) {
+  constexpr int M = 256, KS = 14, PP = KS * KS;
+  __shared__ IColsLds L;
+  __shared__ float4 pre_s[M];
+  __shared__ float2 tw_s[M];
+  const int per_x = (n_items + 7) / 8;
+  const int b = blockIdx.x, slot = b >> 3;
+  const int t = (b & 7) * per_x + slot % per_x, g = slot / per_x;
+  const int i0 = g * IPB;
+  if (t >= n_items || i0 >= n_img) return;
+  const int c = t / qw, strip = t - c * qw;
+  for (int i = threadIdx.x; i < M; i += 256) {
+    pre_s[i] = pre[i];
+    tw_s[i] = tw[i];
+  }
+  // image-independent values of this thread's two tile rows: inverse
+  // PatchNorm of y = +scale (code bit 1) and y = -scale (bit 0)
+  float2 vt[2][KS];
+  {
+    const int tid = itid();
+    const int g16 = tid >> 4, jl = tid & 15;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int h = min(g16 + 16 * r, a.maxph - 1);
+      const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + (jl < KS ? jl : 0) * KS;
+      if (a.use_codes) {
+        const float yp = __fsub_rn(__fmul_rn(1.0f, a.scale * 2.0f), a.scale);   // lfq.py:105-134
+        const float yn = __fsub_rn(__fmul_rn(0.0f, a.scale * 2.0f), a.scale);
+#pragma unroll
+        for (int p = 0; p < KS; ++p) {
+          const float m = a.median[tab + p], bb = a.b[tab + p];
+          vt[r][p] = make_float2(pn_inverse(yp, m, bb, a.eps), pn_inverse(yn, m, bb, a.eps));   // patchnorm.py:167-177
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < IPB; ++u) {
+    const int img = i0 + u;
+    if (img < n_img) idct_col_image(img, imgs[img], c, strip, ws, map, a, vt, L, pre_s, tw_s);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -281,10 +335,15 @@ __global__ __launch_bounds__(256) void k_idct_rows2(const ImgDesc* __restrict__ 
     for (int c = 0; c < 3; ++c) {
       const float* src = ws + d.ws_t + ((int64_t)c * H + y) * Kw;
       float* zf = reinterpret_cast<float*>(z[c]);
+      // unconditional (clamped) loads: a load under `kx < Kw` becomes a branch
+      // with its own vmcnt(0) wait, serialising the row's HBM latencies
+      float lv[PX];
+#pragma unroll
+      for (int i = 0; i < PX; ++i) lv[i] = src[min(lane + 64 * i, Kw - 1)];
 #pragma unroll
       for (int i = 0; i < PX; ++i) {
         const int kx = lane + 64 * i;
-        if (kx < N) zf[kx] = kx < Kw ? src[kx] : 0.0f;
+        if (kx < N) zf[kx] = kx < Kw ? lv[i] : 0.0f;
       }
     }
     // ---- conj Z_k per channel (all reads of a channel before its writes)
@@ -360,10 +419,14 @@ __global__ __launch_bounds__(256) void k_idct_rows2(const ImgDesc* __restrict__ 
   }
 }
 
-void launch_idct_cols512(const ImgDesc* imgs, const int4* blocks, int n_blocks, float* ws, const int32_t* map,
-                         const float2* tw, const float4* pre, const DecodeArgs& a, hipStream_t s) {
-  if (n_blocks > 0)
-    hipLaunchKernelGGL(k_idct_cols512, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, map, tw, pre, a);
+void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, const int32_t* map, const float2* tw,
+                         const float4* pre, const DecodeArgs& a, hipStream_t s) {
+  constexpr int IPB = 2;
+  const int n_items = 3 * qw, per_x = (n_items + 7) / 8;
+  const int grid = 8 * per_x * ((n_img + IPB - 1) / IPB);
+  if (n_img > 0)
+    hipLaunchKernelGGL((k_idct_cols512<IPB>), dim3(grid), dim3(256), 0, s, imgs, n_img, n_items, qw, ws, map, tw,
+                       pre, a);
 }
 
 void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,

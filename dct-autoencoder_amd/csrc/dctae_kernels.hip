@@ -9,6 +9,8 @@
 //    in the reference's op order so it is bit-exact given identical inputs.
 #include "dctae_internal.h"
 #include "dctae_launch.h"
+
+#include <rocprim/block/block_radix_sort.hpp>
 #include "dctae_device.h"
 
 namespace dctae {
@@ -297,9 +299,76 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
   }
 }
 
+// Same contract with rocPRIM's block radix sort (LSD, stable): 32-bit score
+// keys sorted descending, flat indices as values; stability keeps equal
+// scores in ascending index order = the (score desc, index asc) order above.
+// Tokens per image <= 512 x 6 = 3072 (max_patch 32 x 32, 3 channels).
+constexpr int kSortBS = 512, kSortIPT = 6;
+
+__global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restrict__ imgs, EncParams ep,
+                                                        TokenSinks st, PackSinks out) {
+  using Sort = rocprim::block_radix_sort<uint32_t, kSortBS, kSortIPT, uint32_t>;
+  __shared__ typename Sort::storage_type tmp;
+  __shared__ uint16_t order[kSortBS * kSortIPT];
+  const ImgDesc d = imgs[blockIdx.x];
+  const int tid = threadIdx.x;
+  uint32_t keys[kSortIPT], vals[kSortIPT];
+#pragma unroll
+  for (int i = 0; i < kSortIPT; ++i) {
+    const int idx = tid * kSortIPT + i;   // blocked: input order = index order (stability -> index asc)
+    keys[i] = idx < d.T ? float_key(st.scores[d.tok_off + idx]) : 0u;
+    vals[i] = (uint32_t)idx;
+  }
+  Sort().sort_desc_to_striped(keys, vals, tmp);
+#pragma unroll
+  for (int i = 0; i < kSortIPT; ++i) {
+    const int rank = tid + kSortBS * i;
+    if (rank < d.k) order[rank] = (uint16_t)vals[i];
+  }
+  __syncthreads();
+  const int S = ep.S, PP = ep.P * ep.P, C = ep.C;
+  const int64_t base = (int64_t)d.row * S + d.col;
+  for (int t = tid; t < d.k; t += kSortBS) {
+    const uint32_t f = order[t];
+    const int c = f % C, s = f / C, h = s / d.qw, w = s % d.qw;
+    const int64_t o = base + t;
+    *reinterpret_cast<longlong2*>(out.pos + 2 * o) = make_longlong2(h, w);
+    out.ch[o] = c;
+    out.ids[o] = d.local_id;
+    if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
+  }
+  if (out.codes && ep.ncb == 14) {
+    // two codes per lane: one u32 of the u16 staging -> one 16-byte int64 pair (coalesced)
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(st.codes);
+    longlong2* dst = reinterpret_cast<longlong2*>(out.codes);
+    for (int e = tid; e < d.k * 7; e += kSortBS) {
+      const int t = e / 7, q = e - t * 7;
+      const uint32_t v = src[(d.tok_off + order[t]) * 7 + q];
+      dst[(base + t) * 7 + q] = make_longlong2(v & 0xFFFFu, v >> 16);
+    }
+  } else if (out.codes) {
+    const int ncb = ep.ncb;
+    for (int e = tid; e < d.k * ncb; e += kSortBS) {
+      const int t = e / ncb, q = e - t * ncb;
+      out.codes[(base + t) * ncb + q] = st.codes[(d.tok_off + order[t]) * ncb + q];
+    }
+  }
+  if (out.patches || out.raw) {
+    for (int64_t e = tid; e < (int64_t)d.k * PP; e += kSortBS) {
+      const int t = (int)(e / PP), q = (int)(e % PP);
+      const uint32_t f = order[t];
+      if (out.patches) out.patches[(base + t) * PP + q] = st.norm[(d.tok_off + f) * PP + q];
+      if (out.raw) out.raw[(base + t) * PP + q] = st.raw[(d.tok_off + f) * PP + q];
+    }
+  }
+}
+
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
-                      const PackSinks& out, hipStream_t s) {
-  hipLaunchKernelGGL(k_sort_pack, dim3(n_img), dim3(1024), (size_t)np2 * 8, s, imgs, np2, ep, st, out);
+                      const PackSinks& out, hipStream_t s, int kernel, int max_T) {
+  if (kernel == 2 && max_T <= kSortBS * kSortIPT)
+    hipLaunchKernelGGL(k_sort_pack2, dim3(n_img), dim3(kSortBS), 0, s, imgs, ep, st, out);
+  else
+    hipLaunchKernelGGL(k_sort_pack, dim3(n_img), dim3(1024), (size_t)np2 * 8, s, imgs, np2, ep, st, out);
 }
 
 // pad positions j >= row_len[r] of each packed row: the reference pads

@@ -15,7 +15,7 @@ void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_t
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
-                      const PackSinks& out, hipStream_t s);
+                      const PackSinks& out, hipStream_t s, int kernel = 1, int max_T = 1 << 30);
 void launch_pad_fill(const int32_t* row_len, int n_rows, const EncParams& ep, uint8_t* key_pad,
                      const PackSinks& out, hipStream_t s);
 void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t n, int PP, int maxph, int maxpw,
@@ -57,8 +57,8 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
 
 // decode on the FFT path (dctae_idct.hip)
 void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int32_t* map, hipStream_t s);
-void launch_idct_cols512(const ImgDesc* imgs, const int4* blocks, int n_blocks, float* ws, const int32_t* map,
-                         const float2* tw, const float4* pre, const DecodeArgs& a, hipStream_t s);
+void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, const int32_t* map, const float2* tw,
+                         const float4* pre, const DecodeArgs& a, hipStream_t s);
 void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,
                            float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 

@@ -362,7 +362,8 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-DEFAULTS = {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2}
+DEFAULTS = {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2,
+            "sort_kernel": 2}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "fused": {"fused": 1},
@@ -372,6 +373,7 @@ SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS a
     "cols_pairs": {"cols_kernel": 5},
     "cols_multi4_pf": {"cols_kernel": 6, "cols_ipb": 4, "cols_pf": 1},
     "cols_multi2_nopf": {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 0},
+    "sort_bitonic": {"sort_kernel": 1},
     "t_strips": {"t_layout": 1},
     "t_strips16": {"t_layout": 2},
     "t_rowmajor_pad16": {"t_layout": 3},
