@@ -21,6 +21,8 @@ prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
 # library timer names <- kernel symbols
 NAMES = {"k_fft_rows2": "fft_rows", "k_fft_rows": "fft_rows", "k_fft_cols2": "fft_cols", "k_fft_cols": "fft_cols",
+         "k_fft_cols4": "fft_cols", "k_fft_cols5": "fft_cols", "k_fft_cols6": "fft_cols", "k_sort_pack2": "sort_pack",
+         "k_enc_fused": "enc_fused", "k_dec_map": "dec_map", "k_idct_cols512": "idct_cols", "k_idct_rows2": "idct_rows",
          "k_sort_pack": "sort_pack", "k_pad_fill": "pad_fill", "k_gemm_f32": "gemm", "k_rgb_to_ipt": "rgb_to_ipt",
          "k_tile_epilogue": "tile_epilogue", "k_synth": "synth", "k_norm_thresholds": "norm_thresholds"}
 stats = os.path.join(gp, "prof", "run_kernel_stats.csv")
@@ -39,7 +41,8 @@ for sym, d in raw.items():
     ent = {"symbol": sym, **{k: v for k, v in d.items()}}
     if "hbm_read_bytes_corrected" in d and "hbm_write_bytes" in d:
         ent["hbm_bytes_per_dispatch"] = d["hbm_read_bytes_corrected"] + d["hbm_write_bytes"]
-        if big and name in ("fft_rows", "fft_cols", "sort_pack", "pad_fill", "gemm", "tile_epilogue", "rgb_to_ipt"):
+        if big and name in ("fft_rows", "fft_cols", "sort_pack", "pad_fill", "gemm", "tile_epilogue", "rgb_to_ipt",
+                            "enc_fused", "dec_map", "idct_cols", "idct_rows"):
             ent["images_per_dispatch"] = imgs
             ent["hbm_bytes_per_image"] = ent["hbm_bytes_per_dispatch"] / imgs
     out["kernels"][name if name not in out["kernels"] else sym] = ent
