@@ -66,6 +66,9 @@ struct dctae_ctx {
   int cols_ipb = 2, cols_pf = 1;      // cols_kernel 6: images per block, prefetch of the next slice
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
+  int dual_stream = 1;                // several chunks: rows / columns on two streams, T double-buffered
+  hipStream_t s2 = nullptr;
+  std::vector<hipEvent_t> chunk_ev;
   // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
   int sort_kernel = 2;                // 1: bitonic in LDS (1024 threads), 2: rocPRIM block radix sort
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
@@ -486,6 +489,7 @@ struct EncPlan {
   int fused_spec = 0, fused_nr = 0, fused_nc = 0, fused_qw = 0, n_xcd = 1;
   int64_t slot_floats = 0, sync_off = 0;   // floats
   int64_t fused_tw_off = 0, fused_post_off = 0;
+  bool dual = false;   // chunk jobs alternate between two workspace halves (two-stream pipeline)
 };
 
 // ---------------------------------------------------------------------------
@@ -557,6 +561,8 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   for (auto e : ctx->evt_pool) hipEventDestroy(e);
+  for (auto e : ctx->chunk_ev) hipEventDestroy(e);
+  if (ctx->s2) hipStreamDestroy(ctx->s2);
   hipEventDestroy(ctx->plan_evt);
   hipEventDestroy(ctx->done_evt);
   delete ctx;
@@ -606,6 +612,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
+  else if (k == "dual_stream") ctx->dual_stream = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "cols_ipb" && (value == 2 || value == 4)) ctx->cols_ipb = (int)value;
@@ -835,6 +842,18 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     E.ws_need = E.fused_spec ? (size_t)(E.sync_off + 24 + 2ll * n + 2 + 128) * 4 : std::max<size_t>(E.ws_need, (size_t)wsf * 4);
     E.max_T = std::max(E.max_T, j.max_T);
   }
+  // two-stream chunk pipeline: odd chunks use the second workspace half
+  E.dual = !E.fused_spec && ctx->dual_stream && E.jobs.size() > 1;
+  if (E.dual) {
+    const int64_t half = (int64_t)((E.ws_need / 4 + 63) & ~size_t(63));
+    for (size_t k = 1; k < E.jobs.size(); k += 2)
+      for (int i = E.jobs[k].i0; i < E.jobs[k].i1; ++i) {
+        D[i].ws_t += half;
+        D[i].ws_p += half;
+        D[i].ws_y += half;
+      }
+    E.ws_need = (size_t)half * 2 * 4;
+  }
   E.n_tok = tok;
   E.n_img = n;
   {
@@ -990,7 +1009,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout +
                              1024 * ctx->xcd_order + 4096 * ctx->fused + 8192 * ctx->fused_slots +
-                             (1 << 20) * ctx->cols_kernel,
+                             (1 << 20) * ctx->cols_kernel + (1 << 24) * ctx->dual_stream,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1095,51 +1114,86 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     Timer t(ctx, s, "enc_fused");
     launch_enc_fused(E.fused_spec, thr, ctx->n_cu * ctx->fused_bpc, fa, ctx->cm, epj, sk, s);
   }
-  for (auto& j : E.jobs) {
-    if (E.fused_spec) break;
+  // row half / column half of a chunk job on a stream
+  auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
     const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     if (j.any_gemm_rows) {
       {
-        Timer t(ctx, s, "rgb_to_ipt");
-        launch_rgb_to_ipt(dd, nj, j.max_hw, imgs->rgb_dev, ctx->ws, ctx->cm, s);
+        Timer t(ctx, st, "rgb_to_ipt");
+        launch_rgb_to_ipt(dd, nj, j.max_hw, imgs->rgb_dev, ctx->ws, ctx->cm, st);
       }
-      Timer t(ctx, s, "gemm_rows");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, s);
+      Timer t(ctx, st, "gemm_rows");
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st);
     }
     if (j.n_fr[0]) {
-      Timer t(ctx, s, "fft_rows");
+      Timer t(ctx, st, "fft_rows");
       launch_fft_rows(dd, plans_d, (const int2*)(pd + j.fr_off[0]), j.n_fr[0], j.lds_rows, imgs->rgb_dev, ctx->ws,
-                      ctx->fft_tab, ctx->cm, s);
+                      ctx->fft_tab, ctx->cm, st);
     }
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fr[v]) {
-        Timer t(ctx, s, "fft_rows");
+        Timer t(ctx, st, "fft_rows");
         launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
-                             ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, s,
+                             ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st,
                              ctx->rows_prefetch);
       }
+  };
+  auto do_cols = [&](const ChunkJob& j, hipStream_t st) {
+    const int nj = j.i1 - j.i0;
+    const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     if (j.any_gemm_cols) {
       {
-        Timer t(ctx, s, "gemm_cols");
-        launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, s);
+        Timer t(ctx, st, "gemm_cols");
+        launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st);
       }
-      Timer t(ctx, s, "tile_epilogue");
-      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, s);
+      Timer t(ctx, st, "tile_epilogue");
+      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, st);
     }
     if (j.n_fc[0]) {
-      Timer t(ctx, s, "fft_cols");
+      Timer t(ctx, st, "fft_cols");
       launch_fft_cols(dd, plans_d, (const int4*)(pd + j.fc_off[0]), j.n_fc[0], j.lds_cols, ctx->ws, ctx->fft_tab,
-                      epj, sk, s);
+                      epj, sk, st);
     }
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fc[v]) {
-        Timer t(ctx, s, "fft_cols");
+        Timer t(ctx, st, "fft_cols");
         launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
-                             ctx->fft_tab + j.post_off_c[v], epj, sk, s,
+                             ctx->fft_tab + j.post_off_c[v], epj, sk, st,
                              ctx->cols_kernel, ctx->t_layout, v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr,
                              v == 1 ? j.n_pc : 0, j.pc_qw, ctx->cols_ipb, ctx->cols_pf);
       }
+  };
+  const int nJ = E.fused_spec ? 0 : (int)E.jobs.size();
+  if (nJ > 1 && E.dual) {
+    // chunk pipeline on two streams: rows of chunk k (stream s) overlap the
+    // columns of chunk k - 1 (second stream); chunk k's T lives in ws half k % 2,
+    // so rows(k) waits for cols(k - 2).  Chunks are sized so both halves stay
+    // in the Infinity Cache (chunk_bytes).
+    if (!ctx->s2) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+    while ((int)ctx->chunk_ev.size() < 2 * nJ + 1) {
+      hipEvent_t e;
+      HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ctx->chunk_ev.push_back(e);
+    }
+    hipEvent_t* ev_rows = ctx->chunk_ev.data() + 1;
+    hipEvent_t* ev_cols = ctx->chunk_ev.data() + 1 + nJ;
+    HIPCHK(ctx, hipEventRecord(ctx->chunk_ev[0], s));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->s2, ctx->chunk_ev[0], 0));
+    for (int k = 0; k < nJ; ++k) {
+      if (k >= 2) HIPCHK(ctx, hipStreamWaitEvent(s, ev_cols[k - 2], 0));
+      do_rows(E.jobs[k], s);
+      HIPCHK(ctx, hipEventRecord(ev_rows[k], s));
+      HIPCHK(ctx, hipStreamWaitEvent(ctx->s2, ev_rows[k], 0));
+      do_cols(E.jobs[k], ctx->s2);
+      HIPCHK(ctx, hipEventRecord(ev_cols[k], ctx->s2));
+    }
+    HIPCHK(ctx, hipStreamWaitEvent(s, ev_cols[nJ - 1], 0));
+  } else {
+    for (int k = 0; k < nJ; ++k) {
+      do_rows(E.jobs[k], s);
+      do_cols(E.jobs[k], s);
+    }
   }
   if (full && E.n_img > 0) {
     Timer t(ctx, s, "sort_pack");

@@ -363,7 +363,7 @@ def test_thresholds_are_exact(pn):
 
 
 DEFAULTS = {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2,
-            "sort_kernel": 2}
+            "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "fused": {"fused": 1},
@@ -374,6 +374,8 @@ SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS a
     "cols_multi4_pf": {"cols_kernel": 6, "cols_ipb": 4, "cols_pf": 1},
     "cols_multi2_nopf": {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 0},
     "sort_bitonic": {"sort_kernel": 1},
+    "chunks_dual_stream": {"chunk_bytes": 4 << 20, "dual_stream": 1},
+    "chunks_one_stream": {"chunk_bytes": 4 << 20, "dual_stream": 0},
     "t_strips": {"t_layout": 1},
     "t_strips16": {"t_layout": 2},
     "t_rowmajor_pad16": {"t_layout": 3},
