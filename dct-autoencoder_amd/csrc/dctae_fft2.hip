@@ -756,7 +756,7 @@ __device__ __forceinline__ void cols5_compute(const ImgDesc& d, int c, int strip
 #pragma unroll
       for (int r = 1; r < 16; ++r) {
         const float2 w = tw_s[r * jj];
-        v[r] = cmulv(v[r], (cf){w.x, w.y});
+        v[r] = cmul_pk(v[r], (cf){w.x, w.y});
       }
       DFTV<16>::run(v);
     }
@@ -780,17 +780,16 @@ __device__ __forceinline__ void cols5_compute(const ImgDesc& d, int c, int strip
       cf Bc;
       if (i == 0) Bc = jj == 0 ? A : zb[S16 * 15];
       else Bc = zb[S16 * (15 - i)];
-      const cf B = (cf){Bc.x, -Bc.y};
       const float4 ab = ps[16 * i];
       const cf al = (cf){ab.x, ab.y}, be = (cf){ab.z, ab.w};
-      const cf s1 = A + B, d1 = A - B;
-      wv[i] = s1.xx * al + s1.yy * (cf){-al.y, al.x} + d1.xx * be + d1.yy * (cf){-be.y, be.x};
+      const cf s1 = add_conj(A, Bc), d1 = sub_conj(A, Bc);   // A + B, A - B with B = conj Z[M - k]
+      wv[i] = fma_iw(d1, be, fma_x(d1, be, fma_iw(s1, al, mul_x(s1, al))));
     }
     if (jj == 0) {   // k = M
       const cf A = zr[0];
-      const cf B = (cf){A.x, -A.y};
       const float4 ab = post4[M];
-      wv[M16] = cmulv(A + B, (cf){ab.x, ab.y}) + cmulv(A - B, (cf){ab.z, ab.w});
+      const cf s1 = add_conj(A, A), d1 = sub_conj(A, A);
+      wv[M16] = fma_iw(d1, (cf){ab.z, ab.w}, fma_x(d1, (cf){ab.z, ab.w}, cmul_pk(s1, (cf){ab.x, ab.y})));
     }
   }
   __syncthreads();

@@ -164,6 +164,49 @@ __device__ __forceinline__ cf cmulv(cf a, cf w) {
 }
 __device__ __forceinline__ cf mul_mi_v(cf a) { return (cf){a.y, -a.x}; }  // -i * a
 
+// Packed complex ops with the swizzle / sign folded into VOP3P op_sel and neg
+// modifiers (the compiler materialises (a.y, -a.x) with v_mov + v_xor instead).
+// a + (-i) b = (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ cf add_mi(cf a, cf b) {
+  cf d;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+// a - (-i) b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ cf sub_mi(cf a, cf b) {
+  cf d;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+// a + conj(b), a - conj(b)
+__device__ __forceinline__ cf add_conj(cf a, cf b) {
+  cf d;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ cf sub_conj(cf a, cf b) {
+  cf d;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1]" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+// a.x * w   and   a.y * (i w) + c = (c.x - a.y w.y, c.y + a.y w.x): a * w = fma_iw(a, w, mul_x(a, w))
+__device__ __forceinline__ cf mul_x(cf a, cf w) {
+  cf d;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(d) : "v"(a), "v"(w));
+  return d;
+}
+__device__ __forceinline__ cf fma_x(cf a, cf w, cf c) {   // a.x * w + c
+  cf d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
+  return d;
+}
+__device__ __forceinline__ cf fma_iw(cf a, cf w, cf c) {  // a.y * (i w) + c
+  cf d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
+  return d;
+}
+__device__ __forceinline__ cf cmul_pk(cf a, cf w) { return fma_iw(a, w, mul_x(a, w)); }
+
 template <int R>
 struct DFTV;
 
@@ -171,11 +214,11 @@ template <>
 struct DFTV<4> {
   static __device__ __forceinline__ void run(cf* v) {
     const cf t0 = v[0] + v[2], t1 = v[0] - v[2];
-    const cf t2 = v[1] + v[3], t3 = mul_mi_v(v[1] - v[3]);
+    const cf t2 = v[1] + v[3], t3 = v[1] - v[3];
     v[0] = t0 + t2;
     v[2] = t0 - t2;
-    v[1] = t1 + t3;
-    v[3] = t1 - t3;
+    v[1] = add_mi(t1, t3);   // t1 + (-i) t3
+    v[3] = sub_mi(t1, t3);
   }
 };
 
@@ -196,13 +239,23 @@ struct DFTV<16> {
 #pragma unroll
       for (int k1 = 1; k1 < 4; ++k1) {
         const int m = n2 * k1;
-        if (m == 4) a[n2][k1] = mul_mi_v(a[n2][k1]);
-        else a[n2][k1] = cmulv(a[n2][k1], (cf){kCos16[m], -kSin16[m]});
+        if (m != 4) a[n2][k1] = cmulv(a[n2][k1], (cf){kCos16[m], -kSin16[m]});
       }
+    // the W16^4 = -i twiddle of a[2][2] is folded into the k1 = 2 column's DFT4:
+    // its n = 2 input enters as (-i) a[2][1] (t0/t1 of DFTV<4> with +- (-i) terms)
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1) {
       cf b[4] = {a[0][k1], a[1][k1], a[2][k1], a[3][k1]};
-      DFTV<4>::run(b);
+      if (k1 == 2) {
+        const cf t0 = add_mi(b[0], b[2]), t1 = sub_mi(b[0], b[2]);   // b0 +- (-i) b2
+        const cf t2 = b[1] + b[3], t3 = b[1] - b[3];
+        b[0] = t0 + t2;
+        b[2] = t0 - t2;
+        b[1] = add_mi(t1, t3);
+        b[3] = sub_mi(t1, t3);
+      } else {
+        DFTV<4>::run(b);
+      }
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = b[k2];
     }
