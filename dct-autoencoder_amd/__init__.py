@@ -10,7 +10,8 @@ from .dct_patches import DCTPatches, build_attn_mask, from_dict, to_dict  # noqa
 from .feature_extraction import DCTAutoencoderFeatureExtractor, GroupPatchesState  # noqa: F401
 from .lfq import LFQ  # noqa: F401
 from .patchnorm import PatchNorm  # noqa: F401
+from .vector_quantize import VectorQuantize  # noqa: F401
 from . import packing  # noqa: F401
 
-__all__ = ["DCTAutoencoderFeatureExtractor", "DCTPatches", "PatchNorm", "LFQ", "to_dict", "from_dict",
+__all__ = ["DCTAutoencoderFeatureExtractor", "DCTPatches", "PatchNorm", "LFQ", "VectorQuantize", "to_dict", "from_dict",
            "GroupPatchesState", "build_attn_mask", "load_library", "DCTAEError", "DCTAEUnavailable"]

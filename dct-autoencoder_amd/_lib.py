@@ -60,6 +60,15 @@ class PackedOut(C.Structure):
                 ("raw_patches_dev", C.c_void_p), ("scores_dev", C.c_void_p)]
 
 
+class VQCfg(C.Structure):
+    _fields_ = [("dim", C.c_int32), ("heads", C.c_int32), ("codebook_dim", C.c_int32),
+                ("codebook_size", C.c_int32), ("affine", C.c_int32), ("affine_decay", C.c_float),
+                ("w_in_dev", C.c_void_p), ("b_in_dev", C.c_void_p), ("w_out_dev", C.c_void_p),
+                ("b_out_dev", C.c_void_p), ("embed_dev", C.c_void_p), ("codebook_mean_dev", C.c_void_p),
+                ("codebook_variance_dev", C.c_void_p), ("batch_mean_dev", C.c_void_p),
+                ("batch_variance_dev", C.c_void_p), ("batch_initted_dev", C.c_void_p)]
+
+
 _P = C.c_void_p
 _SIGS = {
     "dctae_abi_version": ([], C.c_int),
@@ -80,6 +89,9 @@ _SIGS = {
     "dctae_decode": ([_P, C.POINTER(FECfg), C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.c_int32,
                       C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32), _P, _P, _P, _P,
                       C.POINTER(Norm), C.POINTER(LFQCfg), _P, _P, _P, _P], C.c_int),
+    "dctae_vq_forward": ([_P, C.POINTER(VQCfg), _P, _P, C.c_int64, _P, _P, _P], C.c_int),
+    "dctae_vq_codes_from_indices": ([_P, C.POINTER(VQCfg), _P, C.c_int64, _P, _P], C.c_int),
+    "dctae_vq_output_from_indices": ([_P, C.POINTER(VQCfg), _P, C.c_int64, _P, _P], C.c_int),
     "dctae_check_device_errors": ([_P, _P], C.c_int),
     "dctae_fused_debug_counters": ([_P, C.POINTER(C.c_int32), C.c_int64, _P], C.c_int64),
     "dctae_synth_images": ([_P, C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, _P], C.c_int),

@@ -12,7 +12,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import FECfg, Images, LFQCfg, Norm, PackedOut, Packing, i32, i64, ptr
+from ._lib import FECfg, Images, LFQCfg, Norm, PackedOut, Packing, VQCfg, i32, i64, ptr
 
 
 @dataclass(frozen=True)
@@ -288,6 +288,43 @@ def lfq_codes(idx: torch.Tensor, cfg: LFQCfg) -> torch.Tensor:
     out = torch.empty((*ii.shape[:-1], cfg.num_codebooks * cfg.codebook_dim), dtype=torch.float32, device=dev)
     rc = ctx.lib.dctae_lfq_indices_to_codes(ctx.h, C.byref(cfg), ptr(ii), n, ptr(out), _lib.stream_ptr(dev))
     ctx.check(rc, "dctae_lfq_indices_to_codes")
+    return out
+
+
+def vq_forward(cfg: VQCfg, x: torch.Tensor, mask: Optional[torch.Tensor], want_quantized=True):
+    """x (n, dim) fp32 contiguous on the device; mask (n) bool or None.
+    Returns quantize (n, dim) (None unless wanted) and indices (n, heads)."""
+    dev = _check_dev(x)
+    ctx = _lib.context(dev)
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.ndim != 2 or x.shape[1] != cfg.dim:
+        raise AssertionError(f"VectorQuantize input must be contiguous fp32 (n, {cfg.dim})")
+    n = x.shape[0]
+    m = None
+    if mask is not None:
+        if mask.shape != (n,):
+            raise AssertionError("mask must be (n,)")
+        m = mask.to(device=dev, dtype=torch.uint8).contiguous()
+    q = torch.empty_like(x) if want_quantized else None
+    idx = torch.empty((n, cfg.heads), dtype=torch.long, device=dev)
+    rc = ctx.lib.dctae_vq_forward(ctx.h, C.byref(cfg), ptr(x), ptr(m), n, ptr(q), ptr(idx), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_vq_forward")
+    return q, idx
+
+
+def vq_from_indices(cfg: VQCfg, idx: torch.Tensor, project_out: bool) -> torch.Tensor:
+    """idx (n, heads) -> codes (n, heads*codebook_dim) or project_out(codes) (n, dim)."""
+    dev = _check_dev(idx)
+    ctx = _lib.context(dev)
+    ii = idx.long().contiguous()
+    if ii.ndim != 2 or ii.shape[1] != cfg.heads:
+        raise AssertionError("indices must be (n, heads)")
+    n = ii.shape[0]
+    width = cfg.dim if project_out else cfg.heads * cfg.codebook_dim
+    out = torch.empty((n, width), dtype=torch.float32, device=dev)
+    fn = ctx.lib.dctae_vq_output_from_indices if project_out else ctx.lib.dctae_vq_codes_from_indices
+    rc = fn(ctx.h, C.byref(cfg), ptr(ii), n, ptr(out), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_vq_from_indices")
+    check_device_errors(dev)
     return out
 
 

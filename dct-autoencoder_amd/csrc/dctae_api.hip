@@ -81,6 +81,9 @@ struct dctae_ctx {
   int n_cu = 256;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
+  // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
+  uint8_t* vq_ws = nullptr;
+  size_t vq_bytes = 0;
   size_t st_bytes = 0;
   // cached encode plan
   std::vector<int64_t> enc_key;
@@ -555,6 +558,7 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->err_dev) hipFree(ctx->err_dev);
   if (ctx->fft_tab) hipFree(ctx->fft_tab);
   if (ctx->st_ws) hipFree(ctx->st_ws);
+  if (ctx->vq_ws) hipFree(ctx->vq_ws);
   delete ctx->enc_plan;
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
@@ -697,6 +701,7 @@ int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
   if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
   if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
   if (h & 8) return fail(ctx, DCTAE_EHIP, "fused encode: a dependence wait timed out (outputs invalid)");
+  if (h & 16) return fail(ctx, DCTAE_EINVAL, "VectorQuantize index out of range of the codebook");
   return 0;
 }
 
@@ -1399,6 +1404,151 @@ int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64
   Timer t(ctx, s, "lfq_codes");
   launch_lfq_codes(idx, n, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, codes, s);
   HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+// ---- VectorQuantize inference (dctae_vq.hip) --------------------------------
+static int vq_check(dctae_ctx* ctx, const dctae_vq* vq) {
+  if (!vq || vq->codebook_dim != 16 || vq->heads < 1 || vq->codebook_size < 1 || vq->dim < 1 || !vq->embed_dev)
+    return fail(ctx, DCTAE_EINVAL, "bad VectorQuantize config (codebook_dim 16, heads >= 1, codebook_size >= 1)");
+  const bool proj = vq->dim != vq->heads * vq->codebook_dim;   // vector_quantize.py:725-728
+  if (proj && (!vq->w_in_dev || !vq->b_in_dev || !vq->w_out_dev || !vq->b_out_dev))
+    return fail(ctx, DCTAE_EINVAL, "VectorQuantize: dim != heads * codebook_dim needs project_in / project_out");
+  if (vq->affine && (!vq->codebook_mean_dev || !vq->codebook_variance_dev || !vq->batch_mean_dev ||
+                     !vq->batch_variance_dev || !vq->batch_initted_dev))
+    return fail(ctx, DCTAE_EINVAL, "VectorQuantize: affine_param needs codebook / batch statistics");
+  return 0;
+}
+
+static int vq_scratch(dctae_ctx* ctx, size_t need) {
+  if (need <= ctx->vq_bytes) return 0;
+  HIPCHK(ctx, hipDeviceSynchronize());
+  if (ctx->vq_ws) hipFree(ctx->vq_ws);
+  ctx->vq_ws = nullptr;
+  ctx->vq_bytes = 0;
+  if (hipMalloc((void**)&ctx->vq_ws, need) != hipSuccess)
+    return fail(ctx, DCTAE_ENOMEM, "VectorQuantize scratch allocation of " + std::to_string(need) + " bytes failed");
+  ctx->vq_bytes = need;
+  return 0;
+}
+
+// O (n, N) = A (n, K) W^T (N, K) + bias, on k_gemm_f32 (plan uploaded through the shared plan buffer)
+static int vq_linear(dctae_ctx* ctx, const float* A, int64_t n, int K, const float* W, const float* bias, int N,
+                     float* O, const uint8_t* mask, const float* orig, hipStream_t s, const char* name) {
+  GemmProblem g = gemm(A, 0, K, 1, W, 0, K, 1, O, 0, N, 1, (int)n, N, K, 1);
+  std::vector<TileRef> t;
+  add_tiles(t, 0, g);
+  PlanBuf pb;
+  const size_t g_off = pb.add(&g, 1);
+  const size_t t_off = pb.add(t.data(), t.size());
+  int rc;
+  if ((rc = upload_plan(ctx, pb, s))) return rc;
+  Timer tm(ctx, s, name);
+  launch_gemm(1, (const GemmProblem*)(ctx->plan_dev + g_off), (const TileRef*)(ctx->plan_dev + t_off), (int)t.size(), s);
+  launch_vq_bias(O, bias, n, N, mask, orig, s);
+  return 0;
+}
+
+int dctae_vq_forward(dctae_ctx* ctx, const dctae_vq* vq, const float* x, const uint8_t* mask, int64_t n_tok,
+                     float* quantize, int64_t* indices, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipSetDevice(ctx->device);
+  int rc = vq_check(ctx, vq);
+  if (rc) return rc;
+  if (n_tok < 0 || (n_tok > 0 && (!x || !indices))) return fail(ctx, DCTAE_EINVAL, "bad VectorQuantize tensors");
+  if (n_tok == 0) return 0;
+  if (n_tok > (int64_t)INT32_MAX / 64) return fail(ctx, DCTAE_EINVAL, "VectorQuantize: too many tokens in one call");
+  hipStream_t s = (hipStream_t)stream;
+  const int H = vq->heads, D = vq->codebook_dim, C = vq->codebook_size, HD = H * D;
+  const bool proj = vq->dim != HD;
+  const int64_t nv = n_tok * H;
+  // scratch: acc (64 doubles) | et (C*D) | y2 (C) | xp (n*HD, projected only) | xq (n*HD)
+  const size_t acc_b = 64 * sizeof(double);
+  const size_t et_b = ((size_t)C * D * 4 + 255) & ~size_t(255);
+  const size_t y2_b = ((size_t)C * 4 + 255) & ~size_t(255);
+  const size_t v_b = ((size_t)nv * D * 4 + 255) & ~size_t(255);
+  const bool need_xq = quantize != nullptr;
+  if ((rc = vq_scratch(ctx, acc_b + et_b + y2_b + (proj ? v_b : 0) + ((need_xq && (proj || mask)) ? v_b : 0))))
+    return rc;
+  uint8_t* p = ctx->vq_ws;
+  double* acc = (double*)p;
+  float* et = (float*)(p + acc_b);
+  float* y2 = (float*)(p + acc_b + et_b);
+  uint8_t* q = p + acc_b + et_b + y2_b;
+  float* xp = proj ? (float*)q : const_cast<float*>(x);
+  if (proj) q += v_b;
+  // codes: straight into quantize when nothing follows them
+  float* xq = need_xq ? ((proj || mask) ? (float*)q : quantize) : nullptr;
+  order_after_previous(ctx, s);
+  if (proj && (rc = vq_linear(ctx, x, n_tok, vq->dim, vq->w_in_dev, vq->b_in_dev, HD, xp, nullptr, nullptr, s,
+                              "vq_project_in")))
+    return rc;
+  {
+    Timer t(ctx, s, "vq_codebook");
+    if (vq->affine) {
+      HIPCHK(ctx, hipMemsetAsync(acc, 0, acc_b, s));
+      launch_vq_stats(xp, mask, n_tok, H, acc, s);
+    }
+    launch_vq_codebook(acc, vq->batch_mean_dev, vq->batch_variance_dev, vq->batch_initted_dev, vq->affine_decay,
+                       vq->affine, vq->embed_dev, vq->codebook_mean_dev, vq->codebook_variance_dev, C, et, y2, s);
+  }
+  {
+    Timer t(ctx, s, "vq_assign");
+    launch_vq_assign(xp, nv, H, et, y2, C, xq, indices, s);
+  }
+  if (need_xq) {
+    if (proj) {
+      if ((rc = vq_linear(ctx, xq, n_tok, HD, vq->w_out_dev, vq->b_out_dev, vq->dim, quantize, mask, x, s,
+                          "vq_project_out")))
+        return rc;
+    } else if (mask) {
+      HIPCHK(ctx, hipMemcpyAsync(quantize, xq, sizeof(float) * nv * D, hipMemcpyDeviceToDevice, s));
+      launch_vq_bias(quantize, nullptr, n_tok, HD, mask, x, s);
+    }
+  }
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
+  return 0;
+}
+
+int dctae_vq_codes_from_indices(dctae_ctx* ctx, const dctae_vq* vq, const int64_t* idx, int64_t n, float* codes,
+                                void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipSetDevice(ctx->device);
+  int rc = vq_check(ctx, vq);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && (!idx || !codes))) return fail(ctx, DCTAE_EINVAL, "bad VectorQuantize tensors");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "vq_codes");
+  launch_vq_codes(idx, n * vq->heads, vq->embed_dev, vq->codebook_size, codes, ctx->err_dev, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_vq_output_from_indices(dctae_ctx* ctx, const dctae_vq* vq, const int64_t* idx, int64_t n, float* out,
+                                 void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipSetDevice(ctx->device);
+  int rc = vq_check(ctx, vq);
+  if (rc) return rc;
+  if (n < 0 || (n > 0 && (!idx || !out))) return fail(ctx, DCTAE_EINVAL, "bad VectorQuantize tensors");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int HD = vq->heads * vq->codebook_dim;
+  if (vq->dim == HD) return dctae_vq_codes_from_indices(ctx, vq, idx, n, out, stream);
+  if ((rc = vq_scratch(ctx, ((size_t)n * HD * 4 + 255) & ~size_t(255)))) return rc;
+  float* codes = (float*)ctx->vq_ws;
+  order_after_previous(ctx, s);
+  {
+    Timer t(ctx, s, "vq_codes");
+    launch_vq_codes(idx, n * vq->heads, vq->embed_dev, vq->codebook_size, codes, ctx->err_dev, s);
+  }
+  if ((rc = vq_linear(ctx, codes, n, HD, vq->w_out_dev, vq->b_out_dev, vq->dim, out, nullptr, nullptr, s,
+                      "vq_project_out")))
+    return rc;
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
   return 0;
 }
 

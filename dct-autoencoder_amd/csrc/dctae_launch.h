@@ -24,6 +24,16 @@ void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t 
 void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float scale, float* q, int64_t* idx,
                         hipStream_t s);
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
+// VectorQuantize inference (dctae_vq.hip)
+void launch_vq_bias(float* y, const float* bias, int64_t n, int cols, const uint8_t* mask, const float* orig,
+                    hipStream_t s);
+void launch_vq_stats(const float* xp, const uint8_t* mask, int64_t n_tok, int heads, double* acc, hipStream_t s);
+void launch_vq_codebook(const double* acc, float* bm, float* bv, int32_t* init, float decay, int affine,
+                        const float* embed, const float* cm, const float* cv, int C, float* et, float* y2,
+                        hipStream_t s);
+void launch_vq_assign(const float* xp, int64_t nv, int heads, const float* et, const float* y2, int C, float* xq,
+                      int64_t* ind, hipStream_t s);
+void launch_vq_codes(const int64_t* ind, int64_t nv, const float* embed, int C, float* out, int* err, hipStream_t s);
 void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s);
 
 // PatchNorm training statistics (dctae_stats.hip)

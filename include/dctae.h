@@ -191,6 +191,54 @@ int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, 
 int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev,
                                int64_t n, float* codes_dev, void* stream);
 
+/* VectorQuantize (vector_quantize.py:675-1050) as the model builds it
+ * (modeling_dct_autoencoder.py:76-77): euclidean codebook shared by the
+ * heads, codebook_dim 16, kmeans-initialised, affine codebook parameters,
+ * eval (inference) mode.  Weights are fp32 device tensors with torch's
+ * layouts; w_in/b_in/w_out/b_out are NULL when dim == heads * codebook_dim
+ * (project_in/out = Identity, vector_quantize.py:727-728).  The batch affine
+ * statistics are state the forward updates even in eval
+ * (vector_quantize.py:353-359): batch_mean/batch_variance (codebook_dim
+ * floats each) and *batch_initted_dev (0 until the first forward). */
+typedef struct {
+  int32_t dim;
+  int32_t heads;
+  int32_t codebook_dim;     /* 16 */
+  int32_t codebook_size;
+  int32_t affine;           /* affine_param (the model sets True) */
+  float affine_decay;       /* affine_param_batch_decay, 0.99 */
+  const float* w_in_dev;    /* (heads*codebook_dim, dim) */
+  const float* b_in_dev;    /* (heads*codebook_dim) */
+  const float* w_out_dev;   /* (dim, heads*codebook_dim) */
+  const float* b_out_dev;   /* (dim) */
+  const float* embed_dev;   /* _codebook.embed (1, codebook_size, codebook_dim) */
+  const float* codebook_mean_dev;      /* (codebook_dim) */
+  const float* codebook_variance_dev;  /* (codebook_dim) */
+  float* batch_mean_dev;               /* in/out state (codebook_dim) */
+  float* batch_variance_dev;           /* in/out state (codebook_dim) */
+  int32_t* batch_initted_dev;          /* in/out state: 0 -> first forward sets the statistics */
+} dctae_vq;
+
+/* VectorQuantize.forward, eval (vector_quantize.py:855-1050): x (n_tok, dim)
+ * fp32 (the reference's (b, n, dim) flattened), optional mask (n_tok) u8
+ * (NULL = all valid).  Writes quantize (n_tok, dim) = where(mask,
+ * project_out(codes), x) (nullable) and indices (n_tok, heads) int64
+ * ('b n h').  Updates the batch statistics in place. */
+int dctae_vq_forward(dctae_ctx* ctx, const dctae_vq* vq, const float* x_dev, const uint8_t* mask_dev,
+                     int64_t n_tok, float* quantize_dev, int64_t* indices_dev, void* stream);
+
+/* VectorQuantize.get_codes_from_indices (vector_quantize.py:820-841), shared
+ * codebook: the raw codebook rows, (n, heads * codebook_dim) for indices
+ * (n, heads).  Out-of-range indices raise (DCTAE_EINVAL via
+ * dctae_check_device_errors) like the reference's IndexError. */
+int dctae_vq_codes_from_indices(dctae_ctx* ctx, const dctae_vq* vq, const int64_t* indices_dev, int64_t n,
+                                float* codes_dev, void* stream);
+
+/* VectorQuantize.get_output_from_indices (vector_quantize.py:833-836):
+ * project_out(get_codes_from_indices(indices)), (n, dim). */
+int dctae_vq_output_from_indices(dctae_ctx* ctx, const dctae_vq* vq, const int64_t* indices_dev, int64_t n,
+                                 float* out_dev, void* stream);
+
 /* Decode of a packed batch back to RGB: FE.postprocess (FE:289-310) =
  * revert_patching (FE:607-656) -> zero pad to (3,H,W) -> idct2 -> ipt_to_rgb.
  * With codes_dev != NULL the tokens are first LFQ.indices_to_codes

@@ -513,6 +513,80 @@ def lfq_indices_to_codes(idx: torch.Tensor, cfg: LFQConfig, project_out=None) ->
 
 
 # ---------------------------------------------------------------------------
+# VectorQuantize inference (vector_quantize.py), as the model
+# builds it (modeling_dct_autoencoder.py:76-77): euclidean codebook shared by
+# all heads (separate_codebook_per_head=False), codebook_dim 16, affine_param,
+# learnable codebook, kmeans already run (initted), eval mode.
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class VQState:
+    w_in: torch.Tensor            # project_in.weight (H*d, dim)          vector_quantize.py:727
+    b_in: torch.Tensor            # project_in.bias   (H*d,)
+    w_out: torch.Tensor           # project_out.weight (dim, H*d)         vector_quantize.py:728
+    b_out: torch.Tensor
+    embed: torch.Tensor           # _codebook.embed (1, C, d)             vector_quantize.py:283-288
+    codebook_mean: torch.Tensor   # (1, 1, d)                             vector_quantize.py:300-303
+    codebook_variance: torch.Tensor
+    batch_mean: Optional[torch.Tensor] = None       # (1, 1, d), None until the first forward (:298)
+    batch_variance: Optional[torch.Tensor] = None
+    heads: int = 1
+    decay: float = 0.99           # affine_param_batch_decay (:245)
+
+
+def vq_update_with_decay(old: Optional[torch.Tensor], new: torch.Tensor, decay: float) -> torch.Tensor:
+    """vector_quantize.py:330-343 (no *_needs_init attribute for batch stats)."""
+    if old is None:
+        return new.detach()
+    return old * decay + new.detach() * (1 - decay)
+
+
+def vq_forward_eval(st: VQState, x: torch.Tensor, mask: Optional[torch.Tensor]):
+    """VectorQuantize.forward in eval mode (vector_quantize.py:855-1050) with
+    EuclideanCodebook.forward (:424-508).  Returns (quantize (b,n,dim),
+    embed_ind (b,n,h) int64, new VQState) — the batch affine statistics are
+    updated even in eval mode (:353-359)."""
+    b, n, dim = x.shape
+    h = st.heads
+    d = st.embed.shape[-1]
+    xp = torch.nn.functional.linear(x, st.w_in, st.b_in)                 # :883 project_in
+    xp = xp.reshape(b, n, h, d).permute(0, 2, 1, 3).reshape(1, b * h, n, d)   # :888 '1 (b h) n d'
+    flatten = xp.reshape(1, b * h * n, d)                                 # :444 pack 'h * d'
+    data = flatten
+    if mask is not None:
+        m = mask[:, None, :].expand(b, h, n).reshape(1, b * h * n)          # :447 repeat
+        data = flatten[m].reshape(1, -1, d)                               # :367-369
+    new_mean = data.mean(dim=1, keepdim=True)                             # :373 reduce mean
+    new_var = torch.var(data, dim=1, unbiased=False, keepdim=True)        # :374 var_fn
+    bm = vq_update_with_decay(st.batch_mean, new_mean, st.decay)
+    bv = vq_update_with_decay(st.batch_variance, new_var, st.decay)
+    codebook_std = st.codebook_variance.clamp(min=1e-5).sqrt()           # :458
+    batch_std = bv.clamp(min=1e-5).sqrt()                                  # :459
+    embed = (st.embed - st.codebook_mean) * (batch_std / codebook_std) + bm   # :460
+    x2 = (flatten ** 2).sum(-1)                                           # :29-33 cdist
+    y2 = (embed ** 2).sum(-1)
+    xy = torch.einsum("b i d, b j d -> b i j", flatten, embed) * -2
+    dist = -(x2[..., :, None] + y2[..., None, :] + xy).sqrt()             # :462
+    ind = dist.argmax(dim=-1)                                             # :70-90 gumbel_sample, eval
+    quant = embed[0][ind[0]]                                              # :219-223 batched_embedding
+    quant = quant.reshape(b, h, n, d).permute(0, 2, 1, 3).reshape(b, n, h * d)   # :1032
+    out = torch.nn.functional.linear(quant, st.w_out, st.b_out)          # :1036 project_out
+    if mask is not None:
+        out = torch.where(mask[..., None], out, x)                         # :1044-1048
+    ind = ind.reshape(b, h, n).permute(0, 2, 1)                           # :989 '1 (b h) n -> b n h'
+    new_st = VQState(st.w_in, st.b_in, st.w_out, st.b_out, st.embed, st.codebook_mean, st.codebook_variance,
+                     bm, bv, st.heads, st.decay)
+    return out, ind, new_st, dist
+
+
+def vq_codes_from_indices(st: VQState, ind: torch.Tensor) -> torch.Tensor:
+    """vector_quantize.py:820-841 (shared codebook: raw embed rows, no affine)."""
+    codes = st.embed[0][ind]                                              # '... h d'
+    return codes.reshape(*ind.shape[:-1], -1)
+
+
+# ---------------------------------------------------------------------------
 # a11 / a12: unpatch + inverse transform (FE:289-310, 607-656)
 # ---------------------------------------------------------------------------
 

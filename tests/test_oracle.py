@@ -189,3 +189,28 @@ def test_iter_batches_quirks_match_reference():
                     a = _tok_map(b.patch_positions[r].numpy()[sel], b.patch_channels[r].numpy()[sel])
                     t = _tok_map(g[pre + "positions"][r][sel], g[pre + "channels"][r][sel])
                     assert a.keys() == t.keys()
+
+
+def _vq_state():
+    g = golden("vq_ref.npz")
+    t = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    st = ref_cpu.VQState(t("w_in"), t("b_in"), t("w_out"), t("b_out"), t("embed"), t("codebook_mean"),
+                         t("codebook_variance"), heads=int(g["heads"]))
+    return g, st
+
+
+def test_vq_oracle_matches_reference():
+    """oracle.vq_forward_eval == the reference VectorQuantize (eval, model
+    configuration) on two consecutive masked batches, including the batch
+    affine statistics it carries between calls (vector_quantize.py:353-359)."""
+    g, st = _vq_state()
+    for step in range(2):
+        x = torch.from_numpy(g[f"x{step}"])
+        mask = torch.from_numpy(g[f"mask{step}"])
+        q, ind, st, _ = ref_cpu.vq_forward_eval(st, x, mask)
+        assert torch.equal(ind, torch.from_numpy(g[f"indices{step}"]))
+        assert torch.allclose(q, torch.from_numpy(g[f"quantize{step}"]), atol=1e-6, rtol=1e-6)
+        assert torch.allclose(st.batch_mean, torch.from_numpy(g[f"batch_mean{step}"]), atol=1e-7, rtol=1e-6)
+        assert torch.allclose(st.batch_variance, torch.from_numpy(g[f"batch_variance{step}"]), atol=1e-7, rtol=1e-6)
+    codes = ref_cpu.vq_codes_from_indices(st, torch.from_numpy(g["indices0"]))
+    assert torch.equal(codes, torch.from_numpy(g["codes_from_indices0"]))

@@ -9,7 +9,7 @@ if [ "${BUILD:-0}" = 1 ]; then
   cd dct-autoencoder_amd/csrc
   for m in "$@"; do
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -std=c++17 -ffp-contract=off -DDCTAE_ABLATE=$m \
-      -o ../../_ablate/libdctae_$m.so dctae_kernels.hip dctae_fft.hip dctae_fft2.hip dctae_idct.hip dctae_stats.hip dctae_api.hip || exit 1
+      -o ../../_ablate/libdctae_$m.so dctae_kernels.hip dctae_fft.hip dctae_fft2.hip dctae_idct.hip dctae_vq.hip dctae_stats.hip dctae_api.hip || exit 1
   done
   cd ../..
 fi
