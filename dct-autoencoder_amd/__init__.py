@@ -12,6 +12,7 @@ from .lfq import LFQ  # noqa: F401
 from .patchnorm import PatchNorm  # noqa: F401
 from .vector_quantize import VectorQuantize  # noqa: F401
 from . import packing  # noqa: F401
+from . import shards  # noqa: F401
 
 __all__ = ["DCTAutoencoderFeatureExtractor", "DCTPatches", "PatchNorm", "LFQ", "VectorQuantize", "to_dict", "from_dict",
            "GroupPatchesState", "build_attn_mask", "load_library", "DCTAEError", "DCTAEUnavailable"]
