@@ -61,8 +61,9 @@ struct dctae_ctx {
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16),
                                       // 3 row-major with each tile column padded to 16 floats (64-B segments)
-  int cols_kernel = 6;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses),
-                                      // 5 (complex-pair LDS, N = 512), 6 (5 with several images per block)
+  int cols_kernel = 7;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses),
+                                      // 5 (complex-pair LDS, N = 512), 6 (5 with several images per block),
+                                      // 7 (6 with pass 1 from registers, one LDS exchange)
   int cols_ipb = 2, cols_pf = 1;      // cols_kernel 6: images per block, prefetch of the next slice
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
@@ -613,7 +614,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
   else if (k == "t_layout" && value >= 0 && value <= 3) ctx->t_layout = (int)value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
-  else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6)) ctx->cols_kernel = (int)value;
+  else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6 || value == 7)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
   else if (k == "dual_stream") ctx->dual_stream = value != 0;

@@ -718,6 +718,62 @@ __device__ __forceinline__ void cols5_stage(float2* zc, const f2v (&va)[7], cons
   }
 }
 
+// token epilogue of one (channel, tile column) item: X2 = the 448 x 14 kept
+// coefficients (float index k * 14 + col) in LDS; tile (h, strip) per 16-lane
+// group g16 (+16 r), tile row jl; codes from the thresholds held in registers
+template <bool THR>
+__device__ __forceinline__ void cols5_epilogue(const ImgDesc& d, int c, int strip, const f2v* X2, const float* sbias,
+                                               const float2 (&thr_r)[2][7], const EncParams& ep,
+                                               const TokenSinks& sk) {
+  constexpr int KS = 14, EPR = 2;
+  const int tid = opaque_tid();
+  const int g16 = tid >> 4, jl = tid & 15;
+  if (THR) {
+#pragma unroll
+    for (int r = 0; r < EPR; ++r) {
+      const int h = g16 + 16 * r;
+      if (h < d.qh) {
+        const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
+        uint32_t am = 0, code = 0;
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) {
+          const f2v v2 = row[p];
+          am = max(am, max(__float_as_uint(v2.x) & 0x7fffffffu, __float_as_uint(v2.y) & 0x7fffffffu));
+          code |= (v2.x >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
+          code |= (v2.y >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
+        }
+        am = jl < KS ? am : 0u;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
+        const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
+        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
+        if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
+        if (sk.raw && jl < KS) {
+#pragma unroll
+          for (int p = 0; p < KS / 2; ++p) {
+            const f2v v2 = row[p];
+            sk.raw[tok * KS * KS + jl * KS + 2 * p] = v2.x;
+            sk.raw[tok * KS * KS + jl * KS + 2 * p + 1] = v2.y;
+          }
+        }
+      }
+    }
+  } else {
+    for (int h = g16; h < d.qh; h += 16) {
+      float vals[KS];
+      const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
+#pragma unroll
+      for (int p = 0; p < KS / 2; ++p) {
+        const f2v v2 = row[p];
+        vals[2 * p] = v2.x;
+        vals[2 * p + 1] = v2.y;
+      }
+      const int f = (h * d.qw + strip) * ep.C + c;
+      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+    }
+  }
+}
+
 // z staged (and a barrier since): column FFT-DCT, post-processing, token epilogue
 template <bool THR>
 __device__ __forceinline__ void cols5_compute(const ImgDesc& d, int c, int strip, float2* zc, const float4* post4,
@@ -808,52 +864,8 @@ __device__ __forceinline__ void cols5_compute(const ImgDesc& d, int c, int strip
   }
   __syncthreads();
   // ---- token epilogue: tile (h, strip) of channel c, one 16-lane group per tile, row jl
-  const f2v* X2 = reinterpret_cast<const f2v*>(zc);
   if (DCTAE_ABLATE & 16) return;
-  if (THR) {
-#pragma unroll
-    for (int r = 0; r < EPR; ++r) {
-      const int h = g16 + 16 * r;
-      if (h < d.qh) {
-        const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
-        uint32_t am = 0, code = 0;
-#pragma unroll
-        for (int p = 0; p < KS / 2; ++p) {
-          const f2v v2 = row[p];
-          am = max(am, max(__float_as_uint(v2.x) & 0x7fffffffu, __float_as_uint(v2.y) & 0x7fffffffu));
-          code |= (v2.x >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
-          code |= (v2.y >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
-        }
-        am = jl < KS ? am : 0u;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
-        const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
-        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
-        if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
-        if (sk.raw && jl < KS) {
-#pragma unroll
-          for (int p = 0; p < KS / 2; ++p) {
-            const f2v v2 = row[p];
-            sk.raw[tok * KS * KS + jl * KS + 2 * p] = v2.x;
-            sk.raw[tok * KS * KS + jl * KS + 2 * p + 1] = v2.y;
-          }
-        }
-      }
-    }
-  } else {
-    for (int h = g16; h < d.qh; h += 16) {
-      float vals[KS];
-      const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
-#pragma unroll
-      for (int p = 0; p < KS / 2; ++p) {
-        const f2v v2 = row[p];
-        vals[2 * p] = v2.x;
-        vals[2 * p + 1] = v2.y;
-      }
-      const int f = (h * d.qw + strip) * ep.C + c;
-      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
-    }
-  }
+  cols5_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(zc), sbias, thr_r, ep, sk);
 }
 
 
@@ -938,6 +950,210 @@ __global__ __launch_bounds__(256) void k_fft_cols6(const ImgDesc* __restrict__ i
       }
       cols5_compute<THR>(dk, c, strip, L.z, post4, tw_s, sbias, thr_r, ep, sk);
       __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// cols7 (N = 512): the column FFT with ONE LDS exchange.  Lane (w, g, col) =
+// (wave, 16-lane row, column of the strip; col 14, 15 idle).
+//  * pass 1: butterfly j1 = 4w + g reads z[j1 + 16 r] straight from T in
+//    global memory (Makhoul pairs (x[4m], x[4m+2]) / (x[2N-1-4m], x[2N-3-4m]),
+//    14 consecutive floats of a T row per 16-lane row), DFT16 in registers,
+//    writes z[16 j1 + r] to LDS;
+//  * pass 2: butterfly j2 (wave w owns the pairs j2 / 16 - j2) reads
+//    z[j2 + 16 r], twiddles, DFT16: Z[j2 + 16 r] in registers;
+//  * Makhoul post needs Z[M - k] = the partner row's Z[(16 - j2) + 16 (15 - i)]:
+//    a v_permlane16_swap between rows g and g ^ 1 (j2 = 0 and 8 pair with
+//    themselves), no LDS;
+//  * X (448 x 14 kept coefficients) -> LDS -> the cols5 token epilogue.
+// LDS slot of complex element m, column col: 16 m' + col, m' = m ^ bit3(m)
+// (a permutation): the two 16-lane rows of a ds_read_b64 half-wave
+// (j2 = a, 16 - a: bit 3 differs) fall on opposite 32-bank halves.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ constexpr int z7addr(int m) { return 16 * (m ^ ((m >> 3) & 1)); }
+
+__device__ __forceinline__ int cols7_j2(int w, int g) {
+  // wave 0: 0, 8, 1, 15;  wave w > 0: 2w, 16 - 2w, 2w + 1, 15 - 2w
+  const int a = (g & 2) ? 2 * w + 1 : 2 * w;
+  const int base = (w == 0 && g < 2) ? (g ? 8 : 0) : ((g & 1) ? (g & 2 ? 15 - 2 * w : 16 - 2 * w) : a);
+  return base;
+}
+
+__device__ __forceinline__ float partner_row(float x, bool even_row) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(even_row ? r[1] : r[0]);
+}
+
+// X aliases z (one more barrier, 37 KB instead of 62 KB: 4 workgroups per CU)
+union Cols7Lds {
+  float2 z[256 * 16];
+  float X[448 * 14];
+};
+
+template <bool NTL>
+__device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
+                                           float (&va)[16], float (&vb)[16]) {
+  constexpr int N = 512;
+  const int tid = opaque_tid();
+  const int j1 = tid >> 4, col = min(tid & 15, 13);
+  const int rs = d.Kw;
+  // buffer descriptor on the (channel, tile column) slice: 32-bit lane offsets, uniform row steps
+  const float* cb = T + (int64_t)c * N * rs + strip * 14;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cb), 0, N * rs * 4, 0x00020000);
+  // m = j1 + 16 r: rows 4m (+2) for r < 8, 2N - 1 - 4m (-2) above; 64-row steps
+  const int lo = (4 * j1 * rs + col) * 4;
+  const int hi = ((2 * N - 1 - 4 * j1 - 64 * 15) * rs + col) * 4;   // r = 15: lowest row of the upper half
+  const int step = 64 * rs * 4, two = 2 * rs * 4;
+  constexpr int aux = NTL ? 2 : 0;   // slc: streamed once
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo, r * step, aux));
+    vb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo + two, r * step, aux));
+  }
+#pragma unroll
+  for (int r = 8; r < 16; ++r) {
+    va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, hi, (15 - r) * step, aux));
+    vb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, hi - two, (15 - r) * step, aux));
+  }
+}
+
+// Makhoul post of cols7 for one lane: v = Z[j2 + 16 i]; writes X[k], X[N - k]
+// (Kh = 448: X[N - k] kept for k > 64) and X[M] (j2 = 0).  W0: wave 0, whose
+// rows 0 and 1 (j2 = 0, 8) pair with themselves.
+template <bool W0>
+__device__ __forceinline__ void cols7_post(const cf (&v)[16], int j2, int g, int col, const float4* post4,
+                                           float* Xs) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14;
+  const bool on_col = col < KS;
+  const bool self = W0 && g < 2;
+  float* xa = Xs + j2 * KS + col;                        // X[j2 + 16 i] at + 224 i
+  float* xb = Xs + (N - j2 - 16 * 15) * KS + col;        // X[N - j2 - 16 i] at + 224 (15 - i)
+  const float4* ps = post4 + j2;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    cf P;
+    P.x = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v[15 - i].x), 0x401f));   // lane ^ 16
+    P.y = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v[15 - i].y), 0x401f));
+    if (W0) P = self ? ((j2 == 0) ? v[(16 - i) & 15] : v[15 - i]) : P;
+    const cf A = v[i];
+    const float4 ab = ps[16 * i];
+    const cf al = (cf){ab.x, ab.y}, be = (cf){ab.z, ab.w};
+    const cf s1 = add_conj(A, P), d1 = sub_conj(A, P);
+    const cf W = fma_iw(d1, be, fma_x(d1, be, fma_iw(s1, al, mul_x(s1, al))));
+    if (on_col) {
+      xa[224 * i] = W.x;
+      if (i > 4 || (i == 4 && j2 > 0)) xb[224 * (15 - i)] = -W.y;
+    }
+  }
+  if (W0 && j2 == 0 && on_col) {   // k = M (< Kh): A = B = Z[0]
+    const cf A = v[0];
+    const float4 ab = post4[M];
+    const cf s1 = add_conj(A, A), d1 = sub_conj(A, A);
+    const cf W = fma_iw(d1, (cf){ab.z, ab.w}, fma_x(d1, (cf){ab.z, ab.w}, cmul_pk(s1, (cf){ab.x, ab.y})));
+    Xs[M * KS + col] = W.x;
+  }
+}
+
+template <bool THR>
+__device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip, Cols7Lds& L, const float (&va)[16],
+                                              const float (&vb)[16], const float4* post4, const float2* tw_s,
+                                              const float* sbias, const float2 (&thr_r)[2][7], const EncParams& ep,
+                                              const TokenSinks& sk) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14, M16 = 16;
+  const int tid = opaque_tid();
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), g = (tid >> 4) & 3, col = tid & 15;
+  const bool on_col = col < KS;
+  cf* z = reinterpret_cast<cf*>(L.z);
+  (void)d;
+  // ---- pass 1 (Ns = 1): j1 = tid >> 4
+  {
+    const int j1 = tid >> 4;
+    cf v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = (cf){va[r], vb[r]};
+    DFTV<16>::run(v);
+    if (on_col) {
+      cf* zw = z + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) zw[z7addr(16 * j1 + r)] = v[r];
+    }
+  }
+  __syncthreads();
+  // ---- pass 2 (Ns = 16): z[j2 + 16 r] * W_M^{r j2} -> DFT16 -> Z[j2 + 16 r]
+  const int j2 = cols7_j2(w, g);
+  cf v[16];
+  {
+    const cf* zr = z + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = zr[z7addr(j2 + 16 * r)];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      const float2 tw = tw_s[r * j2];
+      v[r] = cmul_pk(v[r], (cf){tw.x, tw.y});
+    }
+    DFTV<16>::run(v);
+  }
+  // ---- Makhoul post: k = j2 + 16 i; A = Z[k], B = conj Z[M - k]
+  //      j2 >= 1: Z[M - k] = partner row's v[15 - i] (lane ^ 16, ds_swizzle);
+  //      j2 = 0: own v[(16 - i) & 15];  j2 = 8: own v[15 - i]  (wave 0, rows 0 and 1)
+  //      kept rows: Kh = 448 (H = 512): X[k] always, X[N - k] for k > 64
+  if (w == 0) cols7_post<true>(v, j2, g, col, post4, L.X);
+  else cols7_post<false>(v, j2, g, col, post4, L.X);
+  __syncthreads();
+  if (DCTAE_ABLATE & 16) return;
+  cols5_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sbias, thr_r, ep, sk);
+}
+
+template <bool THR, int IPB, bool PF>
+__global__ __launch_bounds__(256) void k_fft_cols7(const ImgDesc* __restrict__ imgs, const int* __restrict__ list,
+                                                   int n_list, int n_items, int qw,
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+  constexpr int M = 256;
+  __shared__ Cols7Lds L;
+  __shared__ float4 post4[M + 1];
+  __shared__ float2 tw_s[M];
+  __shared__ float sbias[32];
+  const int per_x = (n_items + 7) / 8;
+  const int b = blockIdx.x, slot = b >> 3;
+  const int t = (b & 7) * per_x + slot % per_x, g = slot / per_x;
+  const int k0 = g * IPB;
+  if (t >= n_items || k0 >= n_list) return;
+  const int c = t / qw, strip = t - c * qw;
+  const float4* p4 = reinterpret_cast<const float4*>(post);
+  for (int i = threadIdx.x; i < M + 1; i += 256) post4[i] = p4[i];
+  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  float2 thr_r[2][7];
+  cols5_thresholds<THR>(imgs[list[k0]], c, strip, ep, thr_r, sbias);
+  float va[16], vb[16];
+  {
+    const ImgDesc d0 = imgs[list[k0]];
+    cols7_load<false>(d0, c, strip, ws + d0.ws_t, va, vb);
+  }
+  __syncthreads();   // tables
+#pragma unroll
+  for (int u = 0; u < IPB; ++u) {
+    const int k = k0 + u;
+    if (k < n_list) {
+      const ImgDesc dk = imgs[list[k]];
+      if (u > 0 && !PF) cols7_load<false>(dk, c, strip, ws + dk.ws_t, va, vb);
+      float na[16], nb[16];
+      if (PF && u + 1 < IPB && k + 1 < n_list) {
+        const ImgDesc dn = imgs[list[k + 1]];
+        cols7_load<false>(dn, c, strip, ws + dn.ws_t, na, nb);   // in flight during the transform
+      }
+      cols7_compute<THR>(dk, c, strip, L, va, vb, post4, tw_s, sbias, thr_r, ep, sk);
+      __syncthreads();
+      if (PF && u + 1 < IPB) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          va[r] = na[r];
+          vb[r] = nb[r];
+        }
+      }
     }
   }
 }
@@ -1179,6 +1395,24 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
                           hipStream_t s, int kernel, int layout, const int* cols6_list, int cols6_n, int cols6_qw,
                           int cols6_ipb, int cols6_pf) {
   if (n_blocks <= 0) return;
+  if (kernel == 7 && layout == 0 && spec == 1 && cols6_list && cols6_n > 0) {
+    const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
+    const int n_items = 3 * cols6_qw;
+    const int per_x = (n_items + 7) / 8;
+    const int ipb = cols6_ipb;
+    const int grid = 8 * per_x * ((cols6_n + ipb - 1) / ipb);
+#define DCTAE_COLS7(T, I, P)                                                                                  \
+  hipLaunchKernelGGL((k_fft_cols7<T, I, P>), dim3(grid), dim3(256), 0, s, imgs, cols6_list, cols6_n, n_items, \
+                     cols6_qw, ws, tw, post, ep, sk)
+    if (thr && ipb == 2 && cols6_pf) DCTAE_COLS7(true, 2, true);
+    else if (thr && ipb == 2) DCTAE_COLS7(true, 2, false);
+    else if (thr && ipb == 4 && cols6_pf) DCTAE_COLS7(true, 4, true);
+    else if (thr && ipb == 4) DCTAE_COLS7(true, 4, false);
+    else if (ipb == 2) DCTAE_COLS7(false, 2, false);
+    else DCTAE_COLS7(false, 4, false);
+#undef DCTAE_COLS7
+    return;
+  }
   if (kernel == 6 && layout == 0 && spec == 1 && cols6_list && cols6_n > 0) {
     const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
     const int n_items = 3 * cols6_qw;
@@ -1197,7 +1431,7 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
 #undef DCTAE_COLS6
     return;
   }
-  if ((kernel == 5 || kernel == 6) && layout == 0 && spec == 1) {
+  if ((kernel == 5 || kernel == 6 || kernel == 7) && layout == 0 && spec == 1) {
     const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
     if (thr)
       hipLaunchKernelGGL((k_fft_cols5<true>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk);

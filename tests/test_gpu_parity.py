@@ -362,7 +362,7 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-DEFAULTS = {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2,
+DEFAULTS = {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2,
             "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
@@ -373,6 +373,9 @@ SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS a
     "cols_pairs": {"cols_kernel": 5},
     "cols_multi4_pf": {"cols_kernel": 6, "cols_ipb": 4, "cols_pf": 1},
     "cols_multi2_nopf": {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 0},
+    "cols_multi2_pf": {"cols_kernel": 6},
+    "cols_one_exchange4": {"cols_kernel": 7, "cols_ipb": 4, "cols_pf": 1},
+    "cols_one_exchange_nopf": {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 0},
     "sort_bitonic": {"sort_kernel": 1},
     "chunks_dual_stream": {"chunk_bytes": 4 << 20, "dual_stream": 1},
     "chunks_one_stream": {"chunk_bytes": 4 << 20, "dual_stream": 0},
