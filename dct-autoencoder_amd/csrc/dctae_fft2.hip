@@ -1006,6 +1006,11 @@ __device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, c
   const int hi = ((2 * N - 1 - 4 * j1 - 64 * 15) * rs + col) * 4;   // r = 15: lowest row of the upper half
   const int step = 64 * rs * 4, two = 2 * rs * 4;
   constexpr int aux = NTL ? 2 : 0;   // slc: streamed once
+  if (DCTAE_ABLATE & 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) va[r] = vb[r] = (float)(lo + r);
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo, r * step, aux));
@@ -1100,7 +1105,10 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
   //      j2 >= 1: Z[M - k] = partner row's v[15 - i] (lane ^ 16, ds_swizzle);
   //      j2 = 0: own v[(16 - i) & 15];  j2 = 8: own v[15 - i]  (wave 0, rows 0 and 1)
   //      kept rows: Kh = 448 (H = 512): X[k] always, X[N - k] for k > 64
-  if (w == 0) cols7_post<true>(v, j2, g, col, post4, L.X);
+  if (DCTAE_ABLATE & 8) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) L.X[(j2 * 14 + col + 224 * i) % 6272] = v[i].x + v[i].y;
+  } else if (w == 0) cols7_post<true>(v, j2, g, col, post4, L.X);
   else cols7_post<false>(v, j2, g, col, post4, L.X);
   __syncthreads();
   if (DCTAE_ABLATE & 16) return;
@@ -1238,6 +1246,9 @@ __device__ __forceinline__ void wait_all(const int* p, int target, int limit, in
     if (!wait_count(p, target, limit)) atomicOr(err, 8);
   }
   __syncthreads();
+  // acquire: invalidate this CU's L1 (a ring slot read before may hold stale
+  // lines of its previous image) and keep the item's loads below the wait
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
 // claim the next item of a counter (block-uniform result)
@@ -1256,9 +1267,11 @@ __global__ __launch_bounds__(256, 4) void k_enc_fused(FusedParams p_, const ImgD
   union Lds {
     RowsLds<N> r;
     ColsLds<N> c;
+    Cols7Lds c7;   // N = 512 column items (cols7)
   };
   __shared__ Lds L;
-  __shared__ float2 post_s[2 * (M + 1)];
+  __shared__ float4 post4[M + 1];   // (alpha_k, beta_k) pairs
+  float2* const post_s = reinterpret_cast<float2*>(post4);
   __shared__ float2 tw_s[M];
   __shared__ float sbias[32];
   __shared__ int s_int;
@@ -1326,7 +1339,15 @@ __global__ __launch_bounds__(256, 4) void k_enc_fused(FusedParams p_, const ImgD
       const int c = sub / qw, strip = sub - c * qw;
       const EncParams& ep = p_.ep;
       const TokenSinks& sk = p_.sk;
-      cols4_item<N, R2, 14, THR, true, DCTAE_THR_AT>(d, c, strip, T, L.c.z, post_s, tw_s, sbias, ep, sk);
+      if constexpr (N == 512) {
+        float2 thr_r[2][7];
+        cols5_thresholds<THR>(d, c, strip, ep, thr_r, sbias);
+        float va[16], vb[16];
+        cols7_load<true>(d, c, strip, T, va, vb);
+        cols7_compute<THR>(d, c, strip, L.c7, va, vb, post4, tw_s, sbias, thr_r, ep, sk);
+      } else {
+        cols4_item<N, R2, 14, THR, true, DCTAE_THR_AT>(d, c, strip, T, L.c.z, post_s, tw_s, sbias, ep, sk);
+      }
       signal_done(cols_done + img);
       if (a.prof) {
         prof_w += t1 - t0;
