@@ -363,7 +363,7 @@ def test_thresholds_are_exact(pn):
 
 
 DEFAULTS = {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2,
-            "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1}
+            "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1, "pipe": 0}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "fused": {"fused": 1},
@@ -379,6 +379,7 @@ SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS a
     "sort_bitonic": {"sort_kernel": 1},
     "chunks_dual_stream": {"chunk_bytes": 4 << 20, "dual_stream": 1},
     "chunks_one_stream": {"chunk_bytes": 4 << 20, "dual_stream": 0},
+    "chunks_one_grid_pipeline": {"chunk_bytes": 4 << 20, "dual_stream": 1, "pipe": 1},
     "t_strips": {"t_layout": 1},
     "t_strips16": {"t_layout": 2},
     "t_rowmajor_pad16": {"t_layout": 3},
@@ -498,3 +499,27 @@ def test_fft_decode_patches_roundtrip_512(fe):
     (ref,) = ref_cpu.postprocess(ob, CFG)
     ok, dmax = _rgb_close(img.cpu(), ref, atol=1e-5, rtol=1e-5)
     assert ok, dmax
+
+
+@pytest.mark.parametrize("group", [2])
+def test_group_pipeline_matches_default_bitwise(fe, pn, lfq, group):
+    """pipe = 2 (k_enc_pipe2: one launch; the column blocks of image group g
+    interleaved with the row blocks of group g + 1 and waiting on group g's
+    row counter) runs the same row / cols7 arithmetic: outputs bit-identical."""
+    ops = _ops()
+    x = torch.from_numpy(np.stack(rng.synth_images(71, [(512, 512)] * 32))).to(DEV)
+    outs = {}
+    try:
+        for pipe in (2, 0):
+            ops.set_option("pipe", pipe)
+            ops.set_option("pipe_group", group)
+            outs[pipe] = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
+        ops.check_device_errors(x.device)
+    finally:
+        ops.set_option("pipe", 0)
+        ops.set_option("pipe_group", 16)
+    for (dp_a, c_a), (dp_b, c_b) in zip(outs[2], outs[0]):
+        assert torch.equal(c_a, c_b)
+        assert torch.equal(dp_a.patch_positions, dp_b.patch_positions)
+        assert torch.equal(dp_a.key_pad_mask, dp_b.key_pad_mask)
+        assert torch.equal(dp_a.patches.view(torch.int32), dp_b.patches.view(torch.int32))
