@@ -76,6 +76,50 @@ def cpu_baseline(size, seconds, pn_tables, threads):
                       f"(FFT DCT, sort) + iter_batches (attn_mask built) + PatchNorm + LFQ, {el:.1f} s"}
 
 
+def stats_fit_leg(pkg, fe, dev, rank, world, dist, steps, n_img=8, size=512):
+    """Config 5: one data-parallel PatchNorm fit step per
+    iteration — each rank's batch statistics of its own shard, exchanged over
+    RCCL (two all_gathers of the (3, 32, 32, 196) tables, distributed.py) and
+    the running-update chain replayed locally.  At N = 1 a one-rank NCCL group
+    runs the same code.  The shard's encode is outside the timed region."""
+    from importlib import import_module
+    import torch.distributed as tdist
+    ops = import_module("dct_autoencoder_amd._ops")
+    dd = import_module("dct_autoencoder_amd.distributed")
+    own = False
+    if not tdist.is_initialized():
+        import socket
+        so = socket.socket()
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+        so.close()
+        tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+        own = True
+    try:
+        xs = ops.synth_images(n_img, size, size, seed=99, first_index=rank * n_img, device=dev)
+        ((dp, _),) = fe.encode_batch(xs, None, None, return_raw=True)
+        pn_t = pkg.PatchNorm(32, 32, 14, 3).to(dev).train()
+        dd.train_step(pn_t, dp)                          # warm-up (plans, RCCL channels)
+        torch.cuda.synchronize(dev)
+        tdist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dd.train_step(pn_t, dp)
+        torch.cuda.synchronize(dev)
+        tdist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        tdist.all_reduce(el, op=tdist.ReduceOp.MAX)
+        table_bytes = 3 * 32 * 32 * (14 * 14 + 1) * 4
+        return {"workload": f"config 5 stats fit: PatchNorm running statistics of {n_img} x {size}x{size} images "
+                            f"per rank, 2 all_gathers over RCCL + local replay of the update chain",
+                "ranks": world, "ms_per_step": round(float(el.item()) / steps * 1e3, 4),
+                "gathered_bytes_per_rank_per_step": 2 * table_bytes * world,
+                "tokens_per_rank": int((~dp.key_pad_mask).sum().item())}
+    finally:
+        if own:
+            tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,6 +131,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the config-3 decode timing")
+    ap.add_argument("--no-stats", action="store_true", help="skip the config-5 PatchNorm fit (RCCL) timing")
     ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
 
@@ -246,6 +291,13 @@ def main():
         except Exception as e:  # noqa: BLE001 — the encode line must still print
             decode = {"error": f"{type(e).__name__}: {e}"}
 
+    stats = None
+    if not args.no_stats:
+        try:
+            stats = stats_fit_leg(pkg, fe, dev, rank, world, dist, args.steps)
+        except Exception as e:  # noqa: BLE001 — the encode line must still print
+            stats = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import ref_cpu
@@ -278,6 +330,7 @@ def main():
             "cpu_baseline": cpu,
             "kernels": kernels,
             "decode": decode,
+            "stats_fit": stats,
             "options": args.opt,
         }
         print(json.dumps(line))

@@ -21,7 +21,8 @@ prof = os.path.join(ROOT, "profiles")
 os.makedirs(prof, exist_ok=True)
 # library timer names <- kernel symbols
 NAMES = {"k_fft_rows2": "fft_rows", "k_fft_rows": "fft_rows", "k_fft_cols2": "fft_cols", "k_fft_cols": "fft_cols",
-         "k_fft_cols4": "fft_cols", "k_fft_cols5": "fft_cols", "k_fft_cols6": "fft_cols", "k_sort_pack2": "sort_pack",
+         "k_fft_cols4": "fft_cols", "k_fft_cols5": "fft_cols", "k_fft_cols6": "fft_cols", "k_fft_cols7": "fft_cols",
+         "k_enc_pipe": "enc_pipe", "k_enc_pipe2": "enc_pipe", "k_sort_pack2": "sort_pack",
          "k_enc_fused": "enc_fused", "k_dec_map": "dec_map", "k_idct_cols512": "idct_cols", "k_idct_rows2": "idct_rows",
          "k_sort_pack": "sort_pack", "k_pad_fill": "pad_fill", "k_gemm_f32": "gemm", "k_rgb_to_ipt": "rgb_to_ipt",
          "k_tile_epilogue": "tile_epilogue", "k_synth": "synth", "k_norm_thresholds": "norm_thresholds"}
