@@ -112,6 +112,19 @@ _SIGS = {
     "dctae_norm_merge": ([_P, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int32, _P], C.c_int),
     "dctae_norm_train_step": ([_P, C.POINTER(Norm), _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P,
                                C.c_int64, _P, _P], C.c_int),
+    # DCTAutoencoder transformer operators
+    "dctae_model_linear": ([_P, C.c_int64, C.c_int32, C.c_int32, _P, C.c_int64, _P, C.c_int32, C.c_int64, _P,
+                            C.c_int32, _P, C.c_int64, _P], C.c_int),
+    "dctae_model_attention": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, C.c_int64, _P],
+                              C.c_int),
+    "dctae_model_layernorm": ([_P, C.c_int64, C.c_int32, _P, C.c_int64, _P, _P, C.c_float, _P, C.c_int64, _P],
+                              C.c_int),
+    "dctae_model_embed_norm": ([_P, C.c_int64, C.c_int32, _P, C.c_int64, _P, _P, C.c_float, _P, _P, _P, _P, _P, _P,
+                                C.c_int64, _P], C.c_int),
+    "dctae_model_pos_add": ([_P, C.c_int64, C.c_int32, _P, C.c_int64, _P, _P, _P, _P, _P, _P], C.c_int),
+    "dctae_model_to_bf16": ([_P, C.c_int64, C.c_int32, _P, C.c_int64, C.c_int32, _P, _P], C.c_int),
+    "dctae_model_lfq": ([_P, C.c_int64, C.c_int32, C.c_int32, C.c_float, _P, C.c_int64, _P, _P, _P, C.c_int64, _P],
+                        C.c_int),
 }
 
 _lib = None

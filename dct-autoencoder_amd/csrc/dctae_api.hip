@@ -10,6 +10,7 @@
 #include "../../include/dctae.h"
 #include "dctae_internal.h"
 #include "dctae_launch.h"
+#include "dctae_model.h"
 
 using namespace dctae;
 
@@ -1849,6 +1850,132 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// DCTAutoencoder transformer operators (dctae_model.hip)
+// ---------------------------------------------------------------------------
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+int dctae_model_linear(dctae_ctx* ctx, int64_t M, int32_t N, int32_t K, const uint16_t* x, int64_t ldx,
+                       const uint16_t* w, int32_t w_rows, int64_t ldw, const float* bias, int32_t epilogue, void* out,
+                       int64_t ldo, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (M < 0 || N <= 0 || K <= 0 || K % 64 || w_rows < N || ldx < K || ldw < K || ldx % 8 || ldw % 8 || ldo < N)
+    return fail(ctx, DCTAE_EINVAL, "model_linear: bad shape (K % 64, ld % 8, w_rows >= N, ld >= K / N)");
+  if (epilogue < DCTAE_LIN_F32 || epilogue > DCTAE_LIN_F32_RESIDUAL) return fail(ctx, DCTAE_EINVAL, "model_linear: epilogue");
+  if (M == 0) return 0;
+  if (!x || !w || !out || !al16(x) || !al16(w)) return fail(ctx, DCTAE_EINVAL, "model_linear: null or unaligned tensor");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  LinearArgs a{x, w, bias, out, M, ldx, ldw, ldo, N, w_rows, K};
+  Timer t(ctx, s, "model_linear");
+  launch_linear(a, epilogue, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_model_attention(dctae_ctx* ctx, int32_t R, int32_t S, int32_t heads, int32_t head_dim, const uint16_t* qkv,
+                          const int64_t* ids, const uint8_t* key_pad, uint16_t* out, int64_t ldo, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (head_dim != 64) return fail(ctx, DCTAE_EUNSUP, "model_attention: head_dim must be 64");
+  if (R < 0 || S <= 0 || heads <= 0 || ldo < 64ll * heads || ldo % 8)
+    return fail(ctx, DCTAE_EINVAL, "model_attention: bad shape");
+  if (R == 0) return 0;
+  if (!qkv || !ids || !key_pad || !out || !al16(qkv) || !al16(out))
+    return fail(ctx, DCTAE_EINVAL, "model_attention: null or unaligned tensor");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  AttnArgs a{qkv, ids, key_pad, out, R, S, heads, (int32_t)ldo, 0.125f};
+  Timer t(ctx, s, "model_attention");
+  launch_attention(a, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+static int ln_check(dctae_ctx* ctx, int64_t M, int32_t D, const float* x, const float* g, const float* b) {
+  if (M < 0 || D <= 0 || D > 4096) return fail(ctx, DCTAE_EINVAL, "model layernorm: bad shape (D <= 4096)");
+  if (M > 0 && (!x || !g || !b)) return fail(ctx, DCTAE_EINVAL, "model layernorm: null tensor");
+  return 0;
+}
+
+int dctae_model_layernorm(dctae_ctx* ctx, int64_t M, int32_t D, const float* x, int64_t ldx, const float* g,
+                          const float* b, float eps, uint16_t* out, int64_t ldo, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  int rc = ln_check(ctx, M, D, x, g, b);
+  if (rc || M == 0) return rc;
+  if (!out) return fail(ctx, DCTAE_EINVAL, "model_layernorm: null output");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  LnArgs a{};
+  a.x = x; a.gamma = g; a.beta = b; a.out_bf16 = out; a.M = M; a.ldx = ldx; a.ldo = ldo; a.D = D; a.eps = eps;
+  Timer t(ctx, s, "model_layernorm");
+  launch_layernorm(a, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_model_embed_norm(dctae_ctx* ctx, int64_t M, int32_t D, const float* x, int64_t ldx, const float* g,
+                           const float* b, float eps, const float* ph, const float* pw, const float* pc,
+                           const int64_t* ch, const int64_t* pos, float* out, int64_t ldo, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  int rc = ln_check(ctx, M, D, x, g, b);
+  if (rc || M == 0) return rc;
+  if (!out || !ph || !pw || !pc || !ch || !pos) return fail(ctx, DCTAE_EINVAL, "model_embed_norm: null tensor");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  LnArgs a{};
+  a.x = x; a.gamma = g; a.beta = b; a.out_f32 = out; a.pos_h = ph; a.pos_w = pw; a.pos_c = pc; a.ch = ch;
+  a.pos = pos; a.M = M; a.ldx = ldx; a.ldo = ldo; a.D = D; a.eps = eps;
+  Timer t(ctx, s, "model_embed_norm");
+  launch_layernorm(a, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_model_pos_add(dctae_ctx* ctx, int64_t M, int32_t D, float* x, int64_t ldx, const float* ph, const float* pw,
+                        const float* pc, const int64_t* ch, const int64_t* pos, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (M < 0 || D <= 0) return fail(ctx, DCTAE_EINVAL, "model_pos_add: bad shape");
+  if (M == 0) return 0;
+  if (!x || !ph || !pw || !pc || !ch || !pos) return fail(ctx, DCTAE_EINVAL, "model_pos_add: null tensor");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  PosArgs a{x, ph, pw, pc, ch, pos, M, ldx, D};
+  Timer t(ctx, s, "model_pos_add");
+  launch_pos_add(a, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_model_to_bf16(dctae_ctx* ctx, int64_t M, int32_t K, const float* x, int64_t ldx, int32_t Kp, uint16_t* out,
+                        void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (M < 0 || K < 0 || Kp < K || ldx < K) return fail(ctx, DCTAE_EINVAL, "model_to_bf16: bad shape");
+  if (M == 0 || Kp == 0) return 0;
+  if (!x || !out) return fail(ctx, DCTAE_EINVAL, "model_to_bf16: null tensor");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "model_to_bf16");
+  launch_to_bf16(x, ldx, M, K, Kp, out, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_model_lfq(dctae_ctx* ctx, int64_t M, int32_t ncb, int32_t cbd, float scale, const float* x, int64_t ldx,
+                    int64_t* codes, uint16_t* q_bf16, float* q_f32, int64_t ldq, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (M < 0 || ncb <= 0 || cbd <= 0 || cbd > 62 || ldx < (int64_t)ncb * cbd || ((q_bf16 || q_f32) && ldq < (int64_t)ncb * cbd))
+    return fail(ctx, DCTAE_EINVAL, "model_lfq: bad shape");
+  if (M == 0) return 0;
+  if (!x || !codes) return fail(ctx, DCTAE_EINVAL, "model_lfq: null tensor");
+  hipSetDevice(ctx->device);
+  hipStream_t s = (hipStream_t)stream;
+  LfqArgs a{x, codes, q_bf16, q_f32, M, ldx, ldq, ncb, cbd, scale};
+  Timer t(ctx, s, "model_lfq");
+  launch_lfq_codes(a, s);
+  HIPCHK(ctx, hipGetLastError());
   return 0;
 }
 

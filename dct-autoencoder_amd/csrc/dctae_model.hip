@@ -1,0 +1,430 @@
+// DCTAutoencoder transformer forward: the kernels under the
+// CLIPEncoder encoder / decoder around the LFQ bottleneck
+// (modeling_dct_autoencoder.py; transformers==4.35.2 CLIPEncoderLayer).
+//
+//   k_linear<EPI>   y = x W^T (+ bias) on v_mfma_f32_32x32x16_bf16: 128 x 128
+//                   tiles, BK = 64, 4 waves of 64 x 64, LDS rows padded to 72
+//                   bf16 (conflict-free ds_read_b128 fragments), next K tile
+//                   prefetched into registers; epilogues: f32 store, bf16
+//                   store, bf16 quick_gelu, f32 residual add (in place)
+//   k_attention     flash attention, d_head = 64: S^T = K Q^T so the softmax
+//                   probabilities come out of the MFMA already in B-operand
+//                   layout for O^T = V^T P^T (keys permuted consistently in
+//                   V^T); online softmax in fp32; the reference's attention
+//                   "mask" is ADDED (+1.0 where id_i == id_j and key j is a
+//                   pad, FE:580-584 -> modeling:131-133), computed from the
+//                   row's image ids and key_pad_mask (no S x S tensor)
+//   k_layernorm     one wave per token row, fp32 statistics, bf16 out
+//   k_ln_pos        embedding LayerNorm (eps 1e-4) + encoder position terms
+//   k_pos_add       decoder position terms (in place)
+//   k_to_bf16       fp32 -> bf16 with zero K padding
+//   k_lfq_codes     LFQ.forward eval (lfq.py:164-212): sign, MSB-first codes,
+//                   +-1 features (bf16 for project_out, or f32)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dctae_model.h"
+
+namespace dctae {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint16_t f2bf(float f) {   // round to nearest even
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// ---------------------------------------------------------------------------
+// linear
+// ---------------------------------------------------------------------------
+constexpr int LBM = 128, LBN = 128, LBK = 64, LSTR = 72;   // LDS row stride (bf16)
+
+template <int EPI>
+__global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t As[LBM * LSTR];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[LBN * LSTR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.y * LBM;
+  const int n0 = blockIdx.x * LBN;
+  // global -> register staging: 4 x 16 B of A and of W per thread
+  uint4 ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int idx = tid + 256 * j, row = idx >> 3, seg = idx & 7;
+      const int64_t gm = min<int64_t>(m0 + row, a.M - 1);
+      const int gn = min(n0 + row, a.Nw - 1);
+      ra[j] = *reinterpret_cast<const uint4*>(a.x + gm * a.ldx + k0 + seg * 8);
+      rb[j] = *reinterpret_cast<const uint4*>(a.w + (int64_t)gn * a.ldw + k0 + seg * 8);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int idx = tid + 256 * j, row = idx >> 3, seg = idx & 7;
+      *reinterpret_cast<uint4*>(As + row * LSTR + seg * 8) = ra[j];
+      *reinterpret_cast<uint4*>(Bs + row * LSTR + seg * 8) = rb[j];
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.0f;
+  const int nk = a.K / LBK;
+  load(0);
+  store();
+  __syncthreads();
+  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load((kt + 1) * LBK);
+#pragma unroll
+    for (int kk = 0; kk < LBK / 16; ++kk) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 32 + fr) * LSTR + kk * 16 + fk);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 32 + fr) * LSTR + kk * 16 + fk);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      store();
+      __syncthreads();
+    }
+  }
+  // epilogue: acc[i][j][v] = C[row = 8 (v / 4) + 4 (lane / 32) + v % 4][col = lane % 32] of block (i, j)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + j * 32 + fr;
+    if (n >= a.N) continue;
+    const float bias = a.bias ? a.bias[n] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t m = m0 + wm * 64 + i * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        if (m >= a.M) continue;
+        float y = acc[i][j][v] + bias;
+        if (EPI == LIN_F32) {
+          reinterpret_cast<float*>(a.out)[m * a.ldo + n] = y;
+        } else if (EPI == LIN_BF16) {
+          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
+        } else if (EPI == LIN_BF16_QGELU) {
+          y = y / (1.0f + __expf(-1.702f * y));   // quick_gelu: x * sigmoid(1.702 x)
+          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
+        } else {   // LIN_F32_RESIDUAL
+          float* o = reinterpret_cast<float*>(a.out) + m * a.ldo + n;
+          *o = *o + y;
+        }
+      }
+  }
+}
+
+void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0) return;
+  const dim3 grid((a.N + LBN - 1) / LBN, (unsigned)((a.M + LBM - 1) / LBM));
+  switch (epi) {
+    case LIN_F32: hipLaunchKernelGGL(k_linear<LIN_F32>, grid, dim3(256), 0, s, a); break;
+    case LIN_BF16: hipLaunchKernelGGL(k_linear<LIN_BF16>, grid, dim3(256), 0, s, a); break;
+    case LIN_BF16_QGELU: hipLaunchKernelGGL(k_linear<LIN_BF16_QGELU>, grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_linear<LIN_F32_RESIDUAL>, grid, dim3(256), 0, s, a); break;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// attention (d_head = 64): block = (row b, head h, 128 queries), wave = 32
+// queries.  Per 64-key block: K (64 x 64) and V^T (64 x 64) staged in LDS.
+//   S^T tile t (keys 32 t .., 32 queries) = sum_kk mfma(A = K[keys][d kk],
+//   B = Q^T[d kk][queries]):  lane l holds keys 32 t + 8 (v/4) + 4 (l/32) + v%4
+//   of query l % 32.
+//   O^T (64 d x 32 q) += mfma(A = V^T[d][keys], B = P^T[keys][q]) over 4 key
+//   steps; key step kk covers, for lane half h, the keys
+//   32 (kk/2) + 8 (2 (kk%2) + e/4) + 4 h + e%4, e < 8 — exactly the S^T values
+//   the lane already holds, so P needs no shuffle; V^T is read with the same
+//   key order (two 8-byte LDS reads per fragment).
+// ---------------------------------------------------------------------------
+constexpr int AQ = 128, AK = 64, AD = 64, ASTR = 72;
+
+__global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[AK * ASTR];
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[AD * ASTR];
+  __shared__ int32_t kid[AK];   // key image id, or -1 for a non-pad key (no bias)
+  __shared__ __attribute__((aligned(16))) uint16_t Os[AQ * ASTR];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int S = a.S, D = a.heads * AD;
+  const int q0 = blockIdx.x * AQ, h = blockIdx.y, b = blockIdx.z;
+  const int64_t rowbase = (int64_t)b * S;
+  const int64_t ld = 3ll * D;
+  const uint16_t* qkv = a.qkv;
+  // this lane's query and its Q fragments (B operand: Q[q][d kk*16 + 8 (l/32) ..])
+  const int ql = q0 + wave * 32 + (lane & 31);
+  const int qc = min(ql, S - 1);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(qkv + (rowbase + qc) * ld + h * AD + kk * 16 + (lane >> 5) * 8);
+  const int32_t my_id = (int32_t)a.ids[rowbase + qc];
+  const float sc = a.scale * 1.4426950408889634f;   // logits in log2 units
+  const float bias2 = 1.4426950408889634f;           // +1.0 bias in log2 units
+  f32x16 o[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) o[t][v] = 0.0f;
+  float mrun = -INFINITY, lsum = 0.0f;
+  for (int k0 = 0; k0 < S; k0 += AK) {
+    __syncthreads();   // previous block's K / V^T reads done
+    // stage K rows and V^T: 64 keys x 64 d, 16 B per load (two per thread each)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = tid + 256 * j, key = idx >> 3, seg = idx & 7;
+      const int kg = min(k0 + key, S - 1);
+      const uint16_t* src = qkv + (rowbase + kg) * ld + h * AD + seg * 8;
+      const uint4 kv = *reinterpret_cast<const uint4*>(src + D);
+      const uint4 vv = *reinterpret_cast<const uint4*>(src + 2 * D);
+      *reinterpret_cast<uint4*>(Ks + key * ASTR + seg * 8) = kv;
+      const uint16_t* ve = reinterpret_cast<const uint16_t*>(&vv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) Vt[(seg * 8 + e) * ASTR + key] = ve[e];
+    }
+    if (tid < AK) {
+      const int kg = k0 + tid;
+      kid[tid] = (kg < S && a.key_pad[rowbase + kg]) ? (int32_t)a.ids[rowbase + kg] : -1;
+    }
+    __syncthreads();
+    // S^T tiles
+    f32x16 st[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) st[t][v] = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Ks + (t * 32 + (lane & 31)) * ASTR + kk * 16 + (lane >> 5) * 8);
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], st[t], 0, 0, 0);
+      }
+    }
+    // scale + bias, block max over the 64 keys of this query (lanes l and l ^ 32)
+    float bm = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int key = t * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        float x = st[t][v] * sc + (kid[key] == my_id ? bias2 : 0.0f);
+        if (k0 + key >= S) x = -INFINITY;
+        st[t][v] = x;
+        bm = fmaxf(bm, x);
+      }
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(bm), __float_as_uint(bm), false, false);
+      bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float mnew = fmaxf(mrun, bm);
+    const float alpha = exp2f(mrun - mnew);
+    mrun = mnew;
+    lsum *= alpha;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+    // P (bf16) in B-operand order: key step kk = (tile kk / 2, quarters 2 (kk % 2), +1)
+    bf16x8 pf[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int t = kk >> 1, v0 = 8 * (kk & 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = exp2f(st[t][v0 + e] - mnew);
+        lsum += p;
+        pf[kk][e] = (__bf16)p;
+      }
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int kb = 32 * (kk >> 1) + 8 * (2 * (kk & 1)) + 4 * (lane >> 5);
+        const uint16_t* vr = Vt + (dt * 32 + (lane & 31)) * ASTR + kb;
+        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
+        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 8);
+        bf16x8 vf;
+        uint32_t* vu = reinterpret_cast<uint32_t*>(&vf);
+        vu[0] = lo.x;
+        vu[1] = lo.y;
+        vu[2] = hi.x;
+        vu[3] = hi.y;
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kk], o[dt], 0, 0, 0);
+      }
+  }
+  // normalise: the query's sum is split over lanes l and l ^ 32
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(lsum), __float_as_uint(lsum), false, false);
+    lsum = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const float inv = 1.0f / lsum;
+  // O^T[d = 32 dt + 8 (v/4) + 4 (l/32) + v%4][query l%32] -> Os[query][d] -> coalesced rows
+  const int qr = wave * 32 + (lane & 31);
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int d = 32 * dt + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+      Os[qr * ASTR + d] = f2bf(o[dt][v] * inv);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int idx = tid + 256 * j, r = idx >> 3, seg = idx & 7;
+    if (q0 + r < S)
+      *reinterpret_cast<uint4*>(a.out + (rowbase + q0 + r) * (int64_t)a.ldo + h * AD + seg * 8) =
+          *reinterpret_cast<const uint4*>(Os + r * ASTR + seg * 8);
+  }
+}
+
+void launch_attention(const AttnArgs& a, hipStream_t s) {
+  if (a.R <= 0 || a.S <= 0) return;
+  hipLaunchKernelGGL(k_attention, dim3((a.S + AQ - 1) / AQ, a.heads, a.R), dim3(256), 0, s, a);
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm (torch semantics: biased variance, eps inside the sqrt), one wave
+// per token row; D % 64 == 0, D <= 64 * 64.
+// ---------------------------------------------------------------------------
+template <int PER>
+__device__ __forceinline__ void ln_row(const float* x, const float* g, const float* bt, float eps, int D,
+                                       float (&y)[PER]) {
+  const int lane = threadIdx.x & 63;
+  float v[PER];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < D ? x[c] : 0.0f;
+    s += v[i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)D;
+  float q = 0.0f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    const float dv = c < D ? v[i] - mean : 0.0f;
+    q += dv * dv;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    y[i] = c < D ? (v[i] - mean) * rstd * g[c] + bt[c] : 0.0f;
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void k_layernorm(LnArgs a) {
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int lane = threadIdx.x & 63;
+  float y[PER];
+  ln_row<PER>(a.x + m * a.ldx, a.gamma, a.beta, a.eps, a.D, y);
+  if (a.out_f32) {   // + position terms (embedding), f32 out
+    const int64_t c = a.ch[m], ph = a.pos[2 * m], pw = a.pos[2 * m + 1];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int cc = lane + 64 * i;
+      if (cc < a.D)
+        a.out_f32[m * a.ldo + cc] = y[i] + a.pos_h[ph * a.D + cc] + a.pos_w[pw * a.D + cc] + a.pos_c[c * a.D + cc];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int cc = lane + 64 * i;
+      if (cc < a.D) a.out_bf16[m * a.ldo + cc] = f2bf(y[i]);
+    }
+  }
+}
+
+void launch_layernorm(const LnArgs& a, hipStream_t s) {
+  if (a.M <= 0) return;
+  const unsigned grid = (unsigned)((a.M + 3) / 4);
+  const int per = (a.D + 63) / 64;
+  if (per <= 2) hipLaunchKernelGGL(k_layernorm<2>, dim3(grid), dim3(256), 0, s, a);
+  else if (per <= 4) hipLaunchKernelGGL(k_layernorm<4>, dim3(grid), dim3(256), 0, s, a);
+  else if (per <= 8) hipLaunchKernelGGL(k_layernorm<8>, dim3(grid), dim3(256), 0, s, a);
+  else if (per <= 16) hipLaunchKernelGGL(k_layernorm<16>, dim3(grid), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(k_layernorm<64>, dim3(grid), dim3(256), 0, s, a);
+}
+
+// x[m] += pos_h[h] + pos_w[w] + pos_c[c]   (decoder position embedding, modeling:88-93)
+__global__ void k_pos_add(PosArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.M * a.D) return;
+  const int64_t m = i / a.D;
+  const int cc = (int)(i - m * a.D);
+  const int64_t c = a.ch[m], ph = a.pos[2 * m], pw = a.pos[2 * m + 1];
+  a.x[m * a.ldx + cc] += a.pos_h[ph * a.D + cc] + a.pos_w[pw * a.D + cc] + a.pos_c[c * a.D + cc];
+}
+
+void launch_pos_add(const PosArgs& a, hipStream_t s) {
+  const int64_t n = a.M * a.D;
+  if (n > 0) hipLaunchKernelGGL(k_pos_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+// fp32 (M, K) -> bf16 (M, Kp), zero columns K .. Kp
+__global__ void k_to_bf16(const float* x, int64_t ldx, int64_t M, int K, int Kp, uint16_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * Kp) return;
+  const int64_t m = i / Kp;
+  const int k = (int)(i - m * Kp);
+  out[i] = k < K ? f2bf(x[m * ldx + k]) : (uint16_t)0;
+}
+
+void launch_to_bf16(const float* x, int64_t ldx, int64_t M, int K, int Kp, uint16_t* out, hipStream_t s) {
+  const int64_t n = M * Kp;
+  if (n > 0) hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, M, K, Kp, out);
+}
+
+// LFQ eval on (M, ncb * cbd) features: codes (M, ncb) int64 MSB-first
+// (lfq.py:87, 187), +-1 features into q_bf16 (M, ldq; zero pad to ldq) or q_f32
+__global__ void k_lfq_codes(LfqArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.M * a.ncb) return;
+  const int64_t m = i / a.ncb;
+  const int j = (int)(i - m * a.ncb);
+  const float* x = a.x + m * a.ldx + j * a.cbd;
+  int64_t code = 0;
+  for (int d = 0; d < a.cbd; ++d) {
+    const bool pos = x[d] > 0.0f;
+    code |= (int64_t)(pos ? 1 : 0) << (a.cbd - 1 - d);
+    const float q = pos ? a.scale : -a.scale;
+    if (a.q_bf16) a.q_bf16[m * a.ldq + j * a.cbd + d] = f2bf(q);
+    if (a.q_f32) a.q_f32[m * a.ldq + j * a.cbd + d] = q;
+  }
+  a.codes[i] = code;
+  if (a.q_bf16 && j == a.ncb - 1)
+    for (int k = a.ncb * a.cbd; k < a.ldq; ++k) a.q_bf16[m * a.ldq + k] = 0;
+}
+
+void launch_lfq_codes(const LfqArgs& a, hipStream_t s) {
+  const int64_t n = a.M * a.ncb;
+  if (n > 0) hipLaunchKernelGGL(k_lfq_codes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+}  // namespace dctae

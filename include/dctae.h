@@ -309,6 +309,63 @@ int dctae_timing_reset(dctae_ctx* ctx);
 /* Workspace cap in bytes for the chunked encode/decode (default 8 GiB). */
 int dctae_set_workspace_limit(dctae_ctx* ctx, int64_t bytes);
 
+/* ---- DCTAutoencoder transformer forward -----------------
+ * Operator-level entry points under the host mirror of
+ * modeling_dct_autoencoder.py (dct_autoencoder_amd/model.py): the CLIPEncoder
+ * (transformers==4.35.2 CLIPEncoderLayer) encoder / decoder around LFQ.
+ * bf16 tensors are uint16_t bit patterns; the caller owns every buffer.
+ * Linear: K % 64 == 0 (zero-padded), x / w rows 16-byte aligned (ld % 8 == 0). */
+#define DCTAE_LIN_F32 0           /* out f32 = x W^T + b */
+#define DCTAE_LIN_BF16 1          /* out bf16 = x W^T + b */
+#define DCTAE_LIN_BF16_QGELU 2    /* out bf16 = quick_gelu(x W^T + b)          (CLIPMLP fc1 + act) */
+#define DCTAE_LIN_F32_RESIDUAL 3  /* out f32 += x W^T + b (in place)          (residual adds) */
+
+/* nn.Linear (x (M, K) . W (N, K)^T + bias): q/k/v/out_proj, fc1/fc2
+ * (CLIPAttention / CLIPMLP), to_patch_embedding[0] (modeling:57), LFQ
+ * project_in / project_out (lfq.py:61-62), proj_out[1] (modeling:76).
+ * w_rows >= N rows are allocated (padding rows are never stored). */
+int dctae_model_linear(dctae_ctx* ctx, int64_t M, int32_t N, int32_t K, const uint16_t* x_dev, int64_t ldx,
+                       const uint16_t* w_dev, int32_t w_rows, int64_t ldw, const float* bias_dev, int32_t epilogue,
+                       void* out_dev, int64_t ldo, void* stream);
+
+/* CLIPAttention core (softmax(q k^T / sqrt(64) + attn_mask) v) for R packed
+ * rows of S tokens, head_dim 64: qkv (R*S, 3*heads*64) bf16 = [q | k | v];
+ * attn_mask is DCTPatches.attn_mask, (id_i == id_j) & key_pad_mask_j
+ * (FE:580-584), ADDED as +1.0 like transformers 4.35.2 (modeling:131-133),
+ * derived here from ids (R, S) int64 and key_pad (R, S) u8.  out (R*S, ldo)
+ * bf16, head h at columns 64 h. */
+int dctae_model_attention(dctae_ctx* ctx, int32_t R, int32_t S, int32_t heads, int32_t head_dim,
+                          const uint16_t* qkv_dev, const int64_t* ids_dev, const uint8_t* key_pad_dev,
+                          uint16_t* out_dev, int64_t ldo, void* stream);
+
+/* LayerNorm over D (torch semantics) of f32 rows -> bf16 (layer_norm1/2). */
+int dctae_model_layernorm(dctae_ctx* ctx, int64_t M, int32_t D, const float* x_dev, int64_t ldx,
+                          const float* gamma_dev, const float* beta_dev, float eps, uint16_t* out_dev, int64_t ldo,
+                          void* stream);
+
+/* to_patch_embedding[1] LayerNorm (eps 1e-4) + encoder position embedding
+ * (modeling:57-60, 98-108) -> f32 residual stream. */
+int dctae_model_embed_norm(dctae_ctx* ctx, int64_t M, int32_t D, const float* x_dev, int64_t ldx,
+                           const float* gamma_dev, const float* beta_dev, float eps, const float* pos_h_dev,
+                           const float* pos_w_dev, const float* pos_c_dev, const int64_t* ch_dev,
+                           const int64_t* pos_dev, float* out_dev, int64_t ldo, void* stream);
+
+/* x += pos_h[h] + pos_w[w] + pos_c[c] (decoder position embedding, modeling:79-93). */
+int dctae_model_pos_add(dctae_ctx* ctx, int64_t M, int32_t D, float* x_dev, int64_t ldx, const float* pos_h_dev,
+                        const float* pos_w_dev, const float* pos_c_dev, const int64_t* ch_dev,
+                        const int64_t* pos_dev, void* stream);
+
+/* f32 (M, K) -> bf16 (M, Kp), columns K .. Kp zero. */
+int dctae_model_to_bf16(dctae_ctx* ctx, int64_t M, int32_t K, const float* x_dev, int64_t ldx, int32_t Kp,
+                        uint16_t* out_dev, void* stream);
+
+/* LFQ.forward eval on projected features (lfq.py:164-212): x (M, ncb*cbd)
+ * f32 -> codes (M, ncb) int64 MSB-first, +-scale features into q_bf16
+ * (M, ldq; zero-padded) and/or q_f32 (M, ldq). */
+int dctae_model_lfq(dctae_ctx* ctx, int64_t M, int32_t ncb, int32_t cbd, float scale, const float* x_dev,
+                    int64_t ldx, int64_t* codes_dev, uint16_t* q_bf16_dev, float* q_f32_dev, int64_t ldq,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif
