@@ -3,9 +3,9 @@
 // (modeling_dct_autoencoder.py; transformers==4.35.2 CLIPEncoderLayer).
 //
 //   k_linear<EPI>   y = x W^T (+ bias) on v_mfma_f32_32x32x16_bf16: 128 x 128
-//                   tiles, BK = 64, 4 waves of 64 x 64, LDS rows padded to 72
-//                   bf16 (conflict-free ds_read_b128 fragments), next K tile
-//                   prefetched into registers; epilogues: f32 store, bf16
+//                   tiles, BK = 64, 4 waves of 64 x 64, operands staged by
+//                   global_load_lds into two XOR-swizzled LDS buffers (tile
+//                   k+1 in flight during tile k); epilogues: f32 store, bf16
 //                   store, bf16 quick_gelu, f32 residual add (in place)
 //   k_attention     flash attention, d_head = 64: S^T = K Q^T so the softmax
 //                   probabilities come out of the MFMA already in B-operand
@@ -39,36 +39,44 @@ __device__ __forceinline__ uint16_t f2bf(float f) {   // round to nearest even
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
 // ---------------------------------------------------------------------------
-// linear
+// linear: 128 x 128 tile, BK = 64, 4 waves of 64 x 64 (2 x 2 MFMA 32x32x16
+// blocks), A and W tiles staged global -> LDS with global_load_lds_dwordx4
+// (async, no VGPR staging) into two LDS buffers: tile k+1 is in flight while
+// tile k is multiplied.  One wave-instruction writes 1 KB = 8 rows x 64 bf16
+// lane-linearly; the XOR swizzle is applied to the global source address:
+// 16-byte segment s of row r holds k-segment s ^ g(r), g(r) = (r >> 1) & 7,
+// so every ds_read_b128 lane group (16 rows, one k-segment) covers the 16
+// slots of a 256-byte bank row: conflict-free fragment reads.
 // ---------------------------------------------------------------------------
-constexpr int LBM = 128, LBN = 128, LBK = 64, LSTR = 72;   // LDS row stride (bf16)
+constexpr int LBM = 128, LBN = 128, LBK = 64;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ int lswz(int row, int kseg) { return row * LBK + ((kseg ^ ((row >> 1) & 7)) << 3); }
 
 template <int EPI>
 __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t As[LBM * LSTR];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[LBN * LSTR];
+  __shared__ __attribute__((aligned(16))) uint16_t L[2 * (LBM + LBN) * LBK];   // [buf][A 128 rows | W 128 rows][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t m0 = (int64_t)blockIdx.y * LBM;
   const int n0 = blockIdx.x * LBN;
-  // global -> register staging: 4 x 16 B of A and of W per thread
-  uint4 ra[4], rb[4];
-  auto load = [&](int k0) {
+  // this lane's glds sources: wave-instruction j covers rows 8 (4 wave + j) + lane / 8, slot lane % 8
+  const uint16_t* srcA[4];
+  const uint16_t* srcW[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * wave + j) + (lane >> 3), slot = lane & 7;
+    const int kseg = slot ^ ((row >> 1) & 7);
+    srcA[j] = a.x + min<int64_t>(m0 + row, a.M - 1) * a.ldx + kseg * 8;
+    srcW[j] = a.w + (int64_t)min(n0 + row, a.Nw - 1) * a.ldw + kseg * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    uint16_t* base = L + buf * (LBM + LBN) * LBK;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int idx = tid + 256 * j, row = idx >> 3, seg = idx & 7;
-      const int64_t gm = min<int64_t>(m0 + row, a.M - 1);
-      const int gn = min(n0 + row, a.Nw - 1);
-      ra[j] = *reinterpret_cast<const uint4*>(a.x + gm * a.ldx + k0 + seg * 8);
-      rb[j] = *reinterpret_cast<const uint4*>(a.w + (int64_t)gn * a.ldw + k0 + seg * 8);
-    }
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int idx = tid + 256 * j, row = idx >> 3, seg = idx & 7;
-      *reinterpret_cast<uint4*>(As + row * LSTR + seg * 8) = ra[j];
-      *reinterpret_cast<uint4*>(Bs + row * LSTR + seg * 8) = rb[j];
+      __builtin_amdgcn_global_load_lds((const void*)(srcA[j] + k0), (lds_ptr_t)(base + 8 * (4 * wave + j) * LBK), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(srcW[j] + k0), (lds_ptr_t)(base + (LBM + 8 * (4 * wave + j)) * LBK),
+                                       16, 0, 0);
     }
   };
   f32x16 acc[2][2];
@@ -79,31 +87,30 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.0f;
   const int nk = a.K / LBK;
-  load(0);
-  store();
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const int fr = lane & 31, fk = (lane >> 5) * 8;
+  const int fr = lane & 31, fh = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load((kt + 1) * LBK);
+    if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * LBK);
+    const uint16_t* As = L + (kt & 1) * (LBM + LBN) * LBK;
+    const uint16_t* Ws = As + LBM * LBK;
 #pragma unroll
     for (int kk = 0; kk < LBK / 16; ++kk) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 32 + fr) * LSTR + kk * 16 + fk);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + lswz(wm * 64 + i * 32 + fr, 2 * kk + fh));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 32 + fr) * LSTR + kk * 16 + fk);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Ws + lswz(wn * 64 + j * 32 + fr, 2 * kk + fh));
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
-    if (kt + 1 < nk) {
-      store();
-      __syncthreads();
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile kt + 1 landed
+    __syncthreads();                                    // ... for every wave; tile kt's buffer free
   }
   // epilogue: acc[i][j][v] = C[row = 8 (v / 4) + 4 (lane / 32) + v % 4][col = lane % 32] of block (i, j)
 #pragma unroll
@@ -115,7 +122,7 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int64_t m = m0 + wm * 64 + i * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
+        const int64_t m = m0 + wm * 64 + i * 32 + 8 * (v >> 2) + 4 * fh + (v & 3);
         if (m >= a.M) continue;
         float y = acc[i][j][v] + bias;
         if (EPI == LIN_F32) {
