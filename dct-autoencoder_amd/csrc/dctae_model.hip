@@ -167,8 +167,8 @@ constexpr int AQ = 128, AK = 64, AD = 64, ASTR = 72;
 
 __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AK * ASTR];
-  __shared__ __attribute__((aligned(16))) uint16_t Vt[AD * ASTR];
-  __shared__ int32_t kid[AK];   // key image id, or -1 for a non-pad key (no bias)
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[AK * ASTR];   // row-major; read transposed (ds_read_b64_tr_b16)
+  __shared__ __attribute__((aligned(16))) int32_t kid[AK];   // key image id, or -1 for a non-pad key (no bias)
   __shared__ __attribute__((aligned(16))) uint16_t Os[AQ * ASTR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int S = a.S, D = a.heads * AD;
@@ -193,8 +193,8 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
     for (int v = 0; v < 16; ++v) o[t][v] = 0.0f;
   float mrun = -INFINITY, lsum = 0.0f;
   for (int k0 = 0; k0 < S; k0 += AK) {
-    __syncthreads();   // previous block's K / V^T reads done
-    // stage K rows and V^T: 64 keys x 64 d, 16 B per load (two per thread each)
+    __syncthreads();   // previous block's K / V reads done
+    // stage K and V rows: 64 keys x 64 d, 16 B per load (two per thread each)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int idx = tid + 256 * j, key = idx >> 3, seg = idx & 7;
@@ -203,15 +203,15 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
       const uint4 kv = *reinterpret_cast<const uint4*>(src + D);
       const uint4 vv = *reinterpret_cast<const uint4*>(src + 2 * D);
       *reinterpret_cast<uint4*>(Ks + key * ASTR + seg * 8) = kv;
-      const uint16_t* ve = reinterpret_cast<const uint16_t*>(&vv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) Vt[(seg * 8 + e) * ASTR + key] = ve[e];
+      *reinterpret_cast<uint4*>(Vs + key * ASTR + seg * 8) = vv;
     }
+    bool pad = false;
     if (tid < AK) {
       const int kg = k0 + tid;
-      kid[tid] = (kg < S && a.key_pad[rowbase + kg]) ? (int32_t)a.ids[rowbase + kg] : -1;
+      pad = kg < S && a.key_pad[rowbase + kg];
+      kid[tid] = pad ? (int32_t)a.ids[rowbase + kg] : -1;
     }
-    __syncthreads();
+    const bool any_pad = __syncthreads_or(pad);   // block-uniform: the +1 bias only ever hits pad keys
     // S^T tiles
     f32x16 st[2];
 #pragma unroll
@@ -226,16 +226,34 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
     }
     // scale + bias, block max over the 64 keys of this query (lanes l and l ^ 32)
     float bm = -INFINITY;
+    if (any_pad) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const int4 ki = *reinterpret_cast<const int4*>(kid + t * 32 + 8 * q4 + 4 * (lane >> 5));
+          st[t][4 * q4 + 0] = st[t][4 * q4 + 0] * sc + (ki.x == my_id ? bias2 : 0.0f);
+          st[t][4 * q4 + 1] = st[t][4 * q4 + 1] * sc + (ki.y == my_id ? bias2 : 0.0f);
+          st[t][4 * q4 + 2] = st[t][4 * q4 + 2] * sc + (ki.z == my_id ? bias2 : 0.0f);
+          st[t][4 * q4 + 3] = st[t][4 * q4 + 3] * sc + (ki.w == my_id ? bias2 : 0.0f);
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) st[t][v] *= sc;
+    }
+    if (k0 + AK > S) {   // last, partial key block
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          if (k0 + t * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3) >= S) st[t][v] = -INFINITY;
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int key = t * 32 + 8 * (v >> 2) + 4 * (lane >> 5) + (v & 3);
-        float x = st[t][v] * sc + (kid[key] == my_id ? bias2 : 0.0f);
-        if (k0 + key >= S) x = -INFINITY;
-        st[t][v] = x;
-        bm = fmaxf(bm, x);
-      }
+      for (int v = 0; v < 16; ++v) bm = fmaxf(bm, st[t][v]);
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(bm), __float_as_uint(bm), false, false);
       bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
@@ -260,21 +278,26 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
         pf[kk][e] = (__bf16)p;
       }
     }
-    // O^T += V^T P^T
+    // O^T += V^T P^T; the A fragment V^T[d = 32 dt + lane % 32][keys kb + (0..3), kb + 8 + (0..3)] comes
+    // from the row-major V tile by two transposed reads: lane 4q + p of each 16-lane group addresses key
+    // row kb + q, columns 4p .. 4p + 3 of the group's 16 d columns, and receives its own column
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    const int gq = (lane & 15) >> 2, gp = lane & 3, gx = (lane >> 4) & 1;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int kb = 32 * (kk >> 1) + 8 * (2 * (kk & 1)) + 4 * (lane >> 5);
-        const uint16_t* vr = Vt + (dt * 32 + (lane & 31)) * ASTR + kb;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vr);
-        const uint2 hi = *reinterpret_cast<const uint2*>(vr + 8);
+        const uint16_t* vr = Vs + (kb + gq) * ASTR + 32 * dt + 16 * gx + 4 * gp;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)vr);
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vr + 8 * ASTR));
         bf16x8 vf;
-        uint32_t* vu = reinterpret_cast<uint32_t*>(&vf);
-        vu[0] = lo.x;
-        vu[1] = lo.y;
-        vu[2] = hi.x;
-        vu[3] = hi.y;
+        short* vsh = reinterpret_cast<short*>(&vf);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vsh[e] = lo[e];
+          vsh[4 + e] = hi[e];
+        }
         o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kk], o[dt], 0, 0, 0);
       }
   }
