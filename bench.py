@@ -132,6 +132,7 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the config-3 decode timing")
     ap.add_argument("--no-stats", action="store_true", help="skip the config-5 PatchNorm fit (RCCL) timing")
+    ap.add_argument("--no-model", action="store_true", help="skip the DCTAutoencoder transformer timing")
     ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
 
@@ -298,6 +299,16 @@ def main():
         except Exception as e:  # noqa: BLE001 — the encode line must still print
             stats = {"error": f"{type(e).__name__}: {e}"}
 
+    # the DCTAutoencoder transformer forward (patch14-l, 4 rows x 3072 tokens)
+    model = None
+    if not args.no_model:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import model_bench
+            model = model_bench.run(rows=4, steps=3, warmup=1, dev=dev)
+        except Exception as e:  # noqa: BLE001 — the encode line must still print
+            model = {"error": f"{type(e).__name__}: {e}"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import ref_cpu
@@ -331,6 +342,7 @@ def main():
             "kernels": kernels,
             "decode": decode,
             "stats_fit": stats,
+            "model": model,
             "options": args.opt,
         }
         print(json.dumps(line))

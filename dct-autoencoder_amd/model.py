@@ -29,7 +29,7 @@ NotImplementedError.
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, Optional
 
 import torch
@@ -66,22 +66,25 @@ class CLIPEncoderConfig:
         return cls(**{k: v for k, v in c.items() if k in cls.__dataclass_fields__})
 
 
-@dataclass
 class DCTAutoencoderConfig:
-    """configuration_dct_autoencoder.py:5-41 (same argument names and defaults)."""
-    image_channels: int = 3
-    patch_size: int = 16
-    max_patch_h: int = 32
-    max_patch_w: int = 32
-    vq_codebook_size: int = 4096
-    vq_num_codebooks: int = 8
-    vq_type: str = "lfq"
-    encoder_config: CLIPEncoderConfig = field(default_factory=CLIPEncoderConfig)
-    decoder_config: CLIPEncoderConfig = field(default_factory=CLIPEncoderConfig)
+    """configuration_dct_autoencoder.py:5-41: same argument names and defaults;
+    sub-configs may be dicts or CLIPVisionConfig-like objects, extra keys
+    (e.g. ``transformers_version`` of a saved config.json) are kept as attributes."""
 
-    def __post_init__(self):
-        self.encoder_config = CLIPEncoderConfig.from_any(self.encoder_config)
-        self.decoder_config = CLIPEncoderConfig.from_any(self.decoder_config)
+    def __init__(self, image_channels: int = 3, patch_size: int = 16, max_patch_h: int = 32, max_patch_w: int = 32,
+                 vq_codebook_size: int = 4096, vq_num_codebooks: int = 8, vq_type: str = "lfq",
+                 encoder_config=None, decoder_config=None, **kwargs):
+        self.image_channels = image_channels
+        self.patch_size = patch_size
+        self.max_patch_h = max_patch_h
+        self.max_patch_w = max_patch_w
+        self.vq_codebook_size = vq_codebook_size
+        self.vq_num_codebooks = vq_num_codebooks
+        self.vq_type = vq_type
+        self.encoder_config = CLIPEncoderConfig.from_any(encoder_config)
+        self.decoder_config = CLIPEncoderConfig.from_any(decoder_config)
+        for k, v in kwargs.items():
+            setattr(self, k, v)
 
 
 class _Attention(nn.Module):
@@ -160,7 +163,9 @@ class DCTAutoencoder(nn.Module):
     def __init__(self, config: DCTAutoencoderConfig):
         super().__init__()
         if not isinstance(config, DCTAutoencoderConfig):
-            config = DCTAutoencoderConfig(**{k: getattr(config, k) for k in DCTAutoencoderConfig.__dataclass_fields__})
+            keys = ("image_channels", "patch_size", "max_patch_h", "max_patch_w", "vq_codebook_size",
+                    "vq_num_codebooks", "vq_type", "encoder_config", "decoder_config")
+            config = DCTAutoencoderConfig(**{k: getattr(config, k) for k in keys if hasattr(config, k)})
         self.config = config
         d = config.encoder_config.hidden_size
         if config.decoder_config.hidden_size != d:
