@@ -69,18 +69,13 @@ struct dctae_ctx {
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   int dual_stream = 1;                // several chunks: rows / columns on two streams, T double-buffered
-  int pipe = 0;                       // 1: several 512^2 chunks, rows of chunk k + columns of chunk k - 1 per grid;
-                                      // 2: one launch over image groups (columns wait on their group's rows)
-  int pipe_group = 16;                // images per group (pipe 2)
-  int* pipe_cnt = nullptr;            // group counters (pipe 2)
-  int pipe_cnt_n = 0;
   hipStream_t s2 = nullptr;
   std::vector<hipEvent_t> chunk_ev;
   // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
   int sort_kernel = 2;                // 1: bitonic in LDS (1024 threads), 2: rocPRIM block radix sort
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int fused = 0;                      // measured slower than the two kernels so far (profile: DESIGN.md)
-  int fused_slots = 2;                // T slots per XCD (lookahead = slots - 1 images)
+  int fused_slots = 1;                // T slots per XCD (lookahead = slots - 1 images); only 1 is accepted
   int fused_bpc = 4;                  // resident workgroups per CU
   int fused_spin = 1 << 20;           // poll bound of a dependence wait (~1 s), then err |= 8
   int fused_rows_pct = 50;            // share of row workers
@@ -563,7 +558,6 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->plan_host) hipHostFree(ctx->plan_host);
   if (ctx->plan_dev) hipFree(ctx->plan_dev);
   if (ctx->err_dev) hipFree(ctx->err_dev);
-  if (ctx->pipe_cnt) hipFree(ctx->pipe_cnt);
   if (ctx->fft_tab) hipFree(ctx->fft_tab);
   if (ctx->st_ws) hipFree(ctx->st_ws);
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
@@ -625,13 +619,11 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
   else if (k == "dual_stream") ctx->dual_stream = value != 0;
-  else if (k == "pipe" && value >= 0 && value <= 2) ctx->pipe = (int)value;
-  else if (k == "pipe_group" && value >= 2 && value <= 4096 && value % 2 == 0) ctx->pipe_group = (int)value;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "cols_ipb" && (value == 2 || value == 4)) ctx->cols_ipb = (int)value;
   else if (k == "cols_pf") ctx->cols_pf = value != 0;
-  else if (k == "fused_slots" && value >= 1 && value <= 16) ctx->fused_slots = (int)value;
+  else if (k == "fused_slots" && value == 1) ctx->fused_slots = 1;   // 2-3 slots: intermittent code mismatches
   else if (k == "fused_bpc" && value >= 1 && value <= 8) ctx->fused_bpc = (int)value;
   else if (k == "fused_rows_pct" && value >= 1 && value <= 99) ctx->fused_rows_pct = (int)value;
   else if (k == "fused_debug" && value >= 0 && value <= 3) ctx->fused_debug = (int)value;
@@ -711,7 +703,6 @@ int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
   if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
   if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
   if (h & 8) return fail(ctx, DCTAE_EHIP, "fused encode: a dependence wait timed out (outputs invalid)");
-  if (h & 32) return fail(ctx, DCTAE_EHIP, "pipelined encode: a workgroup ran off its XCD (outputs invalid)");
   if (h & 16) return fail(ctx, DCTAE_EINVAL, "VectorQuantize index out of range of the codebook");
   return 0;
 }
@@ -1025,7 +1016,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout +
                              1024 * ctx->xcd_order + 4096 * ctx->fused + 8192 * ctx->fused_slots +
-                             (1 << 20) * ctx->cols_kernel + (1 << 24) * ctx->dual_stream + (1 << 25) * ctx->pipe + (1ll << 28) * ctx->pipe_group,
+                             (1 << 20) * ctx->cols_kernel + (1 << 24) * ctx->dual_stream,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1181,87 +1172,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       }
   };
   const int nJ = E.fused_spec ? 0 : (int)E.jobs.size();
-  // one-grid pipeline: every job all 512^2 (spec 1) with a cols7 image list
-  bool pipe = ctx->pipe && nJ > 1 && E.dual && ctx->cols_kernel == 7 && ctx->t_layout == 0 && ctx->cols_ipb == 2;
-  for (int k = 0; pipe && k < nJ; ++k) {
-    const ChunkJob& j = E.jobs[k];
-    pipe = !j.any_gemm_rows && !j.any_gemm_cols && !j.n_fr[0] && !j.n_fc[0] && j.n_pc > 0 &&
-           (int)j.n_pc == j.i1 - j.i0 && j.n_fr[1] > 0;
-    for (int v = 2; pipe && v < kVariants; ++v) pipe = !j.n_fr[v] && !j.n_fc[v];
-  }
-  if (pipe && !(epj.median && epj.thr && !sk.norm && epj.maxph <= 32 && epj.cb_dim == 14 && epj.ncb == 14))
-    pipe = false;
-  // pipe = 2, one chunk of 512^2 images: ONE launch over image groups (k_enc_pipe2)
-  bool pipe2 = ctx->pipe == 2 && nJ == 1 && ctx->cols_kernel == 7 && ctx->t_layout == 0 && ctx->cols_ipb == 2 &&
-               epj.median && epj.thr && !sk.norm && epj.maxph <= 32 && epj.cb_dim == 14 && epj.ncb == 14;
-  if (pipe2) {
-    const ChunkJob& j = E.jobs[0];
-    const int nimg = j.i1 - j.i0;
-    pipe2 = !j.any_gemm_rows && !j.any_gemm_cols && !j.n_fr[0] && !j.n_fc[0] && j.n_pc == nimg && j.n_fr[1] > 0 &&
-            j.n_fr[1] % nimg == 0 && nimg % (8 * ctx->pipe_group) == 0 && ctx->pipe_group % 2 == 0 &&
-            ctx->n_cu >= 256;
-    for (int v = 2; pipe2 && v < kVariants; ++v) pipe2 = !j.n_fr[v] && !j.n_fc[v];
-  }
-  if (pipe2) {
-    const ChunkJob& j = E.jobs[0];
-    const int nimg = j.i1 - j.i0, gsz = ctx->pipe_group;
-    Pipe2Args pa{};
-    pa.imgs = (const ImgDesc*)(pd + j.desc_off);
-    pa.rblocks = (const int2*)(pd + j.fr_off[1]);
-    pa.list = (const int*)(pd + j.pc_off);
-    pa.rgb = imgs->rgb_dev;
-    pa.ws = ctx->ws;
-    const int ng = nimg / gsz;
-    if (ctx->pipe_cnt_n < ng) {
-      if (ctx->pipe_cnt) HIPCHK(ctx, hipFree(ctx->pipe_cnt));
-      ctx->pipe_cnt = nullptr;
-      HIPCHK(ctx, hipMalloc((void**)&ctx->pipe_cnt, (size_t)ng * sizeof(int)));
-      ctx->pipe_cnt_n = ng;
-    }
-    HIPCHK(ctx, hipMemsetAsync(ctx->pipe_cnt, 0, (size_t)ng * sizeof(int), s));
-    pa.done = ctx->pipe_cnt;
-    pa.err = ctx->err_dev;
-    pa.tw_r = ctx->fft_tab + j.tw_off[1];
-    pa.post_r = ctx->fft_tab + j.post_off_r[1];
-    pa.tw_c = ctx->fft_tab + j.tw_off_c[1];
-    pa.post_c = ctx->fft_tab + j.post_off_c[1];
-    pa.n_groups = nimg / gsz;
-    pa.gsz = gsz;
-    pa.rb_per_img = j.n_fr[1] / nimg;
-    pa.qw = j.pc_qw;
-    pa.nR = pa.rb_per_img * gsz;
-    pa.nC = cols7_grid(gsz, j.pc_qw, 2);
-    pa.spin_limit = ctx->fused_spin;
-    Timer t(ctx, s, "enc_pipe");
-    launch_enc_pipe2(pa, ctx->cm, epj, sk, s);
-  } else if (pipe) {
-    for (int k = 0; k <= nJ; ++k) {
-      PipeArgs pa{};
-      pa.rgb = imgs->rgb_dev;
-      pa.ws = ctx->ws;
-      if (k < nJ) {
-        const ChunkJob& j = E.jobs[k];
-        pa.imgs_r = (const ImgDesc*)(pd + j.desc_off);
-        pa.rblocks = (const int2*)(pd + j.fr_off[1]);
-        pa.n_rb = j.n_fr[1];
-        pa.tw_r = ctx->fft_tab + j.tw_off[1];
-        pa.post_r = ctx->fft_tab + j.post_off_r[1];
-      }
-      if (k >= 1) {
-        const ChunkJob& j = E.jobs[k - 1];
-        pa.imgs_c = (const ImgDesc*)(pd + j.desc_off);
-        pa.list = (const int*)(pd + j.pc_off);
-        pa.n_list = j.n_pc;
-        pa.qw = j.pc_qw;
-        pa.n_items = 3 * j.pc_qw;
-        pa.n_cb = cols7_grid(j.n_pc, j.pc_qw, 2);
-        pa.tw_c = ctx->fft_tab + j.tw_off_c[1];
-        pa.post_c = ctx->fft_tab + j.post_off_c[1];
-      }
-      Timer t(ctx, s, "enc_pipe");
-      launch_enc_pipe(pa, ctx->cm, epj, sk, s);
-    }
-  } else if (nJ > 1 && E.dual) {
+  if (nJ > 1 && E.dual) {
     // chunk pipeline on two streams: rows of chunk k (stream s) overlap the
     // columns of chunk k - 1 (second stream); chunk k's T lives in ws half k % 2,
     // so rows(k) waits for cols(k - 2).  Chunks are sized so both halves stay

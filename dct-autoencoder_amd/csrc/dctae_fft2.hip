@@ -1177,44 +1177,6 @@ __global__ __launch_bounds__(256) void k_fft_cols7(const ImgDesc* __restrict__ i
   cols7_block<THR, IPB, PF>(blockIdx.x, imgs, list, n_list, n_items, qw, ws, tw, post, ep, sk, L, post4, tw_s, sbias);
 }
 
-// ---------------------------------------------------------------------------
-// Row / column pipeline in ONE grid (N = 512, chunked encode): the row blocks
-// of chunk k and the cols7 blocks of chunk k - 1 (its T written by the
-// previous launch) are interleaved in proportion over the grid, so every CU
-// runs HBM-bound row work beside latency-bound column work.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_enc_pipe(PipeArgs a, ColorMats cm, EncParams ep, TokenSinks sk) {
-  union U {
-    RowsLds<512> r;
-    Cols7Lds c;
-  };
-  __shared__ U L;
-  __shared__ float4 post4[257];
-  __shared__ float2 tw_s[256];
-  __shared__ float sbias[32];
-  const int64_t b = blockIdx.x, tot = (int64_t)a.n_rb + a.n_cb;
-  const int64_t r0 = b * a.n_rb / tot, r1 = (b + 1) * a.n_rb / tot;
-  if (r1 > r0) {   // row block r0 of chunk k
-    const float2* p2 = a.post_r;
-    float2* ps = reinterpret_cast<float2*>(post4);
-    for (int i = threadIdx.x; i < 2 * 257; i += 256) ps[i] = p2[i];
-    for (int i = threadIdx.x; i < 256; i += 256) tw_s[i] = a.tw_r[i];
-    __syncthreads();
-    const int2 jb = a.rblocks[r0];
-    const ImgDesc d = a.imgs_r[jb.x];
-    rows2_item<512, 16, 16, false, false>(d, jb.y, a.rgb, a.ws + d.ws_t, L.r, ps, tw_s, cm);
-  } else {         // column block (b - r0) of chunk k - 1
-    cols7_block<true, 2, true>((int)(b - r0), a.imgs_c, a.list, a.n_list, a.n_items, a.qw, a.ws, a.tw_c, a.post_c,
-                               ep, sk, L.c, post4, tw_s, sbias);
-  }
-}
-
-void launch_enc_pipe(const PipeArgs& a, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk,
-                     hipStream_t s) {
-  if (a.n_rb + a.n_cb <= 0) return;
-  hipLaunchKernelGGL(k_enc_pipe, dim3(a.n_rb + a.n_cb), dim3(256), 0, s, a, cm, ep, sk);
-}
-
 int cols7_grid(int n_list, int qw, int ipb) {
   const int n_items = 3 * qw, per_x = (n_items + 7) / 8;
   return 8 * per_x * ((n_list + ipb - 1) / ipb);
@@ -1423,72 +1385,6 @@ __global__ __launch_bounds__(256, 4) void k_enc_fused(FusedParams p_, const ImgD
       atomicAdd(pr + 6, 1ull);
     }
   }
-}
-
-// One launch, eight XCD-local pipelines: workgroup b runs on XCD b % 8 (the
-// round-robin dispatch order; checked against HW_REG_XCC_ID, err |= 32 on a
-// mismatch), XCD x owns the image groups x, x + 8, ...  The T written by a
-// row block is read by column blocks of the same XCD, through that XCD's L2:
-// no L2 write-back / invalidate is needed (a release to another XCD's L2 costs
-// a buffer_wbl2 per row block: 10 ms per 1024 images, measured).  Each T
-// region is read once per launch, after its rows are done, so the CU L1s
-// hold no stale lines of it either.
-__global__ __launch_bounds__(256) void k_enc_pipe2(Pipe2Args a, ColorMats cm, EncParams ep, TokenSinks sk) {
-  union U {
-    RowsLds<512> r;
-    Cols7Lds c;
-  };
-  __shared__ U L;
-  __shared__ float4 post4[257];
-  __shared__ float2 tw_s[256];
-  __shared__ float sbias[32];
-  const int x = blockIdx.x & 7;
-  const int64_t bl = blockIdx.x >> 3;
-  if (is_wave0() && xcc_id() != x) {
-    const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    if (lane == 0) atomicOr(a.err, 32);
-  }
-  const int nR = a.nR, nC = a.nC, G = a.n_groups / 8;   // groups of this XCD
-  // stage 0: rows(0); stage s in [1, G): rows(s) + cols(s - 1); stage G: cols(G - 1)
-  int stage;
-  int64_t off;
-  if (bl < nR) {
-    stage = 0;
-    off = bl;
-  } else {
-    const int64_t u = bl - nR;
-    stage = 1 + (int)min<int64_t>(u / (nR + nC), G - 1);
-    off = u - (int64_t)(stage - 1) * (nR + nC);
-  }
-  const int n_r = stage < G ? nR : 0, n_c = stage > 0 ? nC : 0;
-  const int64_t tot = (int64_t)n_r + n_c;
-  const int64_t r0 = off * n_r / tot, r1 = (off + 1) * n_r / tot;
-  if (r1 > r0) {   // row block r0 of local group `stage`
-    const int g = x + 8 * stage;
-    float2* ps = reinterpret_cast<float2*>(post4);
-    for (int i = threadIdx.x; i < 2 * 257; i += 256) ps[i] = a.post_r[i];
-    for (int i = threadIdx.x; i < 256; i += 256) tw_s[i] = a.tw_r[i];
-    __syncthreads();
-    const int2 jb = a.rblocks[(int64_t)g * nR + r0];
-    const ImgDesc d = a.imgs[jb.x];
-    rows2_item<512, 16, 16, false, false>(d, jb.y, a.rgb, a.ws + d.ws_t, L.r, ps, tw_s, cm);
-    signal_done(a.done + g);
-  } else {         // column block (off - r0) of local group stage - 1, after all its row blocks
-    const int g = x + 8 * (stage - 1);
-    if (is_wave0()) {
-      if (!wait_count(a.done + g, nR, a.spin_limit)) atomicOr(a.err, 8);
-    }
-    __syncthreads();
-    cols7_block<true, 2, true>((int)(off - r0), a.imgs, a.list + (int64_t)g * a.gsz, a.gsz, 3 * a.qw, a.qw, a.ws,
-                               a.tw_c, a.post_c, ep, sk, L.c, post4, tw_s, sbias);
-  }
-}
-
-void launch_enc_pipe2(const Pipe2Args& a, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk,
-                      hipStream_t s) {
-  const int64_t grid = (int64_t)a.n_groups * (a.nR + a.nC);
-  if (grid <= 0) return;
-  hipLaunchKernelGGL(k_enc_pipe2, dim3((unsigned)grid), dim3(256), 0, s, a, cm, ep, sk);
 }
 
 int fused_rows_per_item() { return 16; }

@@ -123,43 +123,6 @@ struct FusedParams {   // k_enc_fused's by-value parameter block (first kernel a
   TokenSinks sk;
 };
 
-// Row / column pipeline launch (k_enc_pipe, dctae_fft2.hip): the row blocks
-// of chunk k and the cols7 blocks of chunk k - 1 in one grid (N = 512).
-struct PipeArgs {
-  const ImgDesc* imgs_r;    // chunk k: descriptors, row blocks (image, first row)
-  const int2* rblocks;
-  int32_t n_rb;
-  const float* rgb;
-  const float2* tw_r;
-  const float2* post_r;
-  const ImgDesc* imgs_c;    // chunk k - 1: descriptors, cols7 image list
-  const int* list;
-  int32_t n_list, n_items, qw, n_cb;
-  const float2* tw_c;
-  const float2* post_c;
-  float* ws;
-};
-
-// One-launch pipeline over image groups (k_enc_pipe2): stage s holds the row
-// blocks of group s and the cols7 blocks of group s - 1 (interleaved); a column
-// block first waits until every row block of its group has signalled.
-struct Pipe2Args {
-  const ImgDesc* imgs;
-  const int2* rblocks;      // all row blocks, grouped by image (rb_per_img per image)
-  const int* list;          // cols7 image list (all images)
-  const float* rgb;
-  float* ws;
-  int* done;                // [n_groups] row blocks finished per group (zeroed per launch)
-  int* err;
-  const float2* tw_r;
-  const float2* post_r;
-  const float2* tw_c;
-  const float2* post_c;
-  int32_t n_groups, gsz, rb_per_img, qw;
-  int32_t nR, nC;           // row / column blocks per group
-  int32_t spin_limit;
-};
-
 struct DecodeArgs {
   const int64_t* ids;       // (R,S)
   const uint8_t* key_pad;   // (R,S)

@@ -73,9 +73,7 @@ void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, in
                            float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 
 int fused_rows_per_item();
-void launch_enc_pipe(const PipeArgs& a, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
 int cols7_grid(int n_list, int qw, int ipb);
-void launch_enc_pipe2(const Pipe2Args& a, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
 void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,
                       const TokenSinks& sk, hipStream_t s);
 

@@ -362,12 +362,11 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-DEFAULTS = {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 2,
-            "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1, "pipe": 0}
+DEFAULTS = {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 1,
+            "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "fused": {"fused": 1},
-    "fused_1slot": {"fused": 1, "fused_slots": 1},
     "cols_lds_scatter": {"cols_kernel": 2},
     "cols_linear": {"cols_kernel": 4},
     "cols_pairs": {"cols_kernel": 5},
@@ -379,7 +378,6 @@ SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS a
     "sort_bitonic": {"sort_kernel": 1},
     "chunks_dual_stream": {"chunk_bytes": 4 << 20, "dual_stream": 1},
     "chunks_one_stream": {"chunk_bytes": 4 << 20, "dual_stream": 0},
-    "chunks_one_grid_pipeline": {"chunk_bytes": 4 << 20, "dual_stream": 1, "pipe": 1},
     "t_strips": {"t_layout": 1},
     "t_strips16": {"t_layout": 2},
     "t_rowmajor_pad16": {"t_layout": 3},
@@ -418,20 +416,20 @@ def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
         assert (c_s.cpu()[r, sj] != c_g.cpu()[r, gj]).sum().item() <= 4
 
 
-@pytest.mark.parametrize("slots", [1, 2, 3])
+@pytest.mark.parametrize("rep", [0, 1, 2])
 @pytest.mark.parametrize("shape,n", [((512, 512), 27), ((224, 224), 70)])
-def test_fused_matches_unfused_bitwise(fe, pn, lfq, shape, n, slots):
+def test_fused_matches_unfused_bitwise(fe, pn, lfq, shape, n, rep):
     """k_enc_fused (rows and columns in one persistent launch, T handed over
     through the XCD's L2 ring slots) runs the same arithmetic as the two
-    separate kernels: every output bit-identical.  n > 8 XCD queues x slots,
-    so every ring slot is reused (write-after-read hand-off) several times.
+    separate kernels: every output bit-identical.  n > 8 XCD queues, so every
+    ring slot is reused (write-after-read hand-off) several times; repeated on
+    fresh inputs (2-3 slots showed intermittent mismatches and are refused).
     The fused kernel runs the column item of cols_kernel 7 (512^2) / 4 (224^2),
     so the unfused leg is pinned to that column kernel (the other column
     kernels order the complex maths differently: last-ulp differences in the
     coefficients, codes agree either way)."""
     ops = _ops()
-    x = torch.from_numpy(np.stack(rng.synth_images(61 + slots, [shape] * n))).to(DEV)
-    ops.set_option("fused_slots", slots)
+    x = torch.from_numpy(np.stack(rng.synth_images(61 + rep, [shape] * n))).to(DEV)
     ops.set_option("cols_kernel", 7)
     try:
         outs = {}
@@ -442,7 +440,6 @@ def test_fused_matches_unfused_bitwise(fe, pn, lfq, shape, n, slots):
         ops.check_device_errors(x.device)
     finally:
         ops.set_option("fused", 0)
-        ops.set_option("fused_slots", 2)
         ops.set_option("cols_kernel", DEFAULTS["cols_kernel"])
     for (a_list, b_list) in zip(outs[1], outs[0]):
         for (dp_a, c_a), (dp_b, c_b) in zip(a_list, b_list):
@@ -500,26 +497,3 @@ def test_fft_decode_patches_roundtrip_512(fe):
     ok, dmax = _rgb_close(img.cpu(), ref, atol=1e-5, rtol=1e-5)
     assert ok, dmax
 
-
-@pytest.mark.parametrize("group", [2])
-def test_group_pipeline_matches_default_bitwise(fe, pn, lfq, group):
-    """pipe = 2 (k_enc_pipe2: one launch; the column blocks of image group g
-    interleaved with the row blocks of group g + 1 and waiting on group g's
-    row counter) runs the same row / cols7 arithmetic: outputs bit-identical."""
-    ops = _ops()
-    x = torch.from_numpy(np.stack(rng.synth_images(71, [(512, 512)] * 32))).to(DEV)
-    outs = {}
-    try:
-        for pipe in (2, 0):
-            ops.set_option("pipe", pipe)
-            ops.set_option("pipe_group", group)
-            outs[pipe] = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
-        ops.check_device_errors(x.device)
-    finally:
-        ops.set_option("pipe", 0)
-        ops.set_option("pipe_group", 16)
-    for (dp_a, c_a), (dp_b, c_b) in zip(outs[2], outs[0]):
-        assert torch.equal(c_a, c_b)
-        assert torch.equal(dp_a.patch_positions, dp_b.patch_positions)
-        assert torch.equal(dp_a.key_pad_mask, dp_b.key_pad_mask)
-        assert torch.equal(dp_a.patches.view(torch.int32), dp_b.patches.view(torch.int32))
