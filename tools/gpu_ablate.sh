@@ -1,6 +1,7 @@
 #!/bin/bash
 # Ablation timing of the column kernel: builds variants with parts skipped
-# (-DDCTAE_ABLATE=mask: 1 load, 2 pass 1, 4 pass 2, 8 post, 16 epilogue) and
+# (-DDCTAE_ABLATE=mask: columns 1 load, 2 pass 1, 4 pass 2, 8 post, 16 epilogue;
+# rows 32 no T stores, 64 no RGB loads) and
 # benches each through DCTAE_LIBRARY (results are wrong; only timings matter).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -9,7 +10,7 @@ if [ "${BUILD:-0}" = 1 ]; then
   cd dct-autoencoder_amd/csrc
   for m in "$@"; do
     /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -std=c++17 -ffp-contract=off -DDCTAE_ABLATE=$m \
-      -o ../../_ablate/libdctae_$m.so dctae_kernels.hip dctae_fft.hip dctae_fft2.hip dctae_idct.hip dctae_vq.hip dctae_stats.hip dctae_api.hip || exit 1
+      -o ../../_ablate/libdctae_$m.so dctae_kernels.hip dctae_fft.hip dctae_fft2.hip dctae_idct.hip dctae_vq.hip dctae_stats.hip dctae_model.hip dctae_api.hip || exit 1
   done
   cd ../..
 fi
