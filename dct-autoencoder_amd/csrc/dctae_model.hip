@@ -58,8 +58,14 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t L[2 * (LBM + LBN) * LBK];   // [buf][A 128 rows | W 128 rows][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * LBM;
-  const int n0 = blockIdx.x * LBN;
+  // XCD-aware tile order: workgroup b runs on XCD b % 8; give each XCD a contiguous
+  // range of tile ids, row-major over (M tile, N tile), so an XCD's blocks share
+  // their A rows through its L2 (A is then read from HBM once, not once per XCD)
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int ntn = (a.N + LBN - 1) / LBN;
+  const int64_t m0 = (int64_t)(wgid / ntn) * LBM;
+  const int n0 = (wgid % ntn) * LBN;
   // this lane's glds sources: wave-instruction j covers rows 8 (4 wave + j) + lane / 8, slot lane % 8
   const uint16_t* srcA[4];
   const uint16_t* srcW[4];
@@ -142,7 +148,7 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
 
 void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0) return;
-  const dim3 grid((a.N + LBN - 1) / LBN, (unsigned)((a.M + LBM - 1) / LBM));
+  const dim3 grid((unsigned)(((a.N + LBN - 1) / LBN) * ((a.M + LBM - 1) / LBM)));
   switch (epi) {
     case LIN_F32: hipLaunchKernelGGL(k_linear<LIN_F32>, grid, dim3(256), 0, s, a); break;
     case LIN_BF16: hipLaunchKernelGGL(k_linear<LIN_BF16>, grid, dim3(256), 0, s, a); break;
