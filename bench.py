@@ -120,6 +120,44 @@ def stats_fit_leg(pkg, fe, dev, rank, world, dist, steps, n_img=8, size=512):
             tdist.destroy_process_group()
 
 
+def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
+    """SURVEY §8(d) configs 2 and 4 on this GPU (informational; the metric is config 3's shape):
+    config 2 = 256 x 224^2 encode (pre-planned BatchEncoder, inputs resident);
+    config 4 = 1024 ragged images, (H, W) ~ U{14..1024}^2 (seed 7), encode_batch (host
+    planning + packing included: the plan depends on the sizes)."""
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    out = {}
+    x2 = ops.synth_images(256, 224, 224, seed=1234, first_index=rank * 256, device=dev)
+    enc2 = fe_mod.BatchEncoder(fe, 256, 224, 224, pn, lfq, device=dev)
+    enc2(x2)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        enc2(x2)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    out["config2"] = {"workload": "256 x 224x224 encode", "ms_per_step": round(el * 1e3, 4),
+                      "value": round(256 * 224 * 224 / el / 1e6, 1), "unit": "Mpix/s"}
+    g = np.random.default_rng(7)
+    hw = g.integers(14, 1025, size=(1024, 2))
+    imgs = [ops.synth_images(1, int(h), int(w), seed=7, first_index=rank * 1024 + i, device=dev)[0]
+            for i, (h, w) in enumerate(hw)]
+    fe.encode_batch(imgs, pn, lfq)
+    torch.cuda.synchronize(dev)
+    n4 = max(1, min(steps, 3))
+    t0 = time.perf_counter()
+    for _ in range(n4):
+        fe.encode_batch(imgs, pn, lfq)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / n4
+    pix = int((hw[:, 0] * hw[:, 1]).sum())
+    out["config4"] = {"workload": "1024 ragged images, (H, W) ~ U{14..1024}^2 seed 7, encode_batch incl. host packing",
+                      "ms_per_step": round(el * 1e3, 3), "value": round(pix / el / 1e6, 1), "unit": "Mpix/s"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,6 +171,7 @@ def main():
     ap.add_argument("--no-decode", action="store_true", help="skip the config-3 decode timing")
     ap.add_argument("--no-stats", action="store_true", help="skip the config-5 PatchNorm fit (RCCL) timing")
     ap.add_argument("--no-model", action="store_true", help="skip the DCTAutoencoder transformer timing")
+    ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / config 4 timings")
     ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
 
@@ -299,6 +338,13 @@ def main():
         except Exception as e:  # noqa: BLE001 — the encode line must still print
             stats = {"error": f"{type(e).__name__}: {e}"}
 
+    configs = None
+    if not args.no_configs:
+        try:
+            configs = config_legs(pkg, fe, pn, lfq, dev, rank, args.steps)
+        except Exception as e:  # noqa: BLE001 — the encode line must still print
+            configs = {"error": f"{type(e).__name__}: {e}"}
+
     # the DCTAutoencoder transformer forward (patch14-l, 4 rows x 3072 tokens)
     model = None
     if not args.no_model:
@@ -343,6 +389,7 @@ def main():
             "decode": decode,
             "stats_fit": stats,
             "model": model,
+            "other_configs": configs,
             "options": args.opt,
         }
         print(json.dumps(line))

@@ -124,40 +124,66 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const GemmProblem* __restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
 
-  for (int k0 = 0; k0 < p.K; k0 += GK) {
-    // ---- stage A and B tiles (generic strides, zero-filled at the edges)
+  // ---- staging: the next K chunk is loaded into registers while the current
+  //      one is multiplied (generic strides, zero-filled at the edges)
+  constexpr int EPT = (GT * GK) / 256;   // elements per thread and operand tile
+  float ra[NC][EPT], rb[NC][EPT];
+  auto load = [&](int k0) {
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       if (c == 0 || !a_shared) {
         const float* A = p.A + (int64_t)c * p.sAc;
         const bool kfast = (p.sAk == 1);
 #pragma unroll
-        for (int i = 0; i < (GT * GK) / 256; ++i) {
-          int e = tid + 256 * i;
-          int mm = kfast ? (e >> 5) : (e & 63);
-          int kk = kfast ? (e & 31) : (e >> 6);
-          int gm = m0 + mm, gk = k0 + kk;
-          float v = 0.0f;
-          if (gm < p.M && gk < p.K) v = A[(int64_t)gm * p.sAm + (int64_t)gk * p.sAk];
-          As[c][mm * GLD + kk] = v;
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + 256 * i;
+          const int mm = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          const int gm = m0 + mm, gk = k0 + kk;
+          ra[c][i] = (gm < p.M && gk < p.K) ? A[(int64_t)gm * p.sAm + (int64_t)gk * p.sAk] : 0.0f;
         }
       }
       if (c == 0 || !b_shared) {
         const float* B = p.B + (int64_t)c * p.sBc;
         const bool kfast = (p.sBk == 1);
 #pragma unroll
-        for (int i = 0; i < (GT * GK) / 256; ++i) {
-          int e = tid + 256 * i;
-          int nn = kfast ? (e >> 5) : (e & 63);
-          int kk = kfast ? (e & 31) : (e >> 6);
-          int gn = n0 + nn, gk = k0 + kk;
-          float v = 0.0f;
-          if (gn < p.N && gk < p.K) v = B[(int64_t)gn * p.sBn + (int64_t)gk * p.sBk];
-          Bs[c][nn * GLD + kk] = v;
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + 256 * i;
+          const int nn = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          const int gn = n0 + nn, gk = k0 + kk;
+          rb[c][i] = (gn < p.N && gk < p.K) ? B[(int64_t)gn * p.sBn + (int64_t)gk * p.sBk] : 0.0f;
         }
       }
     }
-    __syncthreads();
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (c == 0 || !a_shared) {
+        const bool kfast = (p.sAk == 1);
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + 256 * i;
+          const int mm = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          As[c][mm * GLD + kk] = ra[c][i];
+        }
+      }
+      if (c == 0 || !b_shared) {
+        const bool kfast = (p.sBk == 1);
+#pragma unroll
+        for (int i = 0; i < EPT; ++i) {
+          const int e = tid + 256 * i;
+          const int nn = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          Bs[c][nn * GLD + kk] = rb[c][i];
+        }
+      }
+    }
+  };
+  load(0);
+  store();
+  __syncthreads();
+  for (int k0 = 0; k0 < p.K; k0 += GK) {
+    const bool more = k0 + GK < p.K;
+    if (more) load(k0 + GK);
     // ---- MFMA: lane half h takes k = 8g + 4h + s in step s of group g
 #pragma unroll
     for (int g = 0; g < GK / 8; ++g) {
@@ -178,6 +204,10 @@ __global__ __launch_bounds__(256) void k_gemm_f32(const GemmProblem* __restrict_
       }
     }
     __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
   }
   // ---- store: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll

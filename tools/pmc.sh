@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc
 mkdir -p $OUT
-BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-stats --no-model ${BENCH_ARGS:-}"
+BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-stats --no-model --no-configs ${BENCH_ARGS:-}"
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 i=0
 while [ $# -gt 0 ]; do
