@@ -105,7 +105,7 @@ constexpr int GK = 32;      // k chunk
 constexpr int GLD = GK + 4; // LDS row stride (floats), keeps float4 alignment
 
 template <int NC>
-__global__ __launch_bounds__(256) void k_gemm_f32(const GemmProblem* __restrict__ probs,
+__global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restrict__ probs,
                                                   const TileRef* __restrict__ tiles) {
   __shared__ __attribute__((aligned(16))) float As[NC][GT * GLD];
   __shared__ __attribute__((aligned(16))) float Bs[NC][GT * GLD];
