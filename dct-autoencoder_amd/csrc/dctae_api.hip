@@ -259,22 +259,28 @@ int ensure_ws(dctae_ctx* ctx, size_t ws_bytes, size_t stage_bytes) {
   return 0;
 }
 
-// orthonormal DCT-II matrix rows [0, rows) of size N, fp64 -> fp32
-int dct_matrix(dctae_ctx* ctx, int N, int rows, const float** out) {
-  auto key = std::make_pair(N, rows);
+// orthonormal DCT-II matrix rows [0, rows) of size N, fp64 -> fp32.
+// parity 0 / 1: the even / odd rows k = 2i (+1) restricted to the columns
+// n < ceil(N/2) / floor(N/2), the operand of the folded transform
+// X[k] = sum_n C[k][n] (x[n] +- x[N-1-n]) (C[k][N-1-n] = (-1)^k C[k][n]).
+int dct_matrix(dctae_ctx* ctx, int N, int rows, const float** out, int parity = -1) {
+  auto key = std::make_pair(N, rows * 4 + parity + 1);
   auto it = ctx->dct.find(key);
   if (it != ctx->dct.end()) {
     *out = it->second;
     return 0;
   }
-  std::vector<float> h((size_t)rows * N);
+  const int R = parity < 0 ? rows : (parity == 0 ? (rows + 1) / 2 : rows / 2);
+  const int Nc = parity < 0 ? N : (parity == 0 ? (N + 1) / 2 : N / 2);
+  std::vector<float> h((size_t)std::max(R, 1) * std::max(Nc, 1));
   const double pi = 3.14159265358979323846;
-  for (int k = 0; k < rows; ++k) {
+  for (int i = 0; i < R; ++i) {
+    const int k = parity < 0 ? i : 2 * i + parity;
     double sk = (k == 0) ? std::sqrt(1.0 / N) : std::sqrt(2.0 / N);
-    for (int n = 0; n < N; ++n) {
+    for (int n = 0; n < Nc; ++n) {
       // reduce the angle exactly: cos(pi*(2n+1)k/(2N)) with (2n+1)k mod 4N
       long long a = ((long long)(2 * n + 1) * k) % (4ll * N);
-      h[(size_t)k * N + n] = (float)(sk * std::cos(pi * (double)a / (2.0 * N)));
+      h[(size_t)i * Nc + n] = (float)(sk * std::cos(pi * (double)a / (2.0 * N)));
     }
   }
   float* d = nullptr;
@@ -884,13 +890,19 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       const ImgDesc& d = D[i];
       const int li = i - j.i0;
       if (d.plan_w < 0) {
-        const float* CW;
-        if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW))) return rc;
-        // T[c][y][kx] = sum_x CW[kx][x] * IPT[c][y][x]
-        GemmProblem g = gemm(CW, 0, d.W, 1, ws + d.ws_p, (int64_t)d.H * d.W, d.W, 1, ws + d.ws_t,
-                             (int64_t)d.Kw * d.H, 1, d.Kw, d.Kw, d.H, d.W, 3);
-        add_tiles(rt, (int)(probs.size() - p0), g);
-        probs.push_back(g);
+        // T[c][y][kx] = sum_x CW[kx][x] * IPT[c][y][x], folded: even kx over
+        // IPT[x] + IPT[W-1-x], odd kx over IPT[x] - IPT[W-1-x] (half the flops)
+        for (int par = 0; par < 2; ++par) {
+          const int M = par ? d.Kw / 2 : (d.Kw + 1) / 2, K = par ? d.W / 2 : (d.W + 1) / 2;
+          if (M == 0) continue;
+          const float* CW;
+          if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW, par))) return rc;
+          // B: the folded IPT (k_rgb_to_ipt), u at x < ceil(W/2), v after it
+          GemmProblem g = gemm(CW, 0, K, 1, ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1,
+                               ws + d.ws_t + par, (int64_t)d.Kw * d.H, 2, d.Kw, M, d.H, K, 3);
+          add_tiles(rt, (int)(probs.size() - p0), g);
+          probs.push_back(g);
+        }
         j.any_gemm_rows = 1;
       } else {
         const FftPlan& p = plans[d.plan_w];
@@ -903,13 +915,20 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         }
       }
       if (d.plan_h < 0) {
-        const float* CH;
-        if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH))) return rc;
-        // Y[c][ky][kx] = sum_y CH[ky][y] * T[c][y][kx]
-        GemmProblem g = gemm(CH, 0, d.H, 1, ws + d.ws_t, (int64_t)d.Kw * d.H, 1, d.Kw, ws + d.ws_y,
-                             (int64_t)d.Kh * d.Kw, d.Kw, 1, d.Kh, d.Kw, d.H, 3);
-        add_tiles(ct, (int)(probs.size() - p0), g);
-        probs.push_back(g);
+        // Y[c][ky][kx] = sum_y CH[ky][y] * T[c][y][kx], folded along y as the rows
+        for (int par = 0; par < 2; ++par) {
+          const int M = par ? d.Kh / 2 : (d.Kh + 1) / 2, K = par ? d.H / 2 : (d.H + 1) / 2;
+          if (M == 0) continue;
+          const float* CH;
+          if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH, par))) return rc;
+          // B: T folded in place (k_fold_t): u in rows m < ceil(H/2), v[m] in row H-1-m
+          GemmProblem g = gemm(CH, 0, K, 1, ws + d.ws_t + (par ? (int64_t)(d.H - 1) * d.Kw : 0),
+                               (int64_t)d.Kw * d.H, 1, par ? -(int64_t)d.Kw : d.Kw,
+                               ws + d.ws_y + (int64_t)par * d.Kw, (int64_t)d.Kh * d.Kw, 2 * (int64_t)d.Kw, 1, M,
+                               d.Kw, K, 3);
+          add_tiles(ct, (int)(probs.size() - p0), g);
+          probs.push_back(g);
+        }
         j.any_gemm_cols = 1;
       } else {
         const FftPlan& p = plans[d.plan_h];
@@ -1150,6 +1169,10 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     if (j.any_gemm_cols) {
+      {
+        Timer t(ctx, st, "fold_t");
+        launch_fold_t(dd, nj, j.max_hw, ctx->ws, st);
+      }
       {
         Timer t(ctx, st, "gemm_cols");
         launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st);

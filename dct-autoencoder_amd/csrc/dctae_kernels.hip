@@ -42,28 +42,73 @@ void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_
 // colour transforms (reference util.py:70-97)
 // ---------------------------------------------------------------------------
 
+// IPT of the images whose rows run through the GEMM DCT, written folded for
+// the even / odd halves of the transform: row y holds u[x] = p[x] + p[W-1-x]
+// at x < ceil(W/2) (u = p at the middle of an odd W) and v[x] = p[x] - p[W-1-x]
+// at ceil(W/2) + x, x < floor(W/2).  One thread per pixel pair.
 __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
                              float* __restrict__ ws, ColorMats cm) {
   const ImgDesc d = imgs[blockIdx.y];
   if (d.plan_w >= 0) return;  // rows of this image run through k_fft_rows (IPT fused there)
   const int64_t hw = (int64_t)d.H * d.W;
+  const int Wh = (d.W + 1) / 2;
+  const int64_t n_pairs = (int64_t)d.H * Wh;
   const float* src = rgb + d.rgb_off;
   float* dst = ws + d.ws_p;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < hw;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  auto ipt = [&](int64_t e, float out[3]) {
     float r = src[e], g = src[hw + e], b = src[2 * hw + e];
     float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), 0.430000007152557373046875f);
     float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), 0.430000007152557373046875f);
     float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), 0.430000007152557373046875f);
-    dst[e] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
-    dst[hw + e] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
-    dst[2 * hw + e] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+    for (int c = 0; c < 3; ++c) out[c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
+  };
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_pairs;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t y = e / Wh;
+    const int x = (int)(e - y * Wh), x2 = d.W - 1 - x;
+    const int64_t row = y * d.W;
+    float a[3], b[3];
+    ipt(row + x, a);
+    if (x2 != x) {
+      ipt(row + x2, b);
+      for (int c = 0; c < 3; ++c) {
+        dst[c * hw + row + x] = a[c] + b[c];
+        dst[c * hw + row + Wh + x] = a[c] - b[c];
+      }
+    } else {
+      for (int c = 0; c < 3; ++c) dst[c * hw + row + x] = a[c];
+    }
   }
+}
+
+// T (3, H, Kw) of the images whose columns run through the GEMM DCT, folded
+// in place along y: T[m] <- T[m] + T[H-1-m], T[H-1-m] <- T[m] - T[H-1-m]
+// for m < floor(H/2) (the middle row of an odd H is kept).
+__global__ void k_fold_t(const ImgDesc* __restrict__ imgs, float* __restrict__ ws) {
+  const ImgDesc d = imgs[blockIdx.y];
+  if (d.plan_h >= 0) return;
+  const int64_t n = (int64_t)(d.H / 2) * d.Kw;
+  float* t = ws + d.ws_t;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < 3 * n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e / n);
+    const int64_t r = e - c * n;
+    const int64_t m = r / d.Kw, kx = r - m * d.Kw;
+    float* p0 = t + (int64_t)c * d.H * d.Kw + m * d.Kw + kx;
+    float* p1 = t + (int64_t)c * d.H * d.Kw + (d.H - 1 - m) * d.Kw + kx;
+    const float a = *p0, b = *p1;
+    *p0 = a + b;
+    *p1 = a - b;
+  }
+}
+
+void launch_fold_t(const ImgDesc* imgs, int n_img, int64_t max_hw, float* ws, hipStream_t s) {
+  int gx = (int)std::min<int64_t>((3 * max_hw / 2 + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_fold_t, dim3(std::max(gx, 1), n_img), dim3(256), 0, s, imgs, ws);
 }
 
 void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* rgb, float* ws,
                        const ColorMats& cm, hipStream_t s) {
-  int gx = (int)std::min<int64_t>((max_hw + 255) / 256, 1024);
+  int gx = (int)std::min<int64_t>((max_hw / 2 + 256) / 256, 1024);
   hipLaunchKernelGGL(k_rgb_to_ipt, dim3(gx, n_img), dim3(256), 0, s, imgs, rgb, ws, cm);
 }
 
