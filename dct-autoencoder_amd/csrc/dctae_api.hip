@@ -481,7 +481,7 @@ struct ChunkJob {
   int n_rows_tiles, n_cols_tiles;
   size_t pc_off;      // persistent column kernel (cols_kernel 6): spec-1 images of the job, uniform qw
   int n_pc, pc_qw;
-  int max_T, any_gemm_rows, any_gemm_cols;
+  int max_T, any_gemm_rows, any_gemm_cols, fold_t;
   int64_t max_hw;
   size_t lds_rows, lds_cols;
 };
@@ -921,7 +921,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           if (M == 0) continue;
           const float* CH;
           if ((rc = dct_matrix(ctx, d.H, std::min(d.H, rows_cap), &CH, par))) return rc;
-          // B: T folded in place (k_fold_t): u in rows m < ceil(H/2), v[m] in row H-1-m
+          // B: T folded along y (by the row GEMM of the y-folded IPT, or in place by
+          // k_fold_t after FFT rows): u in rows m < ceil(H/2), v[m] in row H-1-m
           GemmProblem g = gemm(CH, 0, K, 1, ws + d.ws_t + (par ? (int64_t)(d.H - 1) * d.Kw : 0),
                                (int64_t)d.Kw * d.H, 1, par ? -(int64_t)d.Kw : d.Kw,
                                ws + d.ws_y + (int64_t)par * d.Kw, (int64_t)d.Kh * d.Kw, 2 * (int64_t)d.Kw, 1, M,
@@ -930,6 +931,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           probs.push_back(g);
         }
         j.any_gemm_cols = 1;
+        if (d.plan_w >= 0) j.fold_t = 1;
       } else {
         const FftPlan& p = plans[d.plan_h];
         // generic kernel: one tile column per block; specialised: groups of
@@ -1169,7 +1171,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     if (j.any_gemm_cols) {
-      {
+      if (j.fold_t) {
         Timer t(ctx, st, "fold_t");
         launch_fold_t(dd, nj, j.max_hw, ctx->ws, st);
       }

@@ -155,7 +155,26 @@ __device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
   if (j == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
-  if (ep.median && sk.codes && j < P) sk.codes[tok * P + j] = (uint16_t)(__builtin_bitreverse32(bits) >> (32 - P));
+  if (ep.median && sk.codes) {
+    if (ep.cb_dim == P && ep.ncb == P) {
+      if (j < P) sk.codes[tok * P + j] = (uint16_t)(__builtin_bitreverse32(bits) >> (32 - P));
+    } else {
+      // other LFQ groupings: gather the group's row bits, cut the flat
+      // (row-major) sign-bit string into codebook_dim-bit codes, MSB first
+      uint32_t rb[P];
+      const int base = (int)(threadIdx.x & 63) & ~15;
+#pragma unroll
+      for (int r = 0; r < P; ++r) rb[r] = (uint32_t)__shfl((int)bits, base + r, 64);
+      for (int q = j; q < ep.ncb; q += 16) {
+        uint32_t code = 0;
+        for (int d = 0; d < ep.cb_dim; ++d) {
+          const int e = q * ep.cb_dim + d;
+          code |= ((rb[e / P] >> (e % P)) & 1u) << (ep.cb_dim - 1 - d);
+        }
+        sk.codes[tok * ep.ncb + q] = (uint16_t)code;
+      }
+    }
+  }
 }
 
 // token_epilogue_p with the thresholds already in registers (thr[p] covers

@@ -43,16 +43,22 @@ void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_
 // ---------------------------------------------------------------------------
 
 // IPT of the images whose rows run through the GEMM DCT, written folded for
-// the even / odd halves of the transform: row y holds u[x] = p[x] + p[W-1-x]
-// at x < ceil(W/2) (u = p at the middle of an odd W) and v[x] = p[x] - p[W-1-x]
-// at ceil(W/2) + x, x < floor(W/2).  One thread per pixel pair.
+// the even / odd halves of the transform.  Along x (every such image): row y
+// holds u[x] = p[x] + p[W-1-x] at x < ceil(W/2) (u = p at the middle of an
+// odd W) and v[x] = p[x] - p[W-1-x] at ceil(W/2) + x, x < floor(W/2).  Along
+// y (images whose columns also run through the GEMM): row m < floor(H/2)
+// holds p[m] + p[H-1-m] and row H-1-m holds p[m] - p[H-1-m]; the row DCT is
+// linear per row, so the row GEMM then yields T already folded for the
+// column GEMM.  One thread per group of up to 4 mirrored pixels.
 __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
                              float* __restrict__ ws, ColorMats cm) {
   const ImgDesc d = imgs[blockIdx.y];
   if (d.plan_w >= 0) return;  // rows of this image run through k_fft_rows (IPT fused there)
   const int64_t hw = (int64_t)d.H * d.W;
   const int Wh = (d.W + 1) / 2;
-  const int64_t n_pairs = (int64_t)d.H * Wh;
+  const bool yfold = d.plan_h < 0;
+  const int Hh = yfold ? (d.H + 1) / 2 : d.H;
+  const int64_t n_groups = (int64_t)Hh * Wh;
   const float* src = rgb + d.rgb_off;
   float* dst = ws + d.ws_p;
   auto ipt = [&](int64_t e, float out[3]) {
@@ -62,31 +68,45 @@ __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __re
     float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), 0.430000007152557373046875f);
     for (int c = 0; c < 3; ++c) out[c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
   };
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_pairs;
+  // x-fold of one row's pair (p[x], p[x2]) into row `row`
+  auto put_row = [&](int64_t row, int x, bool pair, const float* a, const float* b) {
+    for (int c = 0; c < 3; ++c) {
+      dst[c * hw + row + x] = pair ? a[c] + b[c] : a[c];
+      if (pair) dst[c * hw + row + Wh + x] = a[c] - b[c];
+    }
+  };
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_groups;
        e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t y = e / Wh;
-    const int x = (int)(e - y * Wh), x2 = d.W - 1 - x;
-    const int64_t row = y * d.W;
-    float a[3], b[3];
-    ipt(row + x, a);
-    if (x2 != x) {
-      ipt(row + x2, b);
+    const int y = (int)(e / Wh);
+    const int x = (int)(e - (int64_t)y * Wh), x2 = d.W - 1 - x, y2 = d.H - 1 - y;
+    const bool xp = x2 != x, yp = yfold && y2 != y;
+    float a[3], b[3] = {0.f, 0.f, 0.f};
+    ipt((int64_t)y * d.W + x, a);
+    if (xp) ipt((int64_t)y * d.W + x2, b);
+    if (yp) {
+      float c2[3], d2[3] = {0.f, 0.f, 0.f}, s0[3], s1[3], t0[3], t1[3];
+      ipt((int64_t)y2 * d.W + x, c2);
+      if (xp) ipt((int64_t)y2 * d.W + x2, d2);
       for (int c = 0; c < 3; ++c) {
-        dst[c * hw + row + x] = a[c] + b[c];
-        dst[c * hw + row + Wh + x] = a[c] - b[c];
+        s0[c] = a[c] + c2[c];
+        s1[c] = b[c] + d2[c];
+        t0[c] = a[c] - c2[c];
+        t1[c] = b[c] - d2[c];
       }
+      put_row((int64_t)y * d.W, x, xp, s0, s1);
+      put_row((int64_t)y2 * d.W, x, xp, t0, t1);
     } else {
-      for (int c = 0; c < 3; ++c) dst[c * hw + row + x] = a[c];
+      put_row((int64_t)y * d.W, x, xp, a, b);
     }
   }
 }
 
-// T (3, H, Kw) of the images whose columns run through the GEMM DCT, folded
-// in place along y: T[m] <- T[m] + T[H-1-m], T[H-1-m] <- T[m] - T[H-1-m]
-// for m < floor(H/2) (the middle row of an odd H is kept).
+// T (3, H, Kw) of the images whose columns run through the GEMM DCT but rows
+// through the FFT, folded in place along y: T[m] <- T[m] + T[H-1-m],
+// T[H-1-m] <- T[m] - T[H-1-m] for m < floor(H/2) (middle row of an odd H kept).
 __global__ void k_fold_t(const ImgDesc* __restrict__ imgs, float* __restrict__ ws) {
   const ImgDesc d = imgs[blockIdx.y];
-  if (d.plan_h >= 0) return;
+  if (d.plan_h >= 0 || d.plan_w < 0) return;  // GEMM rows: folded by k_rgb_to_ipt
   const int64_t n = (int64_t)(d.H / 2) * d.Kw;
   float* t = ws + d.ws_t;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < 3 * n; e += (int64_t)gridDim.x * blockDim.x) {
@@ -306,9 +326,43 @@ __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict
   }
 }
 
+// patch size fixed at compile time: one block per (tile row h, channel c) of
+// an image stages the P spectrum rows it covers (contiguous in Y) through LDS
+// with coalesced loads, then one 16-lane group per tile runs
+// token_epilogue_p on its row held in registers.
+template <int P>
+__global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restrict__ imgs,
+                                                         const float* __restrict__ ws, EncParams ep,
+                                                         TokenSinks sk) {
+  extern __shared__ float ys[];
+  const ImgDesc d = imgs[blockIdx.y];
+  if (d.plan_h >= 0) return;
+  const int c = blockIdx.x % 3, h = blockIdx.x / 3;
+  if (h >= d.qh) return;
+  const int Kw = d.Kw, ld = Kw + 1;
+  const float* Y = ws + d.ws_y + ((int64_t)c * d.Kh + (int64_t)P * h) * Kw;
+  for (int e = threadIdx.x; e < P * Kw; e += 256) {
+    const int r = e / Kw;
+    ys[r * ld + (e - r * Kw)] = Y[e];
+  }
+  __syncthreads();
+  const int g16 = threadIdx.x >> 4, j = threadIdx.x & 15;
+  const int jr = j < P ? j : 0;
+  for (int w = g16; w < d.qw; w += 16) {
+    float vals[P];
+#pragma unroll
+    for (int p2 = 0; p2 < P; ++p2) vals[p2] = ys[jr * ld + P * w + p2];
+    token_epilogue_p<P>(ep, c, h, w, j, vals, d.tok_off + (int64_t)(h * d.qw + w) * 3 + c, sk);
+  }
+}
+
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws,
                           const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
-  hipLaunchKernelGGL(k_tile_epilogue, dim3((max_T + 63) / 64, n_img), dim3(256), 0, s, imgs, ws, ep, sk);
+  if (ep.P == 14 && ep.C == 3 && 14 * (14 * ep.maxpw + 1) * sizeof(float) <= 64 * 1024)
+    hipLaunchKernelGGL(k_tile_epilogue_p<14>, dim3(3 * ep.maxph, n_img), dim3(256),
+                       (size_t)14 * (14 * ep.maxpw + 1) * sizeof(float), s, imgs, ws, ep, sk);
+  else
+    hipLaunchKernelGGL(k_tile_epilogue, dim3((max_T + 63) / 64, n_img), dim3(256), 0, s, imgs, ws, ep, sk);
 }
 
 // ---------------------------------------------------------------------------

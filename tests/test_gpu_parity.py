@@ -53,6 +53,10 @@ def _case_images(case):
     if case == "real":
         r = golden("real_inputs.npz")
         return [r[f"img{i}"].astype(np.float32) / 255.0 for i in range(len(r.files))]
+    if case == "fold":
+        # the GEMM DCT's even/odd folding: odd / even sizes without an FFT plan,
+        # FFT rows + GEMM columns (fold of T in place) and GEMM rows + FFT columns
+        return rng.synth_images(41, [(511, 512), (512, 511), (333, 517), (15, 17), (14, 14), (29, 1024), (448, 449)])
     c = META[case]
     return rng.synth_images(c["seed"], [tuple(s) for s in c["sizes"]], c["first"])
 
@@ -115,7 +119,7 @@ def _oracle_tokens(x_np):
     return ref_cpu.patch_scores(y[:, :ph, :pw], CFG)
 
 
-@pytest.mark.parametrize("case", ["sq224", "ragged", "real"])
+@pytest.mark.parametrize("case", ["sq224", "ragged", "real", "fold"])
 def test_preprocess_tokens_and_order(fe, case):
     for x_np in _case_images(case):
         out = fe.preprocess(torch.from_numpy(x_np).to(DEV))
@@ -497,3 +501,22 @@ def test_fft_decode_patches_roundtrip_512(fe):
     ok, dmax = _rgb_close(img.cpu(), ref, atol=1e-5, rtol=1e-5)
     assert ok, dmax
 
+
+
+@pytest.mark.parametrize("cbd", [7, 4, 2, 1])
+def test_lfq_groupings_regroup_the_same_bits(pkg, fe, pn, lfq, cbd):
+    """Any LFQ grouping with codebook_dim * num_codebooks = 196 (lfq.py:168)
+    quantises the same sign bits; its codes are the 14 x 14 codes' bits
+    (row-major, MSB first) cut into codebook_dim-bit groups.  Covers the FFT
+    (512, 224) and GEMM (odd / unplanned) paths."""
+    shapes = [(512, 512), (224, 224), (333, 517), (100, 300)]
+    x = [torch.from_numpy(a).to(DEV) for a in rng.synth_images(53, shapes)]
+    other = pkg.LFQ(dim=196, codebook_size=2 ** cbd, num_codebooks=196 // cbd).to(DEV).eval()
+    ((dp_a, c_a),) = fe.encode_batch(x, pn, lfq)
+    ((dp_b, c_b),) = fe.encode_batch(x, pn, other)
+    assert torch.equal(dp_a.patch_positions, dp_b.patch_positions)
+    w14 = 2 ** torch.arange(13, -1, -1, device=DEV)
+    bits = ((c_a[..., None] & w14) != 0).reshape(*c_a.shape[:-1], 196)
+    wb = 2 ** torch.arange(cbd - 1, -1, -1, device=DEV)
+    want = (bits.reshape(*c_a.shape[:-1], 196 // cbd, cbd).long() * wb).sum(-1)
+    assert torch.equal(c_b.long(), want)
