@@ -134,8 +134,13 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
         for (int p = 0; p < KS / 2; ++p) {
           float v0, v1;
           if (a.use_codes) {
-            v0 = ((code[r] >> (KS - 1 - 2 * p)) & 1) ? vt[r][2 * p].x : vt[r][2 * p].y;
-            v1 = ((code[r] >> (KS - 2 - 2 * p)) & 1) ? vt[r][2 * p + 1].x : vt[r][2 * p + 1].y;
+            // bit select by masks: a ?: on the pair lets the compiler select
+            // the address instead and move vt to scratch
+            const uint32_t m0 = 0u - ((uint32_t)(code[r] >> (KS - 1 - 2 * p)) & 1u);
+            const uint32_t m1 = 0u - ((uint32_t)(code[r] >> (KS - 2 - 2 * p)) & 1u);
+            v0 = __uint_as_float((__float_as_uint(vt[r][2 * p].x) & m0) | (__float_as_uint(vt[r][2 * p].y) & ~m0));
+            v1 = __uint_as_float((__float_as_uint(vt[r][2 * p + 1].x) & m1) |
+                                 (__float_as_uint(vt[r][2 * p + 1].y) & ~m1));
           } else {
             v0 = pv[r][2 * p];
             v1 = pv[r][2 * p + 1];
