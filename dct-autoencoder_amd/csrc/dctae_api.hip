@@ -1588,14 +1588,11 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
   const int n_img = (int)D.size();
   const int S = cfg->max_seq_len, P = cfg->patch_size;
   int64_t wsf = 0;
-  std::vector<int4> cb;
   std::vector<int2> rb;
   for (int i = 0; i < n_img; ++i) {
     ImgDesc& d = D[i];
     d.ws_t = wsf;
     wsf += (3ll * d.H * d.Kw + 63) & ~63ll;
-    for (int c = 0; c < 3; ++c)
-      for (int w = 0; w < d.qw; ++w) cb.push_back(make_int4(i, c, w, 0));
     for (int y0 = 0; y0 < d.H; y0 += 16) rb.push_back(make_int2(i, y0));
   }
   const int64_t map_off = wsf;
@@ -1605,7 +1602,6 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
   if ((rc = ensure_ws(ctx, (size_t)wsf * 4, 256))) return rc;
   PlanBuf pb;
   const size_t d_off = pb.add(D.data(), D.size());
-  const size_t cb_off = pb.add(cb.data(), cb.size());
   const size_t rb_off = pb.add(rb.data(), rb.size());
   const size_t lut_off = pb.add(img_lut, (size_t)n_rows * lut_w);
   order_after_previous(ctx, s);

@@ -53,6 +53,50 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 __device__ __forceinline__ int lswz(int row, int kseg) { return row * LBK + ((kseg ^ ((row >> 1) & 7)) << 3); }
 
+// epilogue of a wave's 64 x 64 block at (mb, nb): acc[i][j][v] = C[row =
+// 8 (v / 4) + 4 (lane / 32) + v % 4][col = lane % 32] of 32 x 32 block (i, j)
+template <int EPI>
+__device__ __forceinline__ void lin_epilogue(const LinearArgs& a, const f32x16 (&acc)[2][2], int64_t mb, int nb, int fr,
+                                             int fh) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = nb + j * 32 + fr;
+    if (n >= a.N) continue;
+    const float bias = a.bias ? a.bias[n] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int64_t m = mb + i * 32 + 8 * (v >> 2) + 4 * fh + (v & 3);
+        if (m >= a.M) continue;
+        float y = acc[i][j][v] + bias;
+        if (EPI == LIN_F32) {
+          reinterpret_cast<float*>(a.out)[m * a.ldo + n] = y;
+        } else if (EPI == LIN_BF16) {
+          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
+        } else if (EPI == LIN_BF16_QGELU) {
+          y = y / (1.0f + __expf(-1.702f * y));   // quick_gelu: x * sigmoid(1.702 x)
+          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
+        } else {   // LIN_F32_RESIDUAL
+          float* o = reinterpret_cast<float*>(a.out) + m * a.ldo + n;
+          *o = *o + y;
+        }
+      }
+  }
+}
+
+// tile id -> (M tile, N tile), grouped raster: runs of LGM M tiles per N tile
+// column, so the ~64 tiles an XCD holds at once cover about 8 x 8 tiles and
+// their A rows and W rows (a few MB) stay in that XCD's L2 (a row-major order
+// streams all of W through L2 for every M row: 40 % L2 hit rate measured)
+constexpr int LGM = 8;
+__device__ __forceinline__ void lin_tile(int t, int ntm, int ntn, int& tm, int& tn) {
+  const int per = LGM * ntn, g = t / per, r = t - g * per;
+  const int first = g * LGM, gm = min(ntm - first, LGM);
+  tm = first + r % gm;
+  tn = r / gm;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t L[2 * (LBM + LBN) * LBK];   // [buf][A 128 rows | W 128 rows][64]
@@ -63,9 +107,11 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
   // their A rows through its L2 (A is then read from HBM once, not once per XCD)
   const int nwg = gridDim.x, xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
-  const int ntn = (a.N + LBN - 1) / LBN;
-  const int64_t m0 = (int64_t)(wgid / ntn) * LBM;
-  const int n0 = (wgid % ntn) * LBN;
+  const int ntn = (a.N + LBN - 1) / LBN, ntm = (int)((a.M + LBM - 1) / LBM);
+  int tm, tn;
+  lin_tile(wgid, ntm, ntn, tm, tn);
+  const int64_t m0 = (int64_t)tm * LBM;
+  const int n0 = tn * LBN;
   // this lane's glds sources: wave-instruction j covers rows 8 (4 wave + j) + lane / 8, slot lane % 8
   const uint16_t* srcA[4];
   const uint16_t* srcW[4];
@@ -118,32 +164,7 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile kt + 1 landed
     __syncthreads();                                    // ... for every wave; tile kt's buffer free
   }
-  // epilogue: acc[i][j][v] = C[row = 8 (v / 4) + 4 (lane / 32) + v % 4][col = lane % 32] of block (i, j)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + j * 32 + fr;
-    if (n >= a.N) continue;
-    const float bias = a.bias ? a.bias[n] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int64_t m = m0 + wm * 64 + i * 32 + 8 * (v >> 2) + 4 * fh + (v & 3);
-        if (m >= a.M) continue;
-        float y = acc[i][j][v] + bias;
-        if (EPI == LIN_F32) {
-          reinterpret_cast<float*>(a.out)[m * a.ldo + n] = y;
-        } else if (EPI == LIN_BF16) {
-          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
-        } else if (EPI == LIN_BF16_QGELU) {
-          y = y / (1.0f + __expf(-1.702f * y));   // quick_gelu: x * sigmoid(1.702 x)
-          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
-        } else {   // LIN_F32_RESIDUAL
-          float* o = reinterpret_cast<float*>(a.out) + m * a.ldo + n;
-          *o = *o + y;
-        }
-      }
-  }
+  lin_epilogue<EPI>(a, acc, m0 + wm * 64, n0 + wn * 64, fr, fh);
 }
 
 void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
