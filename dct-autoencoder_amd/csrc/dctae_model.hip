@@ -190,11 +190,15 @@ void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
 //   the lane already holds, so P needs no shuffle; V^T is read with the same
 //   key order (two 8-byte LDS reads per fragment).
 // ---------------------------------------------------------------------------
-constexpr int AQ = 128, AK = 64, AD = 64, ASTR = 72;
+// LDS row strides (bf16): K / O rows 72 (ds_read_b128 fragment reads: rows r
+// land on 16-byte slots 9 r mod 16, conflict-free); V rows 96 (the transposed
+// ds_read_b64_tr_b16 reads: rows kb + q at banks 48 q mod 64 plus the 8-bank
+// column groups tile the 64 banks; at 72 they were 2-way)
+constexpr int AQ = 128, AK = 64, AD = 64, ASTR = 72, AVS = 96;
 
 __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AK * ASTR];
-  __shared__ __attribute__((aligned(16))) uint16_t Vs[AK * ASTR];   // row-major; read transposed (ds_read_b64_tr_b16)
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[AK * AVS];   // row-major; read transposed (ds_read_b64_tr_b16)
   __shared__ __attribute__((aligned(16))) int32_t kid[AK];   // key image id, or -1 for a non-pad key (no bias)
   __shared__ __attribute__((aligned(16))) uint16_t Os[AQ * ASTR];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
       const uint4 kv = *reinterpret_cast<const uint4*>(src + D);
       const uint4 vv = *reinterpret_cast<const uint4*>(src + 2 * D);
       *reinterpret_cast<uint4*>(Ks + key * ASTR + seg * 8) = kv;
-      *reinterpret_cast<uint4*>(Vs + key * ASTR + seg * 8) = vv;
+      *reinterpret_cast<uint4*>(Vs + key * AVS + seg * 8) = vv;
     }
     bool pad = false;
     if (tid < AK) {
@@ -315,9 +319,9 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int kb = 32 * (kk >> 1) + 8 * (2 * (kk & 1)) + 4 * (lane >> 5);
-        const uint16_t* vr = Vs + (kb + gq) * ASTR + 32 * dt + 16 * gx + 4 * gp;
+        const uint16_t* vr = Vs + (kb + gq) * AVS + 32 * dt + 16 * gx + 4 * gp;
         const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)vr);
-        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vr + 8 * ASTR));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(vr + 8 * AVS));
         bf16x8 vf;
         short* vsh = reinterpret_cast<short*>(&vf);
 #pragma unroll
