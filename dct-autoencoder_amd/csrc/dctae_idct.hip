@@ -85,6 +85,15 @@ void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int
 //   3. complex z (zaddr layout, as the encode's cols5) -> radix-16 x 2 FFT;
 //   4. z[m] -> x[y] (natural rows) -> U[c][y][14 strip + col] (56-byte rows).
 // ---------------------------------------------------------------------------
+// X row y lives at row xrow(y) = y ^ ((y >> 4) & 3): the FFT output scatter
+// (rows 4 m, 4 m + 2 for m = jj + 16 r over the 16 lanes jj of a column)
+// then hits 16 distinct bank pairs instead of 4 (4-way -> conflict-free; the
+// other X accesses stay within 2-way: 305 vs 672 extra LDS cycles per item by
+// the bank rule of MI355X_MICROARCH.md, SQ_LDS_BANK_CONFLICT 91.5 M per launch
+// before; the kernel time did not move: it is latency-bound).  Rows
+// 448 .. 511 map onto themselves (the zero fill is unchanged).
+__device__ __forceinline__ int xrow(int y) { return y ^ ((y >> 4) & 3); }
+
 struct IColsLds {
   union {
     float x[512 * 14];
@@ -129,7 +138,7 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
     for (int r = 0; r < 2; ++r) {
       const int h = g16 + 16 * r;
       if (jl < KS) {
-        f2v* xr = reinterpret_cast<f2v*>(L.x + (KS * h + jl) * KS);
+        f2v* xr = reinterpret_cast<f2v*>(L.x + xrow(KS * h + jl) * KS);
 #pragma unroll
         for (int p = 0; p < KS / 2; ++p) {
           float v0, v1;
@@ -162,10 +171,10 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int k = jj + 16 * i;
-      float yk = xc[k * KS];
-      const float ynk = k == 0 ? 0.0f : xc[(N - k) * KS];
+      float yk = xc[xrow(k) * KS];
+      const float ynk = k == 0 ? 0.0f : xc[xrow(N - k) * KS];
       if (k == 0) yk *= 1.41421356237309515f;
-      const float ymk = xc[(M + k) * KS], ymk2 = xc[(M - k) * KS];
+      const float ymk = xc[xrow(M + k) * KS], ymk2 = xc[xrow(M - k) * KS];
       zk[i] = pre_z(yk, ynk, ymk, ymk2, pre_s[k]);
     }
   }
@@ -213,8 +222,8 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
         const int m = jj + 16 * r;
         const int ya = m < M / 2 ? 4 * m : 2 * N - 1 - 4 * m;
         const int yb = m < M / 2 ? ya + 2 : ya - 2;
-        L.x[ya * KS + col] = v[r].x;
-        L.x[yb * KS + col] = -v[r].y;
+        L.x[xrow(ya) * KS + col] = v[r].x;
+        L.x[xrow(yb) * KS + col] = -v[r].y;
       }
     }
     __syncthreads();
@@ -224,9 +233,9 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
     const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
     f2v* dst = reinterpret_cast<f2v*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
     const int64_t rstep = (int64_t)16 * d.Kw;
-    const f2v* src = reinterpret_cast<const f2v*>(L.x + y0 * KS) + p;
+    const f2v* src = reinterpret_cast<const f2v*>(L.x) + p;
 #pragma unroll
-    for (int k = 0; k < N / 32; ++k) dst[k * rstep] = src[k * 16 * KS];
+    for (int k = 0; k < N / 32; ++k) dst[k * rstep] = src[xrow(y0 + 32 * k) * (KS / 2)];
   }
   __syncthreads();
 }
