@@ -255,9 +255,14 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
         st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], st[t], 0, 0, 0);
       }
     }
-    // scale + bias, block max over the 64 keys of this query (lanes l and l ^ 32)
+    // scale + bias, block max over the 64 keys of this query (lanes l and l ^ 32).
+    // Without pad keys in the block the logits stay unscaled (sce = sc) and the
+    // scale is applied inside the exponent's FMA; with pad keys they are scaled
+    // and biased here (sce = 1).
     float bm = -INFINITY;
+    float sce = sc;
     if (any_pad) {
+      sce = 1.0f;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -268,11 +273,6 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
           st[t][4 * q4 + 2] = st[t][4 * q4 + 2] * sc + (ki.z == my_id ? bias2 : 0.0f);
           st[t][4 * q4 + 3] = st[t][4 * q4 + 3] * sc + (ki.w == my_id ? bias2 : 0.0f);
         }
-    } else {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) st[t][v] *= sc;
     }
     if (k0 + AK > S) {   // last, partial key block
 #pragma unroll
@@ -287,28 +287,39 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
       for (int v = 0; v < 16; ++v) bm = fmaxf(bm, st[t][v]);
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(bm), __float_as_uint(bm), false, false);
-      bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      bm = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1])) * sce;
     }
-    const float mnew = fmaxf(mrun, bm);
-    const float alpha = exp2f(mrun - mnew);
-    mrun = mnew;
-    lsum *= alpha;
+    // lazy rescale: the reference max moves only when the block max exceeds it
+    // by more than 8 (log2 units), so p = 2^(s - m) <= 2^8 stays exact in fp32
+    // and in range for bf16; O and the sum always share the same m, so the
+    // normalised result is unchanged.  The O rescale (AGPR round trip) runs
+    // only when some lane moved its max.
+    if (bm > mrun + 8.0f) {
+      const float alpha = __builtin_amdgcn_exp2f(mrun - bm);   // 0 on the first block (mrun = -inf)
+      mrun = bm;
+      lsum *= alpha;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+        for (int v = 0; v < 16; ++v) o[t][v] *= alpha;
+    }
+    const float nm = -mrun;
     // P (bf16) in B-operand order: key step kk = (tile kk / 2, quarters 2 (kk % 2), +1)
     bf16x8 pf[4];
+    float ls2[2] = {0.0f, 0.0f};   // two partial sums (pairs for packed adds)
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int t = kk >> 1, v0 = 8 * (kk & 1);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float p = exp2f(st[t][v0 + e] - mnew);
-        lsum += p;
+        // raw v_exp_f32: exp2f's denormal-range fix-up (5 VALU ops per call)
+        // is not needed (results below 2^-126 are negligible probabilities)
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(st[t][v0 + e], sce, nm));
+        ls2[e & 1] += p;
         pf[kk][e] = (__bf16)p;
       }
     }
+    lsum += ls2[0] + ls2[1];
     // O^T += V^T P^T; the A fragment V^T[d = 32 dt + lane % 32][keys kb + (0..3), kb + 8 + (0..3)] comes
     // from the row-major V tile by two transposed reads: lane 4q + p of each 16-lane group addresses key
     // row kb + q, columns 4p .. 4p + 3 of the group's 16 d columns, and receives its own column
