@@ -35,7 +35,7 @@ def _bits(x):
 
 
 @pytest.mark.parametrize("epi", [0, 1, 2, 3])
-@pytest.mark.parametrize("m,n,k", [(300, 200, 192), (256, 384, 1024), (77, 52, 128), (2304, 200, 192), (3000, 384, 64)])
+@pytest.mark.parametrize("m,n,k", [(300, 200, 192), (256, 384, 1024), (77, 52, 128), (2304, 200, 192), (3000, 384, 64), (4100, 3900, 128)])
 def test_linear_epilogues(pkg, epi, m, n, k):
     L = _lib(pkg)
     ctx = L.context(DEV)
