@@ -73,10 +73,12 @@ __device__ __forceinline__ void lin_epilogue(const LinearArgs& a, const f32x16 (
         if (EPI == LIN_F32) {
           reinterpret_cast<float*>(a.out)[m * a.ldo + n] = y;
         } else if (EPI == LIN_BF16) {
-          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
+          reinterpret_cast<__bf16*>(a.out)[m * a.ldo + n] = (__bf16)y;   // v_cvt_pk_bf16_f32 (RNE)
         } else if (EPI == LIN_BF16_QGELU) {
-          y = y / (1.0f + __expf(-1.702f * y));   // quick_gelu: x * sigmoid(1.702 x)
-          reinterpret_cast<uint16_t*>(a.out)[m * a.ldo + n] = f2bf(y);
+          // quick_gelu x * sigmoid(1.702 x) with the hardware exp2 / reciprocal
+          // (~1 ulp each; the result is rounded to bf16 right after)
+          y = y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.45546696228f * y));   // 1.702 log2(e)
+          reinterpret_cast<__bf16*>(a.out)[m * a.ldo + n] = (__bf16)y;
         } else {   // LIN_F32_RESIDUAL
           float* o = reinterpret_cast<float*>(a.out) + m * a.ldo + n;
           *o = *o + y;
