@@ -164,7 +164,62 @@ __global__ __launch_bounds__(256) void k_linear(LinearArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile kt + 1 landed
     __syncthreads();                                    // ... for every wave; tile kt's buffer free
   }
-  lin_epilogue<EPI>(a, acc, m0 + wm * 64, n0 + wn * 64, fr, fh);
+  // vectorised epilogue: each wave's 64 x 64 block goes through LDS (the last
+  // loop barrier freed the operand buffers) and leaves as 16-byte row
+  // segments (the accumulator layout alone gives 32 x 2- or 4-byte columns)
+  constexpr int VEC = (EPI == LIN_BF16 || EPI == LIN_BF16_QGELU) ? 8 : 4;   // elements per 16 bytes
+  const bool vec_ok = n0 + LBN <= a.N && a.ldo % VEC == 0 && (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+  if (!vec_ok) {
+    lin_epilogue<EPI>(a, acc, m0 + wm * 64, n0 + wn * 64, fr, fh);
+    return;
+  }
+  float* Cs = reinterpret_cast<float*>(L) + wave * 64 * 64;   // [64 rows][64 cols], 4 x 16 KB = the 64 KB of L
+  const int64_t mb = m0 + wm * 64;
+  const int nb = n0 + wn * 64;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float bias = a.bias ? a.bias[nb + j * 32 + fr] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        float y = acc[i][j][v] + bias;
+        if (EPI == LIN_BF16_QGELU)
+          y = y * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.45546696228f * y));   // quick_gelu
+        Cs[(i * 32 + 8 * (v >> 2) + 4 * fh + (v & 3)) * 64 + j * 32 + fr] = y;   // 32 lanes: one row, 32 banks
+      }
+  }
+  if (VEC == 8) {   // bf16: 8 lanes per 128-byte row, 8 rows per pass
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int r = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+      const float4 lo = *reinterpret_cast<const float4*>(Cs + r * 64 + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(Cs + r * 64 + c8 + 4);
+      uint4 pk;
+      pk.x = (uint32_t)f2bf(lo.x) | ((uint32_t)f2bf(lo.y) << 16);
+      pk.y = (uint32_t)f2bf(lo.z) | ((uint32_t)f2bf(lo.w) << 16);
+      pk.z = (uint32_t)f2bf(hi.x) | ((uint32_t)f2bf(hi.y) << 16);
+      pk.w = (uint32_t)f2bf(hi.z) | ((uint32_t)f2bf(hi.w) << 16);
+      if (mb + r < a.M) *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(a.out) + (mb + r) * a.ldo + nb + c8) = pk;
+    }
+  } else {   // f32 (plain or residual): 16 lanes per 256-byte row, 4 rows per pass
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+      float4 y = *reinterpret_cast<const float4*>(Cs + r * 64 + c4);
+      if (mb + r < a.M) {
+        float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(a.out) + (mb + r) * a.ldo + nb + c4);
+        if (EPI == LIN_F32_RESIDUAL) {
+          const float4 x = *o;
+          y.x += x.x;
+          y.y += x.y;
+          y.z += x.z;
+          y.w += x.w;
+        }
+        *o = y;
+      }
+    }
+  }
 }
 
 void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
