@@ -897,9 +897,12 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           if (M == 0) continue;
           const float* CW;
           if ((rc = dct_matrix(ctx, d.W, std::min(d.W, rows_cap), &CW, par))) return rc;
-          // B: the folded IPT (k_rgb_to_ipt), u at x < ceil(W/2), v after it
-          GemmProblem g = gemm(CW, 0, K, 1, ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1,
-                               ws + d.ws_t + par, (int64_t)d.Kw * d.H, 2, d.Kw, M, d.H, K, 3);
+          // A: the folded IPT (k_rgb_to_ipt), u at x < ceil(W/2), v after it; B:
+          // the half DCT matrix (shared by the channels).  T rows y are the GEMM
+          // rows, so a wave's stores run along kx (the accumulator's lane-fast
+          // dimension; with the roles swapped they strided by Kw floats)
+          GemmProblem g = gemm(ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1, CW, 0, K, 1,
+                               ws + d.ws_t + par, (int64_t)d.Kw * d.H, d.Kw, 2, d.H, M, K, 3);
           add_tiles(rt, (int)(probs.size() - p0), g);
           probs.push_back(g);
         }
