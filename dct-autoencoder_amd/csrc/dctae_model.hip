@@ -234,7 +234,7 @@ void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// attention (d_head = 64): block = (row b, head h, 128 queries), wave = 32
+// attention (d_head = 64): block = (row b, head h, 256 queries), wave = 32
 // queries.  Per 64-key block: K (64 x 64) and V^T (64 x 64) staged in LDS.
 //   S^T tile t (keys 32 t .., 32 queries) = sum_kk mfma(A = K[keys][d kk],
 //   B = Q^T[d kk][queries]):  lane l holds keys 32 t + 8 (v/4) + 4 (l/32) + v%4
@@ -249,9 +249,9 @@ void launch_linear(const LinearArgs& a, int epi, hipStream_t s) {
 // land on 16-byte slots 9 r mod 16, conflict-free); V rows 96 (the transposed
 // ds_read_b64_tr_b16 reads: rows kb + q at banks 48 q mod 64 plus the 8-bank
 // column groups tile the 64 banks; at 72 they were 2-way)
-constexpr int AQ = 128, AK = 64, AD = 64, ASTR = 72, AVS = 96;
+constexpr int AQ = 256, AK = 64, AD = 64, ASTR = 72, AVS = 96, ATH = 4 * AQ / 2;   // ATH threads: one wave per 32 queries
 
-__global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
+__global__ __launch_bounds__(ATH) void k_attention(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[AK * ASTR];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[AK * AVS];   // row-major; read transposed (ds_read_b64_tr_b16)
   __shared__ __attribute__((aligned(16))) int32_t kid[AK];   // key image id, or -1 for a non-pad key (no bias)
@@ -282,8 +282,8 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
     __syncthreads();   // previous block's K / V reads done
     // stage K and V rows: 64 keys x 64 d, 16 B per load (two per thread each)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int idx = tid + 256 * j, key = idx >> 3, seg = idx & 7;
+    for (int j = 0; j < AK * 8 / ATH; ++j) {
+      const int idx = tid + ATH * j, key = idx >> 3, seg = idx & 7;
       const int kg = min(k0 + key, S - 1);
       const uint16_t* src = qkv + (rowbase + kg) * ld + h * AD + seg * 8;
       const uint4 kv = *reinterpret_cast<const uint4*>(src + D);
@@ -415,8 +415,8 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
     }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int idx = tid + 256 * j, r = idx >> 3, seg = idx & 7;
+  for (int j = 0; j < AQ * 8 / ATH; ++j) {
+    const int idx = tid + ATH * j, r = idx >> 3, seg = idx & 7;
     if (q0 + r < S)
       *reinterpret_cast<uint4*>(a.out + (rowbase + q0 + r) * (int64_t)a.ldo + h * AD + seg * 8) =
           *reinterpret_cast<const uint4*>(Os + r * ASTR + seg * 8);
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256) void k_attention(AttnArgs a) {
 
 void launch_attention(const AttnArgs& a, hipStream_t s) {
   if (a.R <= 0 || a.S <= 0) return;
-  hipLaunchKernelGGL(k_attention, dim3((a.S + AQ - 1) / AQ, a.heads, a.R), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_attention, dim3((a.S + AQ - 1) / AQ, a.heads, a.R), dim3(ATH), 0, s, a);
 }
 
 // ---------------------------------------------------------------------------
