@@ -488,9 +488,66 @@ __global__ __launch_bounds__(256) void k_layernorm(LnArgs a) {
   }
 }
 
+// LayerNorm -> bf16 for D % 256 == 0 with 16-byte row accesses: lane l holds
+// columns 4 (l + 64 i) .. +3 (float4 loads, 8-byte bf16x4 stores; the scalar
+// kernel moves 2 bytes per lane per store)
+template <int P4>
+__global__ __launch_bounds__(256) void k_layernorm_v(LnArgs a) {
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int lane = threadIdx.x & 63;
+  const float4* x4 = reinterpret_cast<const float4*>(a.x + m * a.ldx);
+  float4 v[P4];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < P4; ++i) {
+    v[i] = x4[lane + 64 * i];
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)a.D;
+  float q = 0.0f;
+#pragma unroll
+  for (int i = 0; i < P4; ++i) {
+    const float d0 = v[i].x - mean, d1 = v[i].y - mean, d2 = v[i].z - mean, d3 = v[i].w - mean;
+    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / (float)a.D + a.eps);
+  const float4* g4 = reinterpret_cast<const float4*>(a.gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(a.beta);
+  uint2* o2 = reinterpret_cast<uint2*>(a.out_bf16 + m * a.ldo);
+#pragma unroll
+  for (int i = 0; i < P4; ++i) {
+    const int c4 = lane + 64 * i;
+    const float4 g = g4[c4], b = b4[c4];
+    uint2 pk;
+    pk.x = (uint32_t)f2bf((v[i].x - mean) * rstd * g.x + b.x) | ((uint32_t)f2bf((v[i].y - mean) * rstd * g.y + b.y) << 16);
+    pk.y = (uint32_t)f2bf((v[i].z - mean) * rstd * g.z + b.z) | ((uint32_t)f2bf((v[i].w - mean) * rstd * g.w + b.w) << 16);
+    o2[c4] = pk;
+  }
+}
+
 void launch_layernorm(const LnArgs& a, hipStream_t s) {
   if (a.M <= 0) return;
   const unsigned grid = (unsigned)((a.M + 3) / 4);
+  const bool vec = !a.out_f32 && a.D % 256 == 0 && a.D <= 4096 && a.ldx % 4 == 0 && a.ldo % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(a.x) | reinterpret_cast<uintptr_t>(a.gamma) |
+                     reinterpret_cast<uintptr_t>(a.beta)) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.out_bf16) & 7) == 0;
+  if (vec) {
+    const int p4 = a.D / 256;
+    if (p4 == 1) hipLaunchKernelGGL(k_layernorm_v<1>, dim3(grid), dim3(256), 0, s, a);
+    else if (p4 == 2) hipLaunchKernelGGL(k_layernorm_v<2>, dim3(grid), dim3(256), 0, s, a);
+    else if (p4 == 4) hipLaunchKernelGGL(k_layernorm_v<4>, dim3(grid), dim3(256), 0, s, a);
+    else if (p4 == 8) hipLaunchKernelGGL(k_layernorm_v<8>, dim3(grid), dim3(256), 0, s, a);
+    else if (p4 == 16) hipLaunchKernelGGL(k_layernorm_v<16>, dim3(grid), dim3(256), 0, s, a);
+    else goto scalar;
+    return;
+  }
+scalar:
   const int per = (a.D + 63) / 64;
   if (per <= 2) hipLaunchKernelGGL(k_layernorm<2>, dim3(grid), dim3(256), 0, s, a);
   else if (per <= 4) hipLaunchKernelGGL(k_layernorm<4>, dim3(grid), dim3(256), 0, s, a);
