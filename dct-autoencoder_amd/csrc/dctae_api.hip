@@ -59,6 +59,9 @@ struct dctae_ctx {
   bool fft_enabled = true;
   bool fft_spec_enabled = true;
   int rows_prefetch = 0;
+  int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
+  int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)
+  int rows_kernel = 3;                // 512-wide rows: 3 = k_rows512 (registers + one LDS transpose), 2 = k_fft_rows2
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16),
                                       // 3 row-major with each tile column padded to 16 floats (64-B segments)
@@ -624,6 +627,9 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6 || value == 7)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "fused") ctx->fused = value != 0;
+  else if (k == "t_alias" && value >= 0) ctx->t_alias = (int)value;
+  else if (k == "rows_ablate" && value >= 0 && value <= 3) ctx->rows_ablate = (int)value;
+  else if (k == "rows_kernel" && (value == 2 || value == 3)) ctx->rows_kernel = (int)value;
   else if (k == "dual_stream") ctx->dual_stream = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
@@ -841,6 +847,15 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     auto up = [](int64_t v) { return (v + 63) & ~63ll; };  // 256-byte aligned regions (float4 strip loads)
     for (int i = j.i0; i < j.i1; ++i) {
       ImgDesc& d = D[i];
+      if (ctx->t_alias > 0 && i - j.i0 >= ctx->t_alias) {   // profiling: T slots shared (wrong output)
+        d.ws_t = D[j.i0 + (i - j.i0) % ctx->t_alias].ws_t;
+        d.ws_p = d.ws_y = wsf;
+        d.tok_off = full ? tok : tok_off_user[i];
+        tok += d.T;
+        j.max_T = std::max(j.max_T, d.T);
+        j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
+        continue;
+      }
       d.ws_t = wsf;
       wsf += up(3ll * (d.t_strips >= 2 ? (d.Kw / 14) * 16 : d.Kw) * d.H);
       d.ws_p = wsf;
@@ -1038,7 +1053,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
-                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout +
+                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout + 64 * ctx->t_alias +
                              1024 * ctx->xcd_order + 4096 * ctx->fused + 8192 * ctx->fused_slots +
                              (1 << 20) * ctx->cols_kernel + (1 << 24) * ctx->dual_stream,
                          (int64_t)(intptr_t)ctx->ws});
@@ -1165,9 +1180,13 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fr[v]) {
         Timer t(ctx, st, "fft_rows");
-        launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
-                             ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st,
-                             ctx->rows_prefetch);
+        if (v == 1 && ctx->rows_kernel == 3 && ctx->t_layout == 0 && cfg->max_patch_w >= 32)
+          launch_rows512(dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
+                         ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st, ctx->rows_ablate);
+        else
+          launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
+                               ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st,
+                               ctx->rows_prefetch);
       }
   };
   auto do_cols = [&](const ChunkJob& j, hipStream_t st) {

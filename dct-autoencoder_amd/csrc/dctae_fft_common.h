@@ -298,4 +298,67 @@ struct DFTV<7> {
   static __device__ __forceinline__ void run(cf* v) { dftv_odd<7>(v, kCos7, kSin7); }
 };
 
+// ---------------------------------------------------------------------------
+// Scalar DFT16 on split (re, im) arrays, natural order in and out (4 x 4
+// with internal twiddles W16^(n2 k1); the W16^4 = -i twiddle is a rename).
+// No packed pairs: the caller's inputs can come from any registers without
+// the moves a (re, im) register pair needs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void dft4s(float& r0, float& i0, float& r1, float& i1, float& r2, float& i2, float& r3,
+                                      float& i3) {
+  const float t0r = r0 + r2, t0i = i0 + i2, t1r = r0 - r2, t1i = i0 - i2;
+  const float t2r = r1 + r3, t2i = i1 + i3, t3r = r1 - r3, t3i = i1 - i3;
+  r0 = t0r + t2r;
+  i0 = t0i + t2i;
+  r2 = t0r - t2r;
+  i2 = t0i - t2i;
+  r1 = t1r + t3i;   // t1 + (-i) t3
+  i1 = t1i - t3r;
+  r3 = t1r - t3i;
+  i3 = t1i + t3r;
+}
+
+__device__ __forceinline__ void dft16s(float (&re)[16], float (&im)[16]) {
+#pragma clang fp contract(fast)
+  float ar[4][4], ai[4][4];   // [n2][k1]
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+    float x0r = re[n2], x0i = im[n2], x1r = re[4 + n2], x1i = im[4 + n2];
+    float x2r = re[8 + n2], x2i = im[8 + n2], x3r = re[12 + n2], x3i = im[12 + n2];
+    dft4s(x0r, x0i, x1r, x1i, x2r, x2i, x3r, x3i);
+    ar[n2][0] = x0r, ai[n2][0] = x0i, ar[n2][1] = x1r, ai[n2][1] = x1i;
+    ar[n2][2] = x2r, ai[n2][2] = x2i, ar[n2][3] = x3r, ai[n2][3] = x3i;
+  }
+  constexpr float c = 7.071067812e-01f;
+#pragma unroll
+  for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; ++k1) {
+      const int m = n2 * k1;
+      const float a = ar[n2][k1], b = ai[n2][k1];
+      if (m == 4) {          // -i
+        ar[n2][k1] = b;
+        ai[n2][k1] = -a;
+      } else if (m == 2) {   // (1 - i) / sqrt2
+        ar[n2][k1] = c * (a + b);
+        ai[n2][k1] = c * (b - a);
+      } else if (m == 6) {   // (-1 - i) / sqrt2
+        ar[n2][k1] = c * (b - a);
+        ai[n2][k1] = -c * (a + b);
+      } else {
+        const float wr = kCos16[m], wi = -kSin16[m];
+        ar[n2][k1] = a * wr - b * wi;
+        ai[n2][k1] = a * wi + b * wr;
+      }
+    }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    float x0r = ar[0][k1], x0i = ai[0][k1], x1r = ar[1][k1], x1i = ai[1][k1];
+    float x2r = ar[2][k1], x2i = ai[2][k1], x3r = ar[3][k1], x3i = ai[3][k1];
+    dft4s(x0r, x0i, x1r, x1i, x2r, x2i, x3r, x3i);
+    re[k1] = x0r, im[k1] = x0i, re[k1 + 4] = x1r, im[k1 + 4] = x1i;
+    re[k1 + 8] = x2r, im[k1 + 8] = x2i, re[k1 + 12] = x3r, im[k1 + 12] = x3i;
+  }
+}
+
 }  // namespace dctae

@@ -73,6 +73,9 @@ void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, cons
 void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,
                            float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 
+void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
+                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate = 0);
+
 int fused_rows_per_item();
 int cols7_grid(int n_list, int qw, int ipb);
 void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,
