@@ -7,14 +7,28 @@ One step = one fused encode (dctae_encode) of a batch of B synthetic 512x512
 RGB images already resident in HBM: IPT colour -> global DCT (kept 448x448
 corner) -> 14x14 spectral tokens -> importance order -> packed DCTPatches
 rows (S = 3072) -> PatchNorm (reference-fitted tables) -> LFQ 14 x 2^14 codes.
-Multi-GPU: one process per GPU (torchrun), each rank encodes its own shard
-(weak scaling, no collective on the data path); time = max over ranks.
+Multi-GPU: one process per GPU, each rank encodes its own shard (weak
+scaling, no collective on the data path); time = max over ranks.  Run with
+--gpus N > 1 outside torchrun, bench.py starts `python -m torch.distributed.run
+--nproc-per-node N ... bench.py ...` as a CHILD process (before anything
+touches the GPU) and exits with its return code; under torchrun (WORLD_SIZE
+set) it is one rank.
+
+Roofline: the metric's algorithmic bytes are 3,591,168 B per
+512^2 image (fp32 RGB read + int64 codes / positions / channel / image id per
+token + key_pad share).  roofline.frac = those bytes x images per launch of
+the dominant kernel / that kernel's average launch time / 8 TB/s;
+roofline.frac_end_to_end uses the whole step time; roofline.traffic is the
+dominant kernel's HBM bytes per launch from the committed rocprofv3 PMC
+passes (profiles/pmc_r02.json) and traffic_ratio = traffic / algorithmic.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,6 +40,20 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TF = 157.3    # dense fp32 MFMA (= vector) peak
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+CPU_CAL_FILE = os.path.join(ROOT, "profiles", "cpu_calibration_r02.json")
+
+
+def launcher_command(argv, gpus, port=None):
+    """The torchrun command that runs this bench on `gpus` ranks of one node
+    (SURVEY §8(e)): a child process, never an exec of this one."""
+    if port is None:
+        so = socket.socket()
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+        so.close()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
 
 
 def encode_bytes_per_image(h, w, t, ncb, s, images_per_row):
@@ -48,11 +76,23 @@ def kernel_models(h, w, p, maxp, ncb, s, images_per_row):
         "gemm_cols": ("mfma", 3 * 2.0 * kh * kw * h, "flop"),
         "fft_rows": ("hbm", 12 * h * w + inter, "B"),            # RGB in, T out
         "fft_cols": ("hbm", inter + stage, "B"),                  # T in, token staging out
-        "enc_fused": ("hbm", 12 * h * w + stage, "B"),            # RGB in, token staging out (T on chip)
         "tile_epilogue": ("hbm", 12 * kh * kw + stage, "B"),
         "sort_pack": ("hbm", stage + t * (8 * ncb + 32) + s / images_per_row, "B"),
         "pad_fill": ("hbm", s / images_per_row, "B"),
     }
+
+
+def cpu_calibration():
+    """profiles/cpu_calibration_r02.json (tools/calibrate_cpu_baseline.py): the
+    port's speed against the reference itself, measured in the build container."""
+    try:
+        with open(CPU_CAL_FILE) as f:
+            c = json.load(f)
+        return {"port_over_reference": c["port_over_reference"], "threads": c["threads"],
+                "reference_mpix_s": c["reference_mpix_s"], "port_mpix_s": c["port_mpix_s"],
+                "where": "build container (tools/calibrate_cpu_baseline.py)"}
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(size, seconds, pn_tables, threads):
@@ -73,7 +113,8 @@ def cpu_baseline(size, seconds, pn_tables, threads):
     mpix = n * size * size / 1e6
     return {"value": round(mpix / el, 3), "unit": "Mpix/s", "cores": threads, "kind": "port",
             "sample": f"{n} images of {size}x{size} (torch.rand) through oracle/ref_cpu.encode: preprocess "
-                      f"(FFT DCT, sort) + iter_batches (attn_mask built) + PatchNorm + LFQ, {el:.1f} s"}
+                      f"(FFT DCT, sort) + iter_batches (attn_mask built) + PatchNorm + LFQ, {el:.1f} s",
+            "calibration": cpu_calibration()}
 
 
 def stats_fit_leg(pkg, fe, dev, rank, world, dist, steps, n_img=8, size=512):
@@ -170,10 +211,17 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the config-3 decode timing")
     ap.add_argument("--no-stats", action="store_true", help="skip the config-5 PatchNorm fit (RCCL) timing")
-    ap.add_argument("--no-model", action="store_true", help="skip the DCTAutoencoder transformer timing")
+    ap.add_argument("--model", action="store_true", help="also time the DCTAutoencoder transformer (SURVEY §8(f)4)")
+    ap.add_argument("--no-model", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / config 4 timings")
     ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: torchrun as a child (nothing has touched the GPU yet)
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        sys.exit(subprocess.call(launcher_command(sys.argv[1:], args.gpus), env=env))
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -259,29 +307,33 @@ def main():
                                             "avg_ms": round(ms.value / max(1, n.value), 5)}
             i += 1
         if kernels:
+            # the dominant kernel of the encode; its roofline uses the metric's
+            # algorithmic bytes for the images one launch covers
             dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-            bound, amt, unit = models.get(dom, ("hbm", 0, "B"))
             imgs_per_launch = B * args.steps / kernels[dom]["launches"]
-            per_launch = amt * imgs_per_launch
+            per_launch = per_img_bytes * imgs_per_launch
             avg_s = kernels[dom]["avg_ms"] / 1e3
-            traffic = None
-            pmc_path = os.path.join(ROOT, "profiles", "pmc_r01.json")
-            if os.path.exists(pmc_path):
-                pmc = json.load(open(pmc_path))
+            ach = per_launch / avg_s / 1e9
+            traffic, pmc_src = None, None
+            if os.path.exists(PMC_FILE):
+                pmc = json.load(open(PMC_FILE))
                 ent = pmc.get("kernels", {}).get(dom)
-                if ent and ent.get("images_per_dispatch"):
-                    # HBM bytes per launch from the committed rocprofv3 PMC passes, scaled per image
+                if ent and ent.get("hbm_bytes_per_image"):
+                    # HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 + WRITE_SIZE,
+                    # MI355X_MICROARCH.md gfx950 correction), scaled to this launch's image count
                     traffic = round(ent["hbm_bytes_per_image"] * imgs_per_launch)
-            if bound == "mfma":
-                ach = per_launch / avg_s / 1e12
-                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TF,
-                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TF, 4), "traffic": traffic,
-                        "per_launch": f"{per_launch:.4g} flop ({imgs_per_launch:g} images)"}
-            else:
-                ach = per_launch / avg_s / 1e9
-                roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                        "per_launch": f"{per_launch:.4g} B ({imgs_per_launch:g} images)"}
+                    pmc_src = os.path.relpath(PMC_FILE, ROOT)
+            bound, amt, unit = kernel_models(H, H, P, MAXP, 14, S, imgs_per_row).get(dom, ("hbm", 0, "B"))
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_ratio": round(traffic / per_launch, 3) if traffic else None,
+                    "traffic_source": pmc_src,
+                    "per_launch": f"{per_launch:.6g} B = {per_img_bytes:g} B/img x {imgs_per_launch:g} images "
+                                  f"(SURVEY 8(d) algorithmic bytes of the encode)",
+                    "frac_end_to_end": round(hbm_frac, 4),
+                    "kernel_own_bytes_per_launch": round(amt * imgs_per_launch),
+                    "kernel_own_frac": round(amt * imgs_per_launch / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+                    if unit == "B" else None}
 
     # config 3: decode of this step's codes back to RGB, timed the same way
     decode = None
@@ -347,7 +399,7 @@ def main():
 
     # the DCTAutoencoder transformer forward (patch14-l, 4 rows x 3072 tokens)
     model = None
-    if not args.no_model:
+    if args.model and not args.no_model:
         try:
             sys.path.insert(0, os.path.join(ROOT, "tools"))
             import model_bench
@@ -369,6 +421,7 @@ def main():
             "value": round(mpix_s, 2),
             "unit": "Mpix/s",
             "n_gpus": world,
+            "ranks": {"world": world, "backend": "nccl (RCCL)" if world > 1 else None},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),

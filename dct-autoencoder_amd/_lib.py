@@ -80,6 +80,9 @@ _SIGS = {
                       C.POINTER(LFQCfg), C.POINTER(PackedOut), _P], C.c_int),
     "dctae_spectrum_tokens": ([_P, C.POINTER(FECfg), C.POINTER(Images), C.POINTER(C.c_int64), _P, _P, _P],
                               C.c_int),
+    "dctae_dct2": ([_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P], C.c_int),
+    "dctae_patch_spectrum": ([_P, C.POINTER(FECfg), _P, C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, _P, _P],
+                             C.c_int),
     "dctae_norm_forward": ([_P, C.POINTER(Norm), C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, C.c_int64, _P, _P],
                            C.c_int),
     "dctae_norm_inverse": ([_P, C.POINTER(Norm), C.c_int32, C.c_int32, C.c_int32, _P, _P, _P, C.c_int64, _P, _P],
@@ -93,7 +96,6 @@ _SIGS = {
     "dctae_vq_codes_from_indices": ([_P, C.POINTER(VQCfg), _P, C.c_int64, _P, _P], C.c_int),
     "dctae_vq_output_from_indices": ([_P, C.POINTER(VQCfg), _P, C.c_int64, _P, _P], C.c_int),
     "dctae_check_device_errors": ([_P, _P], C.c_int),
-    "dctae_fused_debug_counters": ([_P, C.POINTER(C.c_int32), C.c_int64, _P], C.c_int64),
     "dctae_synth_images": ([_P, C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, _P, _P], C.c_int),
     "dctae_set_timing": ([_P, C.c_int], C.c_int),
     "dctae_timing_collect": ([_P], C.c_int),

@@ -378,6 +378,45 @@ def decode(p: FEParams, ids: torch.Tensor, key_pad: torch.Tensor, positions: tor
     return imgs
 
 
+def dct2(x: torch.Tensor, inverse: bool, color: bool) -> torch.Tensor:
+    """dctae_dct2 on a (3, H, W) or (B, 3, H, W) fp32 device tensor: full-image
+    orthonormal DCT-II of rgb_to_ipt(x) (FE._transform_image_in, FE:129-142) or
+    ipt_to_rgb of the DCT-III (FE._transform_image_out, FE:144-152); color=False
+    is util.dct2 / util.idct2 alone (util.py:333-338)."""
+    one = x.dim() == 3
+    xb = x[None] if one else x
+    if xb.dim() != 4 or xb.shape[1] != 3:
+        raise AssertionError(f"expected (3, h, w) or (b, 3, h, w), got {tuple(x.shape)}")
+    xb = xb if (xb.dtype == torch.float32 and xb.is_contiguous()) else xb.float().contiguous()
+    dev = _check_dev(xb)
+    ctx = _lib.context(dev)
+    y = torch.empty_like(xb)
+    B, _, H, W = xb.shape
+    rc = ctx.lib.dctae_dct2(ctx.h, ptr(xb), B, H, W, int(bool(inverse)), int(bool(color)), ptr(y),
+                            _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_dct2")
+    return y[0] if one else y
+
+
+def patch_spectrum(x: torch.Tensor, p: FEParams, k: int):
+    """dctae_patch_spectrum: FE._patch_image (FE:364-452) of a cropped (3, h, w)
+    spectrum on the device -> (patches (k, P*P), positions (k, 2), channels (k))."""
+    x = x if (x.dtype == torch.float32 and x.is_contiguous()) else x.float().contiguous()
+    dev = _check_dev(x)
+    if x.dim() != 3:
+        raise AssertionError(f"expected a (c, h, w) spectrum, got {tuple(x.shape)}")
+    ctx = _lib.context(dev)
+    P = p.patch_size
+    patches = torch.empty((k, P * P), dtype=torch.float32, device=dev)
+    pos = torch.empty((k, 2), dtype=torch.long, device=dev)
+    ch = torch.empty((k,), dtype=torch.long, device=dev)
+    cfg = p.c(p.max_seq_len)
+    rc = ctx.lib.dctae_patch_spectrum(ctx.h, C.byref(cfg), ptr(x), x.shape[1], x.shape[2], int(k), ptr(patches),
+                                      ptr(pos), ptr(ch), None, _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_patch_spectrum")
+    return patches, pos, ch
+
+
 def synth_images(n: int, h: int, w: int, seed: int, first_index: int = 0, device=None) -> torch.Tensor:
     """(n, 3, h, w) counter-RNG images generated on the device (oracle/rng.py hash)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())

@@ -58,31 +58,14 @@ struct dctae_ctx {
   std::map<int, FftPlan> fft_plans;   // N -> plan (N = 0 entries never stored)
   bool fft_enabled = true;
   bool fft_spec_enabled = true;
-  int rows_prefetch = 0;
   int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
   int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)
   int rows_kernel = 3;                // 512-wide rows: 3 = k_rows512 (registers + one LDS transpose), 2 = k_fft_rows2
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
-  int t_layout = 0;                   // T layout for specialised images: 0 row-major, 1 strips(14), 2 strips(16),
-                                      // 3 row-major with each tile column padded to 16 floats (64-B segments)
-  int cols_kernel = 7;                // specialised column kernel: 2 (LDS scatter), 4 (linear LDS addresses),
-                                      // 5 (complex-pair LDS, N = 512), 6 (5 with several images per block),
-                                      // 7 (6 with pass 1 from registers, one LDS exchange)
-  int cols_ipb = 2, cols_pf = 1;      // cols_kernel 6: images per block, prefetch of the next slice
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
-  int dual_stream = 1;                // several chunks: rows / columns on two streams, T double-buffered
-  hipStream_t s2 = nullptr;
-  std::vector<hipEvent_t> chunk_ev;
-  // fused row+column encode (k_enc_fused): one persistent launch, T in per-XCD ring slots
   int sort_kernel = 2;                // 1: bitonic in LDS (1024 threads), 2: rocPRIM block radix sort
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
-  int fused = 0;                      // measured slower than the two kernels so far (profile: DESIGN.md)
-  int fused_slots = 1;                // T slots per XCD (lookahead = slots - 1 images); only 1 is accepted
-  int fused_bpc = 4;                  // resident workgroups per CU
-  int fused_spin = 1 << 20;           // poll bound of a dependence wait (~1 s), then err |= 8
-  int fused_rows_pct = 50;            // share of row workers
-  int fused_debug = 0;                // 1: skip dependence waits; 2: collect per-XCD tick profile
   int n_cu = 256;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
@@ -482,7 +465,7 @@ struct ChunkJob {
   int n_fr[kVariants], n_fc[kVariants];
   int64_t tw_off[kVariants], post_off_r[kVariants], tw_off_c[kVariants], post_off_c[kVariants];
   int n_rows_tiles, n_cols_tiles;
-  size_t pc_off;      // persistent column kernel (cols_kernel 6): spec-1 images of the job, uniform qw
+  size_t pc_off;      // k_fft_cols7 list: the spec-1 images of the job (one tile-column count qw)
   int n_pc, pc_qw;
   int max_T, any_gemm_rows, any_gemm_cols, fold_t;
   int64_t max_hw;
@@ -499,11 +482,6 @@ struct EncPlan {
   size_t rowlen_off = 0, plans_off = 0;
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
-  // fused path (fused_spec != 0): ring of T slots at ws[0], sync ints after it
-  int fused_spec = 0, fused_nr = 0, fused_nc = 0, fused_qw = 0, n_xcd = 1;
-  int64_t slot_floats = 0, sync_off = 0;   // floats
-  int64_t fused_tw_off = 0, fused_post_off = 0;
-  bool dual = false;   // chunk jobs alternate between two workspace halves (two-stream pipeline)
 };
 
 // ---------------------------------------------------------------------------
@@ -576,8 +554,6 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   for (auto e : ctx->evt_pool) hipEventDestroy(e);
-  for (auto e : ctx->chunk_ev) hipEventDestroy(e);
-  if (ctx->s2) hipStreamDestroy(ctx->s2);
   hipEventDestroy(ctx->plan_evt);
   hipEventDestroy(ctx->done_evt);
   delete ctx;
@@ -621,25 +597,13 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   if (k == "fft") ctx->fft_enabled = value != 0;
   else if (k == "fft_spec") ctx->fft_spec_enabled = value != 0;
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
-  else if (k == "rows_prefetch") ctx->rows_prefetch = value != 0;
-  else if (k == "t_layout" && value >= 0 && value <= 3) ctx->t_layout = (int)value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
-  else if (k == "cols_kernel" && (value == 2 || value == 4 || value == 5 || value == 6 || value == 7)) ctx->cols_kernel = (int)value;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
-  else if (k == "fused") ctx->fused = value != 0;
   else if (k == "t_alias" && value >= 0) ctx->t_alias = (int)value;
   else if (k == "rows_ablate" && value >= 0 && value <= 3) ctx->rows_ablate = (int)value;
   else if (k == "rows_kernel" && (value == 2 || value == 3)) ctx->rows_kernel = (int)value;
-  else if (k == "dual_stream") ctx->dual_stream = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
-  else if (k == "cols_ipb" && (value == 2 || value == 4)) ctx->cols_ipb = (int)value;
-  else if (k == "cols_pf") ctx->cols_pf = value != 0;
-  else if (k == "fused_slots" && value == 1) ctx->fused_slots = 1;   // 2-3 slots: intermittent code mismatches
-  else if (k == "fused_bpc" && value >= 1 && value <= 8) ctx->fused_bpc = (int)value;
-  else if (k == "fused_rows_pct" && value >= 1 && value <= 99) ctx->fused_rows_pct = (int)value;
-  else if (k == "fused_debug" && value >= 0 && value <= 3) ctx->fused_debug = (int)value;
-  else if (k == "fused_spin" && value >= 1024) ctx->fused_spin = (int)std::min<int64_t>(value, 1ll << 30);
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -714,23 +678,8 @@ int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
   if (h & 1) return fail(ctx, DCTAE_EINVAL, "channel/position index out of range of the PatchNorm tables");
   if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
   if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
-  if (h & 8) return fail(ctx, DCTAE_EHIP, "fused encode: a dependence wait timed out (outputs invalid)");
   if (h & 16) return fail(ctx, DCTAE_EINVAL, "VectorQuantize index out of range of the codebook");
   return 0;
-}
-
-int64_t dctae_fused_debug_counters(dctae_ctx* ctx, int32_t* host_out, int64_t cap, void* stream) {
-  if (!ctx || !ctx->enc_plan || !ctx->enc_plan->fused_spec) return 0;
-  const EncPlan& E = *ctx->enc_plan;
-  const int64_t n = ((24 + 2ll * E.n_img + 1) & ~1ll) + 128;   // + 64 profile u64 (fused_debug 2)
-  if (host_out && cap > 0) {
-    hipStream_t s = (hipStream_t)stream;
-    if (hipMemcpyAsync(host_out, ctx->ws + E.sync_off, sizeof(int32_t) * std::min(n, cap), hipMemcpyDeviceToHost, s) !=
-            hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-      return fail(ctx, DCTAE_EHIP, "fused counters copy failed");
-  }
-  return n;
 }
 
 int dctae_synth_images(dctae_ctx* ctx, uint64_t seed, int64_t first_index, int32_t n_img, int32_t H, int32_t W,
@@ -784,37 +733,14 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     }
     D[i].plan_w = plan_of(D[i].W);
     D[i].plan_h = plan_of(D[i].H);
-    // strip-major T when both passes run on the specialised kernels
-    D[i].t_strips = (P == 14 && D[i].plan_w >= 0 && D[i].plan_h >= 0 && plans[D[i].plan_w].spec &&
-                     plans[D[i].plan_h].spec) ? ctx->t_layout : 0;
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
       if (pack->row_len[r] < 0 || pack->row_len[r] > S) return fail(ctx, DCTAE_EINVAL, "row_len out of range");
-  // fused path: every image square N x N on one specialised plan, row-major T
-  {
-    bool ok = ctx->fused && n > 0 && P == 14 && ctx->t_layout == 0;
-    for (int i = 0; ok && i < n; ++i) {
-      const ImgDesc& d = D[i];
-      ok = d.plan_w >= 0 && d.plan_w == d.plan_h && plans[d.plan_w].spec != 0 && d.H == d.W && d.H == D[0].H &&
-           d.qh <= 32;
-    }
-    if (ok) {
-      E.fused_spec = plans[D[0].plan_w].spec;
-      E.fused_nr = (D[0].H + fused_rows_per_item() - 1) / fused_rows_per_item();
-      E.fused_nc = 3 * D[0].qw;
-      E.fused_qw = D[0].qw;
-      E.fused_tw_off = plans[D[0].plan_w].tw_off;
-      E.fused_post_off = plans[D[0].plan_w].post_off;
-      E.n_xcd = std::max(1, std::min(8, ctx->n_cu / 32));
-      E.slot_floats = (3ll * D[0].Kw * D[0].H + 63) & ~63ll;
-      E.sync_off = E.n_xcd * (int64_t)ctx->fused_slots * E.slot_floats;
-    }
-  }
   // chunks: FFT images are grouped so the intermediate T of a chunk stays in
   // the 256 MiB Infinity Cache between the row and column kernels
   auto ws_of = [&](const ImgDesc& d) {
-    int64_t w = 3ll * (d.Kw + d.Kw / 7) * d.H + 64;  // room for 16-wide strips
+    int64_t w = 3ll * d.Kw * d.H + 64;
     if (d.plan_w < 0) w += 3ll * d.H * d.W + 64;
     if (d.plan_h < 0) w += 3ll * d.Kh * d.Kw + 64;
     return w * 4;
@@ -829,7 +755,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     while (i < n) {
       const int64_t w = ws_of(D[i]);
       const bool fft = D[i].plan_w >= 0 && D[i].plan_h >= 0;
-      const int64_t cap = E.fused_spec ? INT64_MAX : fft ? std::min<int64_t>(ctx->chunk_bytes, ctx->ws_limit) : ctx->ws_limit;
+      const int64_t cap = fft ? std::min<int64_t>(ctx->chunk_bytes, ctx->ws_limit) : ctx->ws_limit;
       if (i > j.i0 && wsb + w > cap) break;
       wsb += w;
       ++i;
@@ -857,7 +783,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         continue;
       }
       d.ws_t = wsf;
-      wsf += up(3ll * (d.t_strips >= 2 ? (d.Kw / 14) * 16 : d.Kw) * d.H);
+      wsf += up(3ll * d.Kw * d.H);
       d.ws_p = wsf;
       if (d.plan_w < 0) wsf += up(3ll * d.H * d.W);
       d.ws_y = wsf;
@@ -867,20 +793,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.max_T = std::max(j.max_T, d.T);
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
-    E.ws_need = E.fused_spec ? (size_t)(E.sync_off + 24 + 2ll * n + 2 + 128) * 4 : std::max<size_t>(E.ws_need, (size_t)wsf * 4);
+    E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
     E.max_T = std::max(E.max_T, j.max_T);
-  }
-  // two-stream chunk pipeline: odd chunks use the second workspace half
-  E.dual = !E.fused_spec && ctx->dual_stream && E.jobs.size() > 1;
-  if (E.dual) {
-    const int64_t half = (int64_t)((E.ws_need / 4 + 63) & ~size_t(63));
-    for (size_t k = 1; k < E.jobs.size(); k += 2)
-      for (int i = E.jobs[k].i0; i < E.jobs[k].i1; ++i) {
-        D[i].ws_t += half;
-        D[i].ws_p += half;
-        D[i].ws_y += half;
-      }
-    E.ws_need = (size_t)half * 2 * 4;
   }
   E.n_tok = tok;
   E.n_img = n;
@@ -957,7 +871,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         const int G = 1;
         for (int c = 0; c < 3; ++c)
           for (int w = 0; w < d.qw; w += G) fc[p.spec].push_back(make_int4(li, c, w, std::min(G, d.qw - w)));
-        if (p.spec == 1 && d.t_strips == 0) {
+        if (p.spec == 1) {
           pc_ok = pc_ok && (pc.empty() || d.qw == pc_qw);
           pc_qw = d.qw;
           pc.push_back(li);
@@ -1053,9 +967,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
-                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->t_layout + 64 * ctx->t_alias +
-                             1024 * ctx->xcd_order + 4096 * ctx->fused + 8192 * ctx->fused_slots +
-                             (1 << 20) * ctx->cols_kernel + (1 << 24) * ctx->dual_stream,
+                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 64 * ctx->t_alias +
+                             1024 * ctx->xcd_order,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1132,34 +1045,6 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   }
   EncParams epj = ep;
   if (!full) epj.median = nullptr;
-  if (E.fused_spec) {
-    FusedArgs fa{};
-    fa.imgs = (const ImgDesc*)(pd + E.all_desc_off);
-    fa.rgb = imgs->rgb_dev;
-    fa.ring = ctx->ws;
-    fa.slot_floats = E.slot_floats;
-    fa.sync = (int*)(ctx->ws + E.sync_off);
-    fa.err = ctx->err_dev;
-    fa.tw = ctx->fft_tab + E.fused_tw_off;
-    fa.post = ctx->fft_tab + E.fused_post_off;
-    fa.n_img = E.n_img;
-    fa.n_xcd = E.n_xcd;
-    fa.slots = ctx->fused_slots;
-    fa.look = std::max(1, ctx->fused_slots - 1);
-    fa.nr = E.fused_nr;
-    fa.nc = E.fused_nc;
-    fa.qw = E.fused_qw;
-    fa.spin_limit = ctx->fused_spin;
-    fa.rows_pct = ctx->fused_rows_pct;
-    fa.debug = ctx->fused_debug & 1;
-    const size_t n_sync = 24 + 2 * (size_t)E.n_img;
-    fa.prof = (ctx->fused_debug & 2) ? (unsigned long long*)(ctx->ws + E.sync_off + ((n_sync + 1) & ~size_t(1)))
-                                     : nullptr;
-    const bool thr = epj.median && epj.thr && !sk.norm && epj.maxph <= 32 && epj.cb_dim == 14 && epj.ncb == 14;
-    HIPCHK(ctx, hipMemsetAsync(fa.sync, 0, (((n_sync + 1) & ~size_t(1)) + 128) * sizeof(int), s));
-    Timer t(ctx, s, "enc_fused");
-    launch_enc_fused(E.fused_spec, thr, ctx->n_cu * ctx->fused_bpc, fa, ctx->cm, epj, sk, s);
-  }
   // row half / column half of a chunk job on a stream
   auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
     const int nj = j.i1 - j.i0;
@@ -1180,13 +1065,12 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fr[v]) {
         Timer t(ctx, st, "fft_rows");
-        if (v == 1 && ctx->rows_kernel == 3 && ctx->t_layout == 0 && cfg->max_patch_w >= 32)
+        if (v == 1 && ctx->rows_kernel == 3 && cfg->max_patch_w >= 32)
           launch_rows512(dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
                          ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st, ctx->rows_ablate);
         else
           launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
-                               ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st,
-                               ctx->rows_prefetch);
+                               ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st);
       }
   };
   auto do_cols = [&](const ChunkJob& j, hipStream_t st) {
@@ -1214,40 +1098,12 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         Timer t(ctx, st, "fft_cols");
         launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
                              ctx->fft_tab + j.post_off_c[v], epj, sk, st,
-                             ctx->cols_kernel, ctx->t_layout, v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr,
-                             v == 1 ? j.n_pc : 0, j.pc_qw, ctx->cols_ipb, ctx->cols_pf);
+                             v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr, v == 1 ? j.n_pc : 0, j.pc_qw);
       }
   };
-  const int nJ = E.fused_spec ? 0 : (int)E.jobs.size();
-  if (nJ > 1 && E.dual) {
-    // chunk pipeline on two streams: rows of chunk k (stream s) overlap the
-    // columns of chunk k - 1 (second stream); chunk k's T lives in ws half k % 2,
-    // so rows(k) waits for cols(k - 2).  Chunks are sized so both halves stay
-    // in the Infinity Cache (chunk_bytes).
-    if (!ctx->s2) HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
-    while ((int)ctx->chunk_ev.size() < 2 * nJ + 1) {
-      hipEvent_t e;
-      HIPCHK(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      ctx->chunk_ev.push_back(e);
-    }
-    hipEvent_t* ev_rows = ctx->chunk_ev.data() + 1;
-    hipEvent_t* ev_cols = ctx->chunk_ev.data() + 1 + nJ;
-    HIPCHK(ctx, hipEventRecord(ctx->chunk_ev[0], s));
-    HIPCHK(ctx, hipStreamWaitEvent(ctx->s2, ctx->chunk_ev[0], 0));
-    for (int k = 0; k < nJ; ++k) {
-      if (k >= 2) HIPCHK(ctx, hipStreamWaitEvent(s, ev_cols[k - 2], 0));
-      do_rows(E.jobs[k], s);
-      HIPCHK(ctx, hipEventRecord(ev_rows[k], s));
-      HIPCHK(ctx, hipStreamWaitEvent(ctx->s2, ev_rows[k], 0));
-      do_cols(E.jobs[k], ctx->s2);
-      HIPCHK(ctx, hipEventRecord(ev_cols[k], ctx->s2));
-    }
-    HIPCHK(ctx, hipStreamWaitEvent(s, ev_cols[nJ - 1], 0));
-  } else {
-    for (int k = 0; k < nJ; ++k) {
-      do_rows(E.jobs[k], s);
-      do_cols(E.jobs[k], s);
-    }
+  for (const ChunkJob& j : E.jobs) {
+    do_rows(j, s);
+    do_cols(j, s);
   }
   if (full && E.n_img > 0) {
     Timer t(ctx, s, "sort_pack");
@@ -1274,6 +1130,131 @@ int dctae_spectrum_tokens(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_i
   hipSetDevice(ctx->device);
   return encode_impl(ctx, cfg, imgs, nullptr, nullptr, nullptr, nullptr, tok_off, tokens_dev, scores_dev,
                      (hipStream_t)stream);
+}
+
+// Full-image orthonormal 2-D DCT (util.py:333-338 on the whole (3, H, W) image)
+// with the optional colour transform: FE._transform_image_in / _out
+// (FE:129-152) for callers that run (or override) the stages one by one.
+// Two MFMA GEMMs per image on the full DCT matrices (no kept-corner crop).
+int dctae_dct2(dctae_ctx* ctx, const float* x, int32_t n_img, int32_t H, int32_t W, int32_t direction, int32_t color,
+               float* y, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipSetDevice(ctx->device);
+  if (n_img < 0 || H < 1 || W < 1 || (direction != 0 && direction != 1)) return fail(ctx, DCTAE_EINVAL, "bad dct2 shape");
+  if (n_img == 0) return 0;
+  if (!x || !y || x == y) return fail(ctx, DCTAE_EINVAL, "dct2 needs distinct input / output buffers");
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  const int64_t hw = (int64_t)H * W, plane = 3 * hw;
+  const float *CW, *CH;
+  if ((rc = dct_matrix(ctx, W, W, &CW)) || (rc = dct_matrix(ctx, H, H, &CH))) return rc;
+  // workspace: IPT (forward with colour) and the intermediate U / T, per image
+  if ((rc = ensure_ws(ctx, (size_t)2 * plane * n_img * 4, 256))) return rc;
+  float* a = ctx->ws;                        // forward: IPT input; inverse: IPT output
+  float* u = ctx->ws + plane * n_img;        // intermediate
+  std::vector<GemmProblem> probs;
+  std::vector<TileRef> t1, t2;
+  for (int i = 0; i < n_img; ++i) {
+    const int64_t o = plane * i;
+    GemmProblem g1, g2;
+    if (direction == 0) {
+      const float* src = color ? a + o : x + o;
+      // T[c][y][kx] = sum_x src[c][y][x] CW[kx][x];  Y[c][ky][kx] = sum_y CH[ky][y] T[c][y][kx]
+      g1 = gemm(src, hw, W, 1, CW, 0, W, 1, u + o, hw, W, 1, H, W, W, 3);
+      g2 = gemm(CH, 0, H, 1, u + o, hw, 1, W, y + o, hw, W, 1, H, W, H, 3);
+    } else {
+      float* dst = color ? a + o : y + o;
+      // U[c][y][kx] = sum_ky CH[ky][y] Y[c][ky][kx];  X[c][y][x] = sum_kx U[c][y][kx] CW[kx][x]
+      g1 = gemm(CH, 0, 1, H, x + o, hw, 1, W, u + o, hw, W, 1, H, W, H, 3);
+      g2 = gemm(u + o, hw, W, 1, CW, 0, 1, W, dst, hw, W, 1, H, W, W, 3);
+    }
+    const int pr = (int)probs.size();
+    probs.push_back(g1);
+    probs.push_back(g2);
+    add_tiles(t1, pr, g1);
+    add_tiles(t2, pr + 1, g2);
+  }
+  PlanBuf pb;
+  const size_t g_off = pb.add(probs.data(), probs.size());
+  const size_t t1_off = pb.add(t1.data(), t1.size());
+  const size_t t2_off = pb.add(t2.data(), t2.size());
+  order_after_previous(ctx, s);
+  if ((rc = upload_plan(ctx, pb, s))) return rc;
+  uint8_t* pd = ctx->plan_dev;
+  if (direction == 0 && color) {
+    Timer t(ctx, s, "rgb_to_ipt");
+    launch_color(x, a, hw, n_img, 0, ctx->cm, s);
+  }
+  {
+    Timer t(ctx, s, "dct2_gemm");
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s);
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s);
+  }
+  if (direction == 1 && color) {
+    Timer t(ctx, s, "ipt_to_rgb");
+    launch_color(a, y, hw, n_img, 1, ctx->cm, s);
+  }
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
+  return 0;
+}
+
+// FE._patch_image (FE:364-452) of one cropped spectrum (3, H, W), H and W
+// multiples of P: tiles of the kept corner, importance scores, (score desc,
+// index asc) order, top k -> patches (k, P*P), positions (k, 2), channels (k).
+int dctae_patch_spectrum(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const float* spec, int32_t H, int32_t W, int32_t k,
+                         float* patches, int64_t* positions, int64_t* channels, float* scores, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  hipSetDevice(ctx->device);
+  int rc = check_cfg(ctx, cfg);
+  if (rc) return rc;
+  const int P = cfg->patch_size, PP = P * P;
+  if (H % P || W % P) return fail(ctx, DCTAE_EINVAL, "_patch_image: h and w must be multiples of patch_size (FE:368-369)");
+  ImgDesc d;
+  if ((rc = describe(ctx, cfg, H, W, d))) return rc;
+  if (k < 1 || k > d.T) return fail(ctx, DCTAE_EINVAL, "_patch_image: k out of range (FE:429-435)");
+  if (!spec || !patches || !positions || !channels) return fail(ctx, DCTAE_EINVAL, "NULL _patch_image buffer");
+  hipStream_t s = (hipStream_t)stream;
+  d.ws_y = 0;
+  d.tok_off = 0;
+  d.row = 0;
+  d.col = 0;
+  d.k = k;
+  d.local_id = 0;
+  const size_t y_bytes = (size_t)3 * d.Kh * d.Kw * 4;
+  const size_t st_scores = ((size_t)d.T * 4 + 255) & ~size_t(255), st_raw = (size_t)d.T * PP * 4;
+  const size_t st_ids = ((size_t)k * 8 + 255) & ~size_t(255);
+  if ((rc = ensure_ws(ctx, y_bytes, st_scores + st_raw + st_ids + 256))) return rc;
+  PlanBuf pb;
+  const size_t d_off = pb.add(&d, 1);
+  order_after_previous(ctx, s);
+  if ((rc = upload_plan(ctx, pb, s))) return rc;
+  const ImgDesc* dd = (const ImgDesc*)(ctx->plan_dev + d_off);
+  for (int c = 0; c < 3; ++c)   // kept corner (3, Kh, Kw) of the (3, H, W) spectrum
+    HIPCHK(ctx, hipMemcpy2DAsync(ctx->ws + (size_t)c * d.Kh * d.Kw, (size_t)d.Kw * 4, spec + (size_t)c * H * W,
+                                 (size_t)W * 4, (size_t)d.Kw * 4, d.Kh, hipMemcpyDeviceToDevice, s));
+  EncParams ep = enc_params(cfg, nullptr, nullptr);
+  ep.S = k;
+  TokenSinks sk{};
+  sk.scores = (float*)ctx->stage;
+  sk.raw = (float*)(ctx->stage + st_scores);
+  PackSinks ps{};
+  ps.pos = positions;
+  ps.ch = channels;
+  ps.ids = (int64_t*)(ctx->stage + st_scores + st_raw);
+  ps.raw = patches;
+  ps.scores = scores;
+  {
+    Timer t(ctx, s, "tile_epilogue");
+    launch_tile_epilogue(dd, 1, d.T, ctx->ws, ep, sk, s);
+  }
+  {
+    Timer t(ctx, s, "sort_pack");
+    launch_sort_pack(dd, 1, next_pow2(d.T), ep, sk, ps, s, ctx->sort_kernel, d.T);
+  }
+  HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
+  return 0;
 }
 
 static int norm_impl(dctae_ctx* ctx, const dctae_norm* norm, int32_t P, int32_t mh, int32_t mw, const float* x,

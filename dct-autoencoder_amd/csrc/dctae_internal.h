@@ -30,9 +30,7 @@ struct ImgDesc {
   int32_t T;         // tokens = C*qh*qw
   int32_t row, col, k, local_id;  // packing
   int32_t plan_w, plan_h;         // FFT plan index for rows (length W) / cols (length H); -1 = GEMM
-  int32_t t_strips;               // T layout: 0 = [c][y][Kw] row-major, 1 = [c][w][y][P] strips,
-                                  // 2 = [c][w][y][16] padded strips, 3 = [c][y][w][16] padded row-major
-  int32_t t_pad;
+  int32_t pad0, pad1;
 };
 
 // Generic batched strided fp32 GEMM problem:
@@ -93,34 +91,6 @@ struct PackSinks {
   float* patches;     // (R,S,PP) gathered from norm staging
   float* raw;         // (R,S,PP) gathered from raw staging
   float* scores;      // (R,S)
-};
-
-// Fused row+column encode (k_enc_fused, dctae_fft2.hip): one persistent launch;
-// the images of XCD queue q are q, q + n_xcd, ...; T of an image lives in one
-// of `slots` ring slots of that XCD (L2 / Infinity-Cache resident); workers
-// are row or column workers (rows_pct percent rows).
-struct FusedArgs {
-  const ImgDesc* imgs;
-  const float* rgb;
-  float* ring;          // n_xcd * slots slots of slot_floats
-  int64_t slot_floats;
-  int* sync;            // [0, 8) row queues, [8, 16) column queues, [16, 24) worker ids,
-                        // [24, 24 + n) rows done, [24 + n, 24 + 2n) columns done
-  int* err;             // |= 8 on a wait that timed out
-  const float2* tw;
-  const float2* post;
-  int32_t n_img, n_xcd, slots, look;
-  int32_t nr, nc;       // row items (16 rows each) and column items (3 * qw) per image
-  int32_t qw, spin_limit;
-  int32_t rows_pct, debug;      // debug & 1: skip the dependence waits (timing experiments only: wrong output)
-  unsigned long long* prof;     // nullable: per-XCD [wait, row, column ticks, row items, column items, life, wgs, -]
-};
-
-struct FusedParams {   // k_enc_fused's by-value parameter block (first kernel argument)
-  FusedArgs a;
-  ColorMats cm;
-  EncParams ep;
-  TokenSinks sk;
 };
 
 struct DecodeArgs {

@@ -158,6 +158,42 @@ void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const flo
   hipLaunchKernelGGL(k_ipt_to_rgb, dim3(gx, n_img), dim3(256), 0, s, imgs, ws, out, cm);
 }
 
+// colour transform of a contiguous batch of (3, H, W) images, out of place:
+// dir 0 = rgb_to_ipt (util.py:70-82), dir 1 = ipt_to_rgb (util.py:85-97).
+// The standalone FE._transform_image_in / _out entry points (dctae_dct2).
+__global__ void k_color(const float* __restrict__ x, float* __restrict__ y, int64_t hw, int n_img, int dir,
+                        ColorMats cm) {
+  const int64_t n = hw * n_img;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / hw, p = e - i * hw;
+    const float* s = x + 3 * hw * i + p;
+    float* d = y + 3 * hw * i + p;
+    const float a = s[0], b = s[hw], c = s[2 * hw];
+    if (dir == 0) {
+      const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, a, b, c), 0.430000007152557373046875f);
+      const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, a, b, c), 0.430000007152557373046875f);
+      const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, a, b, c), 0.430000007152557373046875f);
+      d[0] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
+      d[hw] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
+      d[2 * hw] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+    } else {
+      const float inv_gamma = 2.3255813121795654296875f;  // fp32(1/0.43)
+      const float l0 = signed_pow(mat3_row(cm.ipt2lms, 0, a, b, c), inv_gamma);
+      const float l1 = signed_pow(mat3_row(cm.ipt2lms, 1, a, b, c), inv_gamma);
+      const float l2 = signed_pow(mat3_row(cm.ipt2lms, 2, a, b, c), inv_gamma);
+      d[0] = mat3_row(cm.lms2rgb, 0, l0, l1, l2);
+      d[hw] = mat3_row(cm.lms2rgb, 1, l0, l1, l2);
+      d[2 * hw] = mat3_row(cm.lms2rgb, 2, l0, l1, l2);
+    }
+  }
+}
+
+void launch_color(const float* x, float* y, int64_t hw, int n_img, int dir, const ColorMats& cm, hipStream_t s) {
+  const int64_t n = hw * n_img;
+  const int g = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_color, dim3(std::max(g, 1)), dim3(256), 0, s, x, y, hw, n_img, dir, cm);
+}
+
 // ---------------------------------------------------------------------------
 // generic batched strided fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32)
 //   O[c][m][n] = sum_k A[c][m][k] * B[c][n][k]

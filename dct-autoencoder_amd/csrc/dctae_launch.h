@@ -11,6 +11,7 @@ void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const flo
                        const ColorMats& cm, hipStream_t s);
 void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* ws, float* out,
                        const ColorMats& cm, hipStream_t s);
+void launch_color(const float* x, float* y, int64_t hw, int n_img, int dir, const ColorMats& cm, hipStream_t s);
 void launch_fold_t(const ImgDesc* imgs, int n_img, int64_t max_hw, float* ws, hipStream_t s);
 void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
@@ -60,11 +61,10 @@ void launch_norm_thresholds(const float* med, const float* b, int64_t n, float e
 int fft_spec_id(int N, const int* radix, int npass, int P);
 int fft_spec_rows_per_block(int spec);
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int prefetch);
+                          const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s);
 void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int n_blocks, const float* ws,
                           const float2* tw, const float2* post, const EncParams& ep, const TokenSinks& sk,
-                          hipStream_t s, int kernel, int layout, const int* cols6_list = nullptr, int cols6_n = 0,
-                          int cols6_qw = 0, int cols6_ipb = 4, int cols6_pf = 1);
+                          hipStream_t s, const int* list, int n_list, int qw);
 
 // decode on the FFT path (dctae_idct.hip)
 void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int32_t* map, hipStream_t s);
@@ -76,9 +76,6 @@ void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, in
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                     const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate = 0);
 
-int fused_rows_per_item();
 int cols7_grid(int n_list, int qw, int ipb);
-void launch_enc_fused(int spec, bool thr, int grid, const FusedArgs& a, const ColorMats& cm, const EncParams& ep,
-                      const TokenSinks& sk, hipStream_t s);
 
 }  // namespace dctae

@@ -7,7 +7,15 @@ Reference methods keep their names, arguments and results:
   iter_batches(loader, bs)       FE:179-287   -> DCTPatches generator (same emission quirks)
   postprocess(dct_patches)       FE:289-310   -> list of (3, H, W) RGB images
   revert_patching(dct_patches)   FE:607-656   -> list of (3, 14ph, 14pw) spectra
-  _get_crop_dims / _crop_image / _patch_image / _group_patches_by_max_seq_len / _batch_groups
+  _transform_image_in / _transform_image_out   FE:129-152 (dctae_dct2)
+  _get_crop_dims / _crop_image / _patch_image (dctae_patch_spectrum) / _group_patches_by_max_seq_len / _batch_groups
+Stage hooks: callers replace these per instance or in a subclass (the
+reference's decode_gif.py:86-91 sets ``_transform_image_out = lambda x: x`` to
+render the spectrum; its tests/testpatching.py:42-43 makes both transforms the
+identity).  preprocess / postprocess / iter_batches / encode_batch then run the
+reference's stage sequence (FE:154-177, 179-287, 289-310) through the hooks,
+each default stage still a HIP kernel; with no override they run the fused
+launch sequence.
 Additive fused entry points (the MI355X hot path):
   encode_batch(images, patchnorm, lfq, batch_size)  preprocess + pack + PatchNorm + LFQ in one launch sequence
   decode_batch(dct_patches, codes, patchnorm, lfq)  indices_to_codes + inverse_norm + postprocess
@@ -84,6 +92,29 @@ class DCTAutoencoderFeatureExtractor:
     def _k(self, h: int, w: int) -> int:
         return packing.choose_k(self._tokens(h, w), self.sample_patches_beta, self.max_seq_len, self.rng)
 
+    # ------------------------------------------------------------- stage hooks
+    def _overridden(self, name: str) -> bool:
+        """True when a caller replaced the stage `name` on this instance or in a subclass."""
+        return name in self.__dict__ or getattr(type(self), name) is not getattr(DCTAutoencoderFeatureExtractor, name)
+
+    def _staged_in(self) -> bool:
+        return any(self._overridden(n) for n in ("_transform_image_in", "_crop_image", "_patch_image"))
+
+    def _staged_out(self) -> bool:
+        return any(self._overridden(n) for n in ("_transform_image_out", "revert_patching"))
+
+    @torch.no_grad()
+    def _transform_image_in(self, x: torch.Tensor) -> torch.Tensor:
+        """FE:129-142: rgb_to_ipt, then the orthonormal dct2 of the whole
+        (c, h, w) image (dctae_dct2); result in x's dtype and on x's device."""
+        y = _ops.dct2(self._dev(x).float(), inverse=False, color=True)
+        return y.to(x.dtype).to(x.device)
+
+    def _transform_image_out(self, x: torch.Tensor) -> torch.Tensor:
+        """FE:144-152: idct2 of the whole (c, h, w) spectrum, then ipt_to_rgb (dctae_dct2)."""
+        y = _ops.dct2(self._dev(x).float(), inverse=True, color=True)
+        return y.to(x.dtype).to(x.device)
+
     # ------------------------------------------------------------- reference API
     def _get_crop_dims(self, h: int, w: int):
         """FE:312-345"""
@@ -98,14 +129,49 @@ class DCTAutoencoderFeatureExtractor:
         return x[:, :ch, :cw]
 
     @torch.no_grad()
+    def _patch_image(self, x: torch.Tensor):
+        """FE:364-452 on a cropped (c, h, w) spectrum (dctae_patch_spectrum):
+        tiles of the kept corner, importance order (score desc, flat index asc),
+        top k (k drawn like the reference, FE:429-435)."""
+        c, h, w = x.shape
+        P = self.patch_size
+        assert h % P == 0
+        assert w % P == 0
+        assert c == self.channels
+        k = self._k(h, w)
+        patches, pos, channels = _ops.patch_spectrum(self._dev(x), self.params(), k)
+        s, z = patches.shape
+        assert z == P ** 2, f"{z} != {P ** 2}"
+        assert s <= self.max_seq_len
+        return patches, pos, channels
+
+    @torch.no_grad()
     def preprocess(self, im: torch.Tensor) -> Dict[str, Any]:
         """FE:154-177 for one (c, h, w) RGB image in [0, 1]: IPT + DCT +
-        spectral patching + importance order + top-k, all on the GPU."""
+        spectral patching + importance order + top-k, all on the GPU.  With
+        an overridden stage hook the reference's stage sequence runs instead."""
+        if self._staged_in():
+            return self._preprocess_staged(im)
         return self.preprocess_many([im])[0]
+
+    @torch.no_grad()
+    def _preprocess_staged(self, im: torch.Tensor) -> Dict[str, Any]:
+        """FE:154-177 stage by stage, every stage through its (possibly replaced) hook."""
+        im = self._transform_image_in(im)
+        _, h, w = im.shape
+        original_size = (h, w)
+        im = self._crop_image(im)
+        _, ch, cw = im.shape
+        patch_size = (ch // self.patch_size, cw // self.patch_size)
+        patches, pos, channels = self._patch_image(im)
+        return dict(patches=patches, positions=pos, channels=channels, original_sizes=original_size,
+                    patch_sizes=patch_size)
 
     @torch.no_grad()
     def preprocess_many(self, images: Sequence[torch.Tensor]) -> List[Dict[str, Any]]:
         """``preprocess`` for several images in one launch sequence."""
+        if self._staged_in():
+            return [self._preprocess_staged(im) for im in images]
         images = [self._dev(im) for im in images]
         for im in images:
             assert im.shape[0] == self.channels
@@ -129,6 +195,9 @@ class DCTAutoencoderFeatureExtractor:
     def iter_batches(self, dataloader, batch_size: Optional[int] = None) -> Iterator[DCTPatches]:
         """FE:179-287: greedy packing of preprocessed items into rows of
         max_seq_len; same emission rules (see packing.iter_batch_plans)."""
+        if self._overridden("_group_patches_by_max_seq_len"):
+            yield from self._iter_batches_staged(dataloader, batch_size)
+            return
         fixed = {"patches", "positions", "channels", "original_sizes", "patch_sizes"}
         items: Dict[int, Tuple] = {}
         cum_o: List = []
@@ -169,6 +238,48 @@ class DCTAutoencoderFeatureExtractor:
                                            original_sizes=o_now, patch_sizes=p_now, _data=x_now)
                 if batch_size is not None:
                     assert batch.patches.shape[0] == batch_size
+                    # emitted groups leave the state for good (FE:235-243): drop their items
+                    for r in emit:
+                        for i in r:
+                            items.pop(i, None)
+                yield batch
+
+    @torch.no_grad()
+    def _iter_batches_staged(self, dataloader, batch_size: Optional[int]) -> Iterator[DCTPatches]:
+        """FE:179-287 step by step through the (replaced) _group_patches_by_max_seq_len
+        and _batch_groups hooks."""
+        fixed = {"patches", "positions", "channels", "original_sizes", "patch_sizes"}
+        state = None
+        cum_o, cum_p, cum_x = [], [], {}
+        while True:
+            try:
+                d = next(dataloader)
+            except StopIteration:
+                return
+            cum_o = cum_o + list(d["original_sizes"])
+            cum_p = cum_p + list(d["patch_sizes"])
+            for k, v in d.items():
+                if k not in fixed:
+                    cum_x.setdefault(k, []).extend(v)
+            state = self._group_patches_by_max_seq_len(d["patches"], d["positions"], d["channels"], state)
+            if batch_size is None and len(state.group) > 0:
+                state.groups.append(state.group)
+                state.groups_pos.append(state.group_pos)
+                state.groups_channels.append(state.group_channels)
+                state.seq_len, state.group, state.group_pos, state.group_channels = 0, [], [], []
+            if batch_size is None or len(state.groups) > batch_size:
+                keep = GroupPatchesState(state.groups[batch_size:], state.groups_pos[batch_size:], state.group,
+                                         state.group_pos, state.groups_channels[batch_size:], state.group_channels,
+                                         state.seq_len)
+                emit = (state.groups[:batch_size], state.groups_pos[:batch_size], state.groups_channels[:batch_size])
+                n = sum(len(g) for g in emit[0])
+                batch = self._batch_groups(*emit, original_sizes=cum_o[:n], patch_sizes=cum_p[:n],
+                                           _data={k: v[:n] for k, v in cum_x.items()})
+                if batch_size is not None:
+                    assert batch.patches.shape[0] == batch_size
+                cum_o, cum_p = cum_o[n:], cum_p[n:]
+                cum_x = {k: v[n:] for k, v in cum_x.items()}
+                state = keep
                 yield batch
 
     @torch.no_grad()
@@ -249,7 +360,17 @@ class DCTAutoencoderFeatureExtractor:
     @torch.no_grad()
     def postprocess(self, x: DCTPatches) -> List[torch.Tensor]:
         """FE:289-310: un-normalised DCTPatches -> RGB images (revert_patching,
-        zero pad, DCT-III, IPT -> RGB fused on the GPU)."""
+        zero pad, DCT-III, IPT -> RGB fused on the GPU).  With an overridden
+        _transform_image_out / revert_patching the reference's stage sequence
+        runs through the hooks (e.g. the spectrum itself for decode_gif.py:86-91)."""
+        if self._staged_out():
+            images = []
+            for image, (h, w) in zip(self.revert_patching(x), x.original_sizes):
+                ch, cw = image.shape[-2:]
+                im_pad = torch.zeros(self.channels, h, w, device=image.device, dtype=image.dtype)
+                im_pad[:, :ch, :cw] = image
+                images.append(self._transform_image_out(im_pad))
+            return images
         return _ops.decode(self.params(x.patches.shape[1]), x.batched_image_ids, x.key_pad_mask,
                            x.patch_positions, x.patch_channels, x.patch_sizes, x.original_sizes,
                            patches=x.patches)
@@ -267,7 +388,11 @@ class DCTAutoencoderFeatureExtractor:
         Returns [(DCTPatches, codes)] per emitted batch; DCTPatches.patches
         holds the PatchNorm output if return_patches, the raw DCT tokens if
         return_raw, else an empty (R, S, 0) tensor.  codes is None without lfq.
+        With an overridden stage hook the reference's stages run one by one.
         """
+        if self._staged_in() or self._overridden("_group_patches_by_max_seq_len") or \
+                self._overridden("_batch_groups"):
+            return self._encode_staged(images, patchnorm, lfq, batch_size, return_patches, return_raw)
         if isinstance(images, torch.Tensor) and images.dim() == 4:
             x = self._dev(images)
             B, _, H, W = x.shape
@@ -314,6 +439,27 @@ class DCTAutoencoderFeatureExtractor:
             outs.append((dp, res.get("codes")))
         return outs
 
+    @torch.no_grad()
+    def _encode_staged(self, images, patchnorm, lfq, batch_size, return_patches, return_raw):
+        """encode_batch through the stage hooks: preprocess -> iter_batches ->
+        PatchNorm (eval) -> LFQ (eval), each stage on its own launch."""
+        items = [self.preprocess(im) for im in images]
+        loader = iter([{k: [it[k] for it in items] for k in items[0]}])
+        outs = []
+        for batch in self.iter_batches(loader, batch_size):
+            codes, normed = None, None
+            if patchnorm is not None:
+                normed = patchnorm(batch.shallow_copy())
+                if lfq is not None:
+                    _, codes, _, _ = lfq(normed, mask=~batch.key_pad_mask)
+            if not return_raw:
+                batch.patches = normed if (return_patches and normed is not None) else \
+                    torch.empty((*batch.patches.shape[:2], 0), device=batch.patches.device)
+            elif return_patches and normed is not None:
+                batch._data = (batch._data or {}) | {"normalised_patches": normed}
+            outs.append((batch, codes))
+        return outs
+
     @staticmethod
     def _subset(desc, keep, idx):
         import ctypes as C
@@ -349,6 +495,8 @@ class BatchEncoder:
         from ._lib import Images, LFQCfg, Packing, PackedOut, i32, i64, ptr
         self.fe = fe
         self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.dev.index is None:   # "cuda" -> the current device, as tensors report it
+            self.dev = torch.device(self.dev.type, torch.cuda.current_device())
         self.B, self.H, self.W = batch, height, width
         if fe.sample_patches_beta > 0:
             raise AssertionError("BatchEncoder needs sample_patches_beta == 0 (fixed k)")

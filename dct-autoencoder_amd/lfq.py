@@ -73,7 +73,7 @@ class LFQ(nn.Module):
         is_img_or_video = indices.ndim >= (3 + int(self.keep_num_codebooks_dim))
         if not self.keep_num_codebooks_dim:
             indices = rearrange(indices, "... -> ... 1")
-        codes = _ops.lfq_codes(indices, self.cfg())
+        codes = _ops.lfq_codes(indices, self.cfg()).to(self.dtype)
         if project_out:
             codes = self.project_out(codes)
         if is_img_or_video:
@@ -95,7 +95,7 @@ class LFQ(nn.Module):
         assert x.shape[-1] == self.dim, f"expected dimension of {self.dim} but received {x.shape[-1]}"
         x = self.project_in(x)
         q, indices = _ops.lfq_forward(x, self.cfg())
-        q = self.project_out(q)
+        q = self.project_out(q.to(x.dtype))   # the reference keeps the input dtype (fp16 / bf16 models)
         if is_img_or_video:
             q = q.reshape(*shape[:-1], q.shape[-1])
             q = rearrange(q, "b ... d -> b d ...")

@@ -40,6 +40,11 @@ from .dct_patches import DCTPatches
 from .lfq import LFQ
 from .patchnorm import PatchNorm
 
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    """fp32 contiguous view / copy of a parameter for a kernel's float* operand."""
+    return t.detach().float().contiguous()
+
 LIN_F32, LIN_BF16, LIN_BF16_QGELU, LIN_F32_RESIDUAL = 0, 1, 2, 3
 
 
@@ -232,10 +237,16 @@ class DCTAutoencoder(nn.Module):
             self._packed_key = key
         return self._packed
 
-    def _check_mode(self):
+    def _check_mode(self, dev=None):
         if self.training:
             raise NotImplementedError("DCTAutoencoder training (losses, backward) is not on the MI355X path: "
                                       "call .eval()")
+        if dev is not None:
+            # kernels take raw device pointers: a parameter left on another device (or the
+            # CPU) would be read as garbage, so refuse it like torch's device mismatch error
+            for n, p in self.named_parameters():
+                if p.device != dev:
+                    raise RuntimeError(f"parameter {n} is on {p.device}, the input on {dev}: move the model with .to()")
 
     @staticmethod
     def _linear(ctx, x, w, bias, n, epi, out):
@@ -266,7 +277,8 @@ class DCTAutoencoder(nn.Module):
     @staticmethod
     def _layernorm(ctx, h, ln, out):
         m, d = h.shape
-        ctx.check(ctx.lib.dctae_model_layernorm(ctx.h, m, d, _lib.ptr(h), d, _lib.ptr(ln.weight), _lib.ptr(ln.bias),
+        g, b = _f32(ln.weight), _f32(ln.bias)   # fp32 copies when the model was cast (e.g. .half())
+        ctx.check(ctx.lib.dctae_model_layernorm(ctx.h, m, d, _lib.ptr(h), d, _lib.ptr(g), _lib.ptr(b),
                                                 C.c_float(ln.eps), _lib.ptr(out), out.shape[1],
                                                 _lib.stream_ptr(h.device)), "layer_norm")
         return out
@@ -311,7 +323,7 @@ class DCTAutoencoder(nn.Module):
     # ---- modeling:119-200 ----
     @torch.no_grad()
     def encode(self, dct_patches: DCTPatches, do_normalize: bool = False):
-        self._check_mode()
+        self._check_mode(dct_patches.patches.device)
         if do_normalize:
             dct_patches = self.normalize_(dct_patches)
         pk = self._weights()
@@ -326,8 +338,9 @@ class DCTAutoencoder(nn.Module):
         ln = self.to_patch_embedding[1]
         ch, pos = self._meta(dct_patches)
         tabs = self._pos_tables("encoder")
-        ctx.check(ctx.lib.dctae_model_embed_norm(ctx.h, r * s, d, _lib.ptr(e), d, _lib.ptr(ln.weight),
-                                                 _lib.ptr(ln.bias), C.c_float(ln.eps), *[_lib.ptr(t) for t in tabs],
+        g, b = _f32(ln.weight), _f32(ln.bias)
+        ctx.check(ctx.lib.dctae_model_embed_norm(ctx.h, r * s, d, _lib.ptr(e), d, _lib.ptr(g),
+                                                 _lib.ptr(b), C.c_float(ln.eps), *[_lib.ptr(t) for t in tabs],
                                                  _lib.ptr(ch), _lib.ptr(pos), _lib.ptr(h), d, _lib.stream_ptr(dev)),
                   "to_patch_embedding")
         self._clip("encoder", h, dct_patches)
@@ -380,7 +393,7 @@ class DCTAutoencoder(nn.Module):
 
     @torch.no_grad()
     def decode(self, x: DCTPatches, do_inv_norm: bool = False) -> DCTPatches:
-        self._check_mode()
+        self._check_mode(x.patches.device)
         pk = self._weights()
         r, s, d = x.patches.shape
         dev = x.patches.device

@@ -138,6 +138,23 @@ int dctae_encode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* im
 int dctae_spectrum_tokens(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
                           const int64_t* tok_off, float* tokens_dev, float* scores_dev, void* stream);
 
+/* FE._transform_image_in / _transform_image_out (FE:129-152) on n_img
+ * contiguous (3, H, W) fp32 images: direction 0 = dct2(rgb_to_ipt(x)),
+ * direction 1 = ipt_to_rgb(idct2(x)); color = 0 skips the colour transform
+ * (util.dct2 / util.idct2 alone, util.py:333-338).  Orthonormal DCT-II / III
+ * over the whole H x W (no crop).  x_dev and y_dev must not alias. */
+int dctae_dct2(dctae_ctx* ctx, const float* x_dev, int32_t n_img, int32_t H, int32_t W, int32_t direction,
+               int32_t color, float* y_dev, void* stream);
+
+/* FE._patch_image (FE:364-452) of one cropped spectrum x (3, H, W), H and W
+ * multiples of patch_size: 14x14 tiles of the kept corner (max_patch_h/w),
+ * importance scores, order (score desc, flat index asc), top k.  Outputs:
+ * patches (k, P*P) fp32, positions (k, 2) int64 [h, w], channels (k) int64,
+ * scores (k) fp32 (nullable). */
+int dctae_patch_spectrum(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const float* x_dev, int32_t H, int32_t W,
+                         int32_t k, float* patches_dev, int64_t* positions_dev, int64_t* channels_dev,
+                         float* scores_dev, void* stream);
+
 /* PatchNorm.forward, eval/frozen (patchnorm.py:157-165) on n tokens of dim
  * P*P with their channel / position (int64 device arrays). Pad tokens are
  * normalised like the reference does (with c=h=w=0). */
@@ -274,20 +291,17 @@ int dctae_set_fft(dctae_ctx* ctx, int enable);
 int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
 
 /* Tuning / test knobs: "fft" (0/1), "fft_spec" (0/1: compile-time
- * specialised FFT kernels), "chunk_bytes", "workspace_limit" (bytes). */
+ * specialised FFT kernels), "chunk_bytes", "workspace_limit" (bytes),
+ * "rows_kernel" (3: k_rows512, 2: k_fft_rows2 for 512-wide rows),
+ * "sort_kernel" (2: rocPRIM radix, 1: bitonic), "fft_decode" (0/1),
+ * "xcd_order" (0/1); profiling only (outputs invalid): "rows_ablate",
+ * "t_alias". */
 int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
 
 /* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an
  * out-of-range channel / position / image id (the reference raises
  * IndexError there).  Synchronises `stream`. */
 int dctae_check_device_errors(dctae_ctx* ctx, void* stream);
-
-/* Diagnostics of the fused encode (k_enc_fused): copies the last launch's
- * dependence counters (24 queue/worker ints, then rows_done[n], cols_done[n])
- * into host_out (up to cap ints, synchronising the stream).  Returns the
- * number of ints available, 0 if the last encode was not fused.  No reference
- * counterpart (test / profiling aid). */
-int64_t dctae_fused_debug_counters(dctae_ctx* ctx, int32_t* host_out, int64_t cap, void* stream);
 
 /* Counter-based synthetic RGB images (same hash as oracle/rng.py):
  * value(seed, first_index + i, e) for i < n_img, images of (3, H, W)

@@ -274,6 +274,38 @@ def test_roundtrip_dct_idct(fe, shape):
         assert ok, dmax
 
 
+def _guard_band_flips(gcodes, ocodes, toks_o, ch, pos, tables, d):
+    """Code mismatches, each required to lie in the guard band: some element of
+    the mismatching codebook row has |x_oracle - median| <= 2 d + 1e-7, d = the
+    measured GPU-vs-oracle coefficient difference."""
+    diff = gcodes != ocodes
+    if not diff.any():
+        return 0
+    med = tables.median[ch, pos[:, 0], pos[:, 1]]
+    near = ((toks_o - med).abs() <= 2 * d + 1e-7).view(-1, 14, 14).any(-1)
+    assert torch.all(near[diff]), "code mismatch outside the guard band"
+    return int(diff.sum())
+
+
+def _check_image_vs_oracle(raw_g, codes_g, pos_g, ch_g, x_np, tables):
+    """One image's GPU tokens / codes against the oracle, per (c, h, w) key:
+    tokens within 2e-6 max|Y|, codes equal but inside the guard band.
+    Returns (flips, codes compared)."""
+    toks, opos, och, _ = _oracle_tokens(x_np)
+    omap = {_key(c, p): i for i, (p, c) in enumerate(zip(opos.tolist(), och.tolist()))}
+    gkeys = [_key(c, p) for p, c in zip(pos_g.tolist(), ch_g.tolist())]
+    assert len(set(gkeys)) == len(gkeys) and all(k in omap for k in gkeys)
+    oj = torch.tensor([omap[k] for k in gkeys])
+    toks_o = toks[oj]
+    d = (raw_g - toks_o).abs().max().item()
+    ymax = toks_o.abs().max().item()
+    assert d <= 2e-6 * ymax + 1e-6, (d, ymax)
+    y = ref_cpu.norm_forward_eval(tables, toks_o[None], och[oj][None], opos[oj, 0][None], opos[oj, 1][None])
+    _, oidx = ref_cpu.lfq_forward(y, ref_cpu.LFQConfig())
+    oidx = oidx[0]
+    return _guard_band_flips(codes_g, oidx, toks_o, och[oj], opos[oj], tables, d), codes_g.numel()
+
+
 def test_encode_512_full_size(fe, pn, lfq, ref_tables):
     """Config 3 image size: 2 x 512^2, codes vs oracle inside the guard band, order self-consistent."""
     xs = rng.synth_images(1234, [(512, 512)] * 2, 200)
@@ -282,16 +314,143 @@ def test_encode_512_full_size(fe, pn, lfq, ref_tables):
     assert dp.key_pad_mask.shape == (2, 3072) and not dp.key_pad_mask.any()
     sc = dp._data["scores"].cpu()
     assert torch.all(sc[:, 1:] <= sc[:, :-1])
-    ((ob, oidx),) = ref_cpu.encode([torch.from_numpy(a) for a in xs], CFG, ref_tables, ref_cpu.LFQConfig())
     raw, codes = dp.patches.cpu(), codes.cpu()
+    flips = n = 0
     for r in range(2):
-        gm = {_key(c, p): j for j, (p, c) in enumerate(zip(dp.patch_positions[r].tolist(), dp.patch_channels[r].tolist()))}
-        om = {_key(c, p): j for j, (p, c) in enumerate(zip(ob.patch_positions[r].tolist(), ob.patch_channels[r].tolist()))}
-        assert gm.keys() == om.keys()
-        gj = torch.tensor([gm[k] for k in om])
-        oj = torch.tensor(list(om.values()))
-        mism = (codes[r, gj] != oidx[r, oj]).sum().item()
-        assert mism <= 8, mism
+        f, m = _check_image_vs_oracle(raw[r], codes[r], dp.patch_positions[r].cpu(), dp.patch_channels[r].cpu(), xs[r],
+                                      ref_tables)
+        flips, n = flips + f, n + m
+    print(f"[512^2] code mismatches inside the guard band: {flips} / {n}")
+    assert flips <= max(2, n // 10000)
+
+
+def test_sq512_reference_codes(fe, pn, lfq, ref_tables):
+    """The headline config against the REFERENCE's own codes (case_sq512: the
+    reference run on the 512^2 image seed 1234 #100): per (c, h, w) token the
+    GPU's 14 codes equal the reference's, any mismatch inside the guard band;
+    the reference's stored 128-token head equals the oracle's tokens (to fp32
+    rounding: bit-equal on the build container's CPU)."""
+    g = golden("case_sq512.npz")
+    m = META["sq512"]
+    (x_np,) = rng.synth_images(m["seed"], [tuple(s) for s in m["sizes"]], m["first"])
+    ((dp, codes),) = fe.encode_batch(torch.from_numpy(x_np)[None].to(DEV), pn, lfq, return_raw=True)
+    raw, codes = dp.patches.cpu()[0], codes.cpu()[0]
+    gpos, gch = dp.patch_positions.cpu()[0], dp.patch_channels.cpu()[0]
+    rpos = torch.from_numpy(g["patch_positions"][0].astype(np.int64))
+    rch = torch.from_numpy(g["patch_channels"][0].astype(np.int64))
+    ridx = torch.from_numpy(g["indices"][0].astype(np.int64))
+    rmap = {_key(c, p): j for j, (p, c) in enumerate(zip(rpos.tolist(), rch.tolist()))}
+    gkeys = [_key(c, p) for p, c in zip(gpos.tolist(), gch.tolist())]
+    assert sorted(gkeys) == sorted(rmap)
+    rj = torch.tensor([rmap[k] for k in gkeys])
+    toks, opos, och, _ = _oracle_tokens(x_np)
+    omap = {_key(c, p): i for i, (p, c) in enumerate(zip(opos.tolist(), och.tolist()))}
+    toks_o = toks[torch.tensor([omap[k] for k in gkeys])]
+    head = torch.from_numpy(g["img0_patches_head"])
+    hk = [_key(c, p) for p, c in zip(g["img0_positions"][:128].astype(np.int64).tolist(),
+                                     g["img0_channels"][:128].astype(np.int64).tolist())]
+    # bit-equal in the build container; other host CPUs round the oracle's FFT differently
+    hd = (head - toks[torch.tensor([omap[k] for k in hk])]).abs().max().item()
+    assert hd <= 1e-6 * head.abs().max().item(), hd
+    d = (raw - toks_o).abs().max().item()
+    assert d <= 2e-6 * toks_o.abs().max().item(), d
+    flips = _guard_band_flips(codes, ridx[rj], toks_o, gch, gpos, ref_tables, d)
+    print(f"[sq512 vs reference codes] mismatches inside the guard band: {flips} / {codes.numel()}")
+    assert flips <= max(2, codes.numel() // 10000)
+
+
+@pytest.mark.parametrize("sizes", [[(1024, 1024)], [(1023, 997), (768, 1000)]])
+def test_large_ragged_vs_oracle(fe, pn, lfq, ref_tables, sizes):
+    """Config 4's upper sizes: 1024 x 1024 (runtime-plan FFT rows / columns),
+    1023 x 997 (odd, no FFT plan: MFMA GEMM both ways), 768 x 1000 (7-smooth
+    FFT plans of other radices): tokens and codes vs the oracle."""
+    xs = rng.synth_images(97, sizes)
+    ((dp, codes),) = fe.encode_batch([torch.from_numpy(a).to(DEV) for a in xs], pn, lfq, return_raw=True)
+    raw, codes = dp.patches.cpu(), codes.cpu()
+    kp, ids = dp.key_pad_mask.cpu(), dp.batched_image_ids.cpu()
+    slots = _image_slots(kp, ids)
+    assert len(slots) == len(xs)
+    flips = n = 0
+    for (r, im, tj), x_np in zip(slots, xs):
+        f, m = _check_image_vs_oracle(raw[r, tj], codes[r, tj], dp.patch_positions.cpu()[r, tj],
+                                      dp.patch_channels.cpu()[r, tj], x_np, ref_tables)
+        flips, n = flips + f, n + m
+    print(f"[{sizes}] code mismatches inside the guard band: {flips} / {n}")
+    assert flips <= max(2, n // 10000)
+
+
+@pytest.mark.parametrize("B,H", [(1024, 512), (256, 224)])
+def test_batch_encoder_matches_encode_batch(pkg, fe, pn, lfq, B, H):
+    """Full bench geometry (config 3: 1024 x 512^2; config 2: 256 x 224^2):
+    the pre-planned BatchEncoder equals encode_batch on a sampled subset of the
+    same images, bit for bit (codes, positions, channels; one image per row
+    at 512^2, four at 224^2)."""
+    from importlib import import_module
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    x = _ops().synth_images(B, H, H, seed=1234, first_index=0, device=DEV)
+    enc = fe_mod.BatchEncoder(fe, B, H, H, pn, lfq, device=DEV)
+    out = enc(x)
+    codes_b = out["codes"].clone()
+    pos_b, ch_b, ids_b, kp_b = out["positions"].clone(), out["channels"].clone(), out["image_ids"], out["key_pad_mask"]
+    assert not kp_b.all(-1).any()
+    sub = sorted(set([0, 1, B - 1] + list(range(5, B, max(1, B // 13)))))
+    ((dp, codes_s),) = fe.encode_batch([x[i] for i in sub], pn, lfq)
+    pl = enc.plan
+    k = enc.k
+    for n, i in enumerate(sub):
+        r, c0 = pl.row[i], pl.col[i]
+        rr, cc = _slot_of(dp, n)
+        assert torch.equal(codes_b[r, c0:c0 + k], codes_s[rr, cc:cc + k])
+        assert torch.equal(pos_b[r, c0:c0 + k], dp.patch_positions[rr, cc:cc + k])
+        assert torch.equal(ch_b[r, c0:c0 + k], dp.patch_channels[rr, cc:cc + k])
+        assert torch.all(ids_b[r, c0:c0 + k] == pl.local_id[i])
+
+
+def _slot_of(dp, n):
+    """(row, first column) of the n-th image (reference enumeration order) of a packed batch."""
+    kp, ids = dp.key_pad_mask.cpu(), dp.batched_image_ids.cpu()
+    (r, im, tj) = _image_slots(kp, ids)[n]
+    return r, int(tj[0])
+
+
+def test_to_dict_of_gpu_codes(pkg, fe, pn, lfq, ref_tables):
+    """HIP-encoded codes of the ragged case through to_dict give
+    the reference's JSON (ragged_to_dict.json, made by the reference's
+    dct_patches.to_dict): same images, sizes and per-(c, h, w) codes (a code
+    may differ only inside the guard band; token order compared as a map)."""
+    from importlib import import_module
+    dpm = import_module("dct_autoencoder_amd.dct_patches")
+    imgs = _case_images("ragged")
+    ((dp, codes),) = fe.encode_batch([torch.from_numpy(a).to(DEV) for a in imgs], pn, lfq, return_raw=True)
+    objs = json.loads(json.dumps(dpm.to_dict(dp, codes)))
+    ref = json.load(open(os.path.join(GOLDEN, "ragged_to_dict.json")))
+    assert len(objs) == len(ref)
+    flips = 0
+    for a, b in zip(objs, ref):
+        assert list(a["size"]) == list(b["size"]) and list(a["original_size"]) == list(b["original_size"])
+        ma = {(t["c"], t["h"], t["w"]): t["data"] for t in a["codes"]}
+        mb = {(t["c"], t["h"], t["w"]): t["data"] for t in b["codes"]}
+        assert ma.keys() == mb.keys()
+        flips += sum(x != y for k in ma for x, y in zip(ma[k], mb[k]))
+    assert flips <= 2, flips
+    # and back: from_dict of the GPU dump decodes like the packed batch
+    one, c1 = dpm.from_dict(objs[0])
+    assert c1.shape == (len(objs[0]["codes"]), 14)
+
+
+def test_revert_patching_vs_oracle(fe):
+    """FE.revert_patching (FE:607-656) of a packed ragged batch: each image's
+    (3, 14 ph, 14 pw) spectrum equals the oracle's, exactly (a scatter)."""
+    imgs = _case_images("ragged")
+    items = [fe.preprocess(torch.from_numpy(a).to(DEV)) for a in imgs]
+    (batch,) = list(fe.iter_batches(iter([{k: [it[k] for it in items] for k in items[0]}]), None))
+    got = fe.revert_patching(batch)
+    ob = ref_cpu.Batch(batch.patches.cpu(), batch.key_pad_mask.cpu(), None, batch.batched_image_ids.cpu(),
+                       batch.patch_channels.cpu(), batch.patch_positions.cpu(), batch.patch_sizes, batch.original_sizes)
+    want = ref_cpu.revert_patching(ob, CFG)
+    assert len(got) == len(want) == len(imgs)
+    for a, b in zip(got, want):
+        assert torch.equal(a.cpu(), b)
 
 
 def test_beta_sampling_matches_reference_k(pkg):
@@ -366,25 +525,12 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-DEFAULTS = {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 1, "t_layout": 0, "fused": 0, "fused_slots": 1,
-            "sort_kernel": 2, "chunk_bytes": 1 << 40, "dual_stream": 1}
+DEFAULTS = {"rows_kernel": 3, "sort_kernel": 2, "chunk_bytes": 1 << 40}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
-    "fused": {"fused": 1},
-    "cols_lds_scatter": {"cols_kernel": 2},
-    "cols_linear": {"cols_kernel": 4},
-    "cols_pairs": {"cols_kernel": 5},
-    "cols_multi4_pf": {"cols_kernel": 6, "cols_ipb": 4, "cols_pf": 1},
-    "cols_multi2_nopf": {"cols_kernel": 6, "cols_ipb": 2, "cols_pf": 0},
-    "cols_multi2_pf": {"cols_kernel": 6},
-    "cols_one_exchange4": {"cols_kernel": 7, "cols_ipb": 4, "cols_pf": 1},
-    "cols_one_exchange_nopf": {"cols_kernel": 7, "cols_ipb": 2, "cols_pf": 0},
+    "rows_lds": {"rows_kernel": 2},
     "sort_bitonic": {"sort_kernel": 1},
-    "chunks_dual_stream": {"chunk_bytes": 4 << 20, "dual_stream": 1},
-    "chunks_one_stream": {"chunk_bytes": 4 << 20, "dual_stream": 0},
-    "t_strips": {"t_layout": 1},
-    "t_strips16": {"t_layout": 2},
-    "t_rowmajor_pad16": {"t_layout": 3},
+    "chunks": {"chunk_bytes": 4 << 20},
 }
 
 
@@ -418,43 +564,6 @@ def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
         a, b = dp_s.patches.cpu()[r, sj], dp_g.patches.cpu()[r, gj]
         assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item()
         assert (c_s.cpu()[r, sj] != c_g.cpu()[r, gj]).sum().item() <= 4
-
-
-@pytest.mark.parametrize("rep", [0, 1, 2])
-@pytest.mark.parametrize("shape,n", [((512, 512), 27), ((224, 224), 70)])
-def test_fused_matches_unfused_bitwise(fe, pn, lfq, shape, n, rep):
-    """k_enc_fused (rows and columns in one persistent launch, T handed over
-    through the XCD's L2 ring slots) runs the same arithmetic as the two
-    separate kernels: every output bit-identical.  n > 8 XCD queues, so every
-    ring slot is reused (write-after-read hand-off) several times; repeated on
-    fresh inputs (2-3 slots showed intermittent mismatches and are refused).
-    The fused kernel runs the column item of cols_kernel 7 (512^2) / 4 (224^2),
-    so the unfused leg is pinned to that column kernel (the other column
-    kernels order the complex maths differently: last-ulp differences in the
-    coefficients, codes agree either way)."""
-    ops = _ops()
-    x = torch.from_numpy(np.stack(rng.synth_images(61 + rep, [shape] * n))).to(DEV)
-    ops.set_option("cols_kernel", 7)
-    try:
-        outs = {}
-        for fused in (1, 0):
-            ops.set_option("fused", fused)
-            outs[fused] = [fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True),
-                           fe.encode_batch(x, pn, lfq)]
-        ops.check_device_errors(x.device)
-    finally:
-        ops.set_option("fused", 0)
-        ops.set_option("cols_kernel", DEFAULTS["cols_kernel"])
-    for (a_list, b_list) in zip(outs[1], outs[0]):
-        for (dp_a, c_a), (dp_b, c_b) in zip(a_list, b_list):
-            assert torch.equal(c_a, c_b)
-            assert torch.equal(dp_a.patch_positions, dp_b.patch_positions)
-            assert torch.equal(dp_a.patch_channels, dp_b.patch_channels)
-            assert torch.equal(dp_a.batched_image_ids, dp_b.batched_image_ids)
-            assert torch.equal(dp_a.key_pad_mask, dp_b.key_pad_mask)
-            assert torch.equal(dp_a.patches.view(torch.int32), dp_b.patches.view(torch.int32))
-            if dp_a._data:
-                assert torch.equal(dp_a._data["scores"].view(torch.int32), dp_b._data["scores"].view(torch.int32))
 
 
 def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables):
