@@ -237,11 +237,12 @@ class DCTAutoencoder(nn.Module):
             self._packed_key = key
         return self._packed
 
-    def _check_mode(self, dev=None):
+    def _check_mode(self, dp: Optional[DCTPatches] = None):
         if self.training:
             raise NotImplementedError("DCTAutoencoder training (losses, backward) is not on the MI355X path: "
                                       "call .eval()")
-        if dev is not None:
+        if dp is not None:
+            dev = dp.patches.device
             # kernels take raw device pointers: a parameter left on another device (or the
             # CPU) would be read as garbage, so refuse it like torch's device mismatch error
             for n, p in self.named_parameters():
@@ -323,7 +324,7 @@ class DCTAutoencoder(nn.Module):
     # ---- modeling:119-200 ----
     @torch.no_grad()
     def encode(self, dct_patches: DCTPatches, do_normalize: bool = False):
-        self._check_mode(dct_patches.patches.device)
+        self._check_mode(dct_patches)
         if do_normalize:
             dct_patches = self.normalize_(dct_patches)
         pk = self._weights()
@@ -393,7 +394,7 @@ class DCTAutoencoder(nn.Module):
 
     @torch.no_grad()
     def decode(self, x: DCTPatches, do_inv_norm: bool = False) -> DCTPatches:
-        self._check_mode(x.patches.device)
+        self._check_mode(x)
         pk = self._weights()
         r, s, d = x.patches.shape
         dev = x.patches.device
