@@ -262,9 +262,6 @@ def main():
     torch.cuda.synchronize(dev)
 
     timing = not args.no_kernel_timing
-    if timing:
-        ctx.lib.dctae_timing_reset(ctx.h)
-        ctx.lib.dctae_set_timing(ctx.h, 1)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -275,8 +272,14 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    ops.check_device_errors(dev)   # raises if a fused-kernel dependence wait timed out
+    ops.check_device_errors(dev)
     if timing:
+        # per-kernel device times (HIP events around each launch, on its stream) in a
+        # separate pass: the event records stay out of the timed region above
+        ctx.lib.dctae_timing_reset(ctx.h)
+        ctx.lib.dctae_set_timing(ctx.h, 1)
+        for _ in range(args.steps):
+            enc(x)
         ctx.lib.dctae_set_timing(ctx.h, 0)
         ctx.lib.dctae_timing_collect(ctx.h)
     el_t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -344,9 +347,6 @@ def main():
             for _ in range(args.warmup):
                 dec(packed)
             torch.cuda.synchronize(dev)
-            if timing:
-                ctx.lib.dctae_timing_reset(ctx.h)
-                ctx.lib.dctae_set_timing(ctx.h, 1)
             if dist:
                 dist.barrier()
             torch.cuda.synchronize(dev)
@@ -361,6 +361,10 @@ def main():
             dk = {}
             if timing:
                 import ctypes as C
+                ctx.lib.dctae_timing_reset(ctx.h)
+                ctx.lib.dctae_set_timing(ctx.h, 1)
+                for _ in range(args.steps):
+                    dec(packed)
                 ctx.lib.dctae_set_timing(ctx.h, 0)
                 ctx.lib.dctae_timing_collect(ctx.h)
                 i = 0

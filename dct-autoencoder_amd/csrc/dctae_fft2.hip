@@ -7,6 +7,7 @@
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
 #include "dctae_launch.h"
+#include "dctae_spec512.h"
 
 
 namespace dctae {
@@ -26,15 +27,6 @@ struct RowsLds {
   static constexpr int MP = pad16(M - 1) + 2;
   float2 z[4][3][MP];
 };
-
-// threadIdx.x through a volatile asm: not loop-invariant to the compiler, so
-// the lane-derived LDS addresses of an item body are rebuilt per item instead
-// of being hoisted out of a multi-image loop (and kept live in VGPRs)
-__device__ __forceinline__ int opaque_tid() {
-  int t;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
-  return t;
-}
 
 template <int N, int R1, int R2>
 __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const float* __restrict__ rgb,
@@ -390,90 +382,6 @@ __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, c
 }
 
 // ---------------------------------------------------------------------------
-// Column pieces of N = 512 (P = 14) used by k_fft_cols7: the LFQ thresholds of
-// a thread's epilogue rows and the token epilogue.
-// ---------------------------------------------------------------------------
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// Thresholds of this thread's epilogue rows: tiles h = g16 + 16 r, row jl.
-template <bool THR>
-__device__ __forceinline__ void cols_thresholds(const ImgDesc& d, int c, int strip, const EncParams& ep,
-                                                 float2 (&thr_r)[2][7], float* sbias) {
-  constexpr int KS = 14, EPR = 2;
-  const int tid = opaque_tid();
-  const int g16 = tid >> 4, jl = tid & 15;
-  if (THR) {
-#pragma unroll
-    for (int r = 0; r < EPR; ++r) {
-      const int h = g16 + 16 * r;
-      if (h < d.qh && jl < KS) {
-        const float2* t2 = reinterpret_cast<const float2*>(
-            ep.thr + ((((int64_t)c * ep.maxph + h) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jl * KS);
-#pragma unroll
-        for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
-      }
-    }
-  }
-  if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
-}
-
-// token epilogue of one (channel, tile column) item: X2 = the 448 x 14 kept
-// coefficients (float index k * 14 + col) in LDS; tile (h, strip) per 16-lane
-// group g16 (+16 r), tile row jl; codes from the thresholds held in registers
-template <bool THR>
-__device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip, const f2v* X2, const float* sbias,
-                                               const float2 (&thr_r)[2][7], const EncParams& ep,
-                                               const TokenSinks& sk) {
-  constexpr int KS = 14, EPR = 2;
-  const int tid = opaque_tid();
-  const int g16 = tid >> 4, jl = tid & 15;
-  if (THR) {
-#pragma unroll
-    for (int r = 0; r < EPR; ++r) {
-      const int h = g16 + 16 * r;
-      if (h < d.qh) {
-        const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
-        uint32_t am = 0, code = 0;
-#pragma unroll
-        for (int p = 0; p < KS / 2; ++p) {
-          const f2v v2 = row[p];
-          am = max(am, max(__float_as_uint(v2.x) & 0x7fffffffu, __float_as_uint(v2.y) & 0x7fffffffu));
-          code |= (v2.x >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
-          code |= (v2.y >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
-        }
-        am = jl < KS ? am : 0u;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
-        const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
-        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
-        if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
-        if (sk.raw && jl < KS) {
-#pragma unroll
-          for (int p = 0; p < KS / 2; ++p) {
-            const f2v v2 = row[p];
-            sk.raw[tok * KS * KS + jl * KS + 2 * p] = v2.x;
-            sk.raw[tok * KS * KS + jl * KS + 2 * p + 1] = v2.y;
-          }
-        }
-      }
-    }
-  } else {
-    for (int h = g16; h < d.qh; h += 16) {
-      float vals[KS];
-      const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
-#pragma unroll
-      for (int p = 0; p < KS / 2; ++p) {
-        const f2v v2 = row[p];
-        vals[2 * p] = v2.x;
-        vals[2 * p + 1] = v2.y;
-      }
-      const int f = (h * d.qw + strip) * ep.C + c;
-      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // cols7 (N = 512): the column FFT with ONE LDS exchange.  Lane (w, g, col) =
 // (wave, 16-lane row, column of the strip; col 14, 15 idle).
 //  * pass 1: butterfly j1 = 4w + g reads z[j1 + 16 r] straight from T in
@@ -490,15 +398,6 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
 // (a permutation): the two 16-lane rows of a ds_read_b64 half-wave
 // (j2 = a, 16 - a: bit 3 differs) fall on opposite 32-bank halves.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ constexpr int z7addr(int m) { return 16 * (m ^ ((m >> 3) & 1)); }
-
-__device__ __forceinline__ int cols7_j2(int w, int g) {
-  // wave 0: 0, 8, 1, 15;  wave w > 0: 2w, 16 - 2w, 2w + 1, 15 - 2w
-  const int a = (g & 2) ? 2 * w + 1 : 2 * w;
-  const int base = (w == 0 && g < 2) ? (g ? 8 : 0) : ((g & 1) ? (g & 2 ? 15 - 2 * w : 16 - 2 * w) : a);
-  return base;
-}
-
 __device__ __forceinline__ float partner_row(float x, bool even_row) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(even_row ? r[1] : r[0]);
@@ -509,32 +408,6 @@ union Cols7Lds {
   float2 z[256 * 16];
   float X[448 * 14];
 };
-
-__device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
-                                           float (&va)[16], float (&vb)[16]) {
-  constexpr int N = 512;
-  const int tid = opaque_tid();
-  const int j1 = tid >> 4, col = min(tid & 15, 13);
-  const int rs = d.Kw;
-  // buffer descriptor on the (channel, tile column) slice: 32-bit lane offsets, uniform row steps
-  const float* cb = T + (int64_t)c * N * rs + strip * 14;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cb), 0, N * rs * 4, 0x00020000);
-  // m = j1 + 16 r: rows 4m (+2) for r < 8, 2N - 1 - 4m (-2) above; 64-row steps
-  const int lo = (4 * j1 * rs + col) * 4;
-  const int hi = ((2 * N - 1 - 4 * j1 - 64 * 15) * rs + col) * 4;   // r = 15: lowest row of the upper half
-  const int step = 64 * rs * 4, two = 2 * rs * 4;
-  constexpr int aux = 0;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo, r * step, aux));
-    vb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo + two, r * step, aux));
-  }
-#pragma unroll
-  for (int r = 8; r < 16; ++r) {
-    va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, hi, (15 - r) * step, aux));
-    vb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, hi - two, (15 - r) * step, aux));
-  }
-}
 
 // Makhoul post of cols7 for one lane: v = Z[j2 + 16 i]; writes X[k], X[N - k]
 // (Kh = 448: X[N - k] kept for k > 64) and X[M] (j2 = 0).  W0: wave 0, whose
@@ -614,6 +487,8 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
     }
     DFTV<16>::run(v);
   }
+  // X aliases z: every wave's pass-2 reads of z must be done before any post writes X
+  __syncthreads();
   // ---- Makhoul post: k = j2 + 16 i; A = Z[k], B = conj Z[M - k]
   //      j2 >= 1: Z[M - k] = partner row's v[15 - i] (lane ^ 16, ds_swizzle);
   //      j2 = 0: own v[(16 - i) & 15];  j2 = 8: own v[15 - i]  (wave 0, rows 0 and 1)

@@ -200,3 +200,24 @@ def test_model_forward_roundtrip_shapes(pkg, golden_model):
     assert out["dct_patches"].patches.shape == t["decoded"].shape
     assert out["codes"].shape == t["codes"].shape and out["codes"].dtype == torch.long
     assert torch.isfinite(out["dct_patches"].patches).all()
+
+
+def test_model_half_and_device_checks(pkg, golden_model):
+    """The reference's loader casts the model to fp16 (factory.py:36-64,
+    prepare_autoregressive_dataset.py): the kernels then get fp32 copies of
+    the LayerNorm / position / bias operands, so the forward stays sane and
+    its codes match the fp32 model's except near zero; a model left on the CPU
+    is refused instead of handing host pointers to the kernels."""
+    import copy
+    m, w, t, c = golden_model
+    mh = copy.deepcopy(m).half()
+    ref_codes = m.encode(_dp(pkg, t, t["patches_in"].to(DEV)))[1]
+    dp, codes, _, _ = mh.encode(_dp(pkg, t, t["patches_in"].to(DEV)))
+    torch.cuda.synchronize()
+    assert torch.isfinite(dp.patches.float()).all()
+    mask = 2 ** torch.arange(c["cbd"] - 1, -1, -1, device=DEV)
+    differ = (((codes[..., None] & mask) != 0) != ((ref_codes[..., None] & mask) != 0)).float().mean().item()
+    assert differ < 0.02, differ
+    cpu_model = copy.deepcopy(m).cpu()
+    with pytest.raises(RuntimeError):
+        cpu_model.encode(_dp(pkg, t, t["patches_in"].to(DEV)))
