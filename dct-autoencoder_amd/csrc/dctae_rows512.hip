@@ -47,8 +47,14 @@ __device__ __forceinline__ float ipt_pow(float x) {
   return __builtin_copysignf(y, x);
 }
 
+// transpose region of one row group: re plane at 0, im plane at + 256; 528
+// floats apart (16 mod 32 banks), so the two row groups of a 32-lane
+// ds_write_b32 land on opposite bank halves; the b128 reads stay conflict-free
+// (a 16-bank shift keeps each lane group's 4-bank sets distinct)
+constexpr int kXchStride = 528;
+
 struct Rows512Lds {
-  float xch[4][4][2][256];   // [wave][row group][re / im][transpose slot]
+  float xch[4][4][kXchStride];   // [wave][row group][re 256 | im 256 | pad]
   float2 tw2[16][16];        // W_256^{r s}
   float4 pc[257];            // Makhoul post coefficients (c1, c2, c3, c4), see below
 };
@@ -129,8 +135,8 @@ __global__ __launch_bounds__(256) void k_rows512(const ImgDesc* __restrict__ img
   }
   __syncthreads();   // tables
 
-  float* xre = L.xch[wv][g][0];
-  float* xim = L.xch[wv][g][1];
+  float* xre = L.xch[wv][g];
+  float* xim = L.xch[wv][g] + 256;
   const bool lane0 = (j == 0);
   // T stores: buffer stores on the channel plane (H x KW floats); rows y >= H
   // (and every store under ablate & 1) fall outside num_records and are dropped
