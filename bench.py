@@ -194,8 +194,32 @@ def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
     torch.cuda.synchronize(dev)
     el = (time.perf_counter() - t0) / n4
     pix = int((hw[:, 0] * hw[:, 1]).sum())
+    lib = import_module("dct_autoencoder_amd._lib")
+    kern = kernel_times(lib.context(dev), lambda: fe.encode_batch(imgs, pn, lfq), 1)
     out["config4"] = {"workload": "1024 ragged images, (H, W) ~ U{14..1024}^2 seed 7, encode_batch incl. host packing",
-                      "ms_per_step": round(el * 1e3, 3), "value": round(pix / el / 1e6, 1), "unit": "Mpix/s"}
+                      "ms_per_step": round(el * 1e3, 3), "value": round(pix / el / 1e6, 1), "unit": "Mpix/s",
+                      "kernels": kern,
+                      "device_ms": round(sum(v["total_ms"] for v in kern.values()), 3)}
+    return out
+
+
+def kernel_times(ctx, fn, n):
+    """Per-kernel device times of n calls of fn (HIP events around each launch
+    on its own stream, dctae_set_timing), outside any timed region."""
+    import ctypes as C
+    ctx.lib.dctae_timing_reset(ctx.h)
+    ctx.lib.dctae_set_timing(ctx.h, 1)
+    for _ in range(n):
+        fn()
+    ctx.lib.dctae_set_timing(ctx.h, 0)
+    ctx.lib.dctae_timing_collect(ctx.h)
+    out, i = {}, 0
+    while True:
+        name, ms, cnt = C.c_char_p(), C.c_double(), C.c_int64()
+        if ctx.lib.dctae_timing_get(ctx.h, i, C.byref(name), C.byref(ms), C.byref(cnt)) != 0:
+            break
+        out[name.value.decode()] = {"total_ms": round(ms.value / n, 4), "launches": int(cnt.value) // n}
+        i += 1
     return out
 
 

@@ -1,6 +1,7 @@
 // C ABI of libdctae.so: context, planning, workspace and launch sequencing.
 // See include/dctae.h for the contract of every entry point.
 #include <cmath>
+#include <complex>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -56,10 +57,14 @@ struct dctae_ctx {
   float2* fft_tab = nullptr;
   int64_t fft_tab_cap = 0, fft_tab_used = 0;
   std::map<int, FftPlan> fft_plans;   // N -> plan (N = 0 entries never stored)
+  std::map<int, FftPlan> bs_plans;    // N -> Bluestein plan (kind 1; kind 0 = none)
+  std::map<int, int64_t> bs_tw;       // L -> offset of W_L^m in fft_tab
   bool fft_enabled = true;
+  bool bluestein = true;              // lengths without a Makhoul plan: Bluestein FFT (else the MFMA GEMM)
   bool fft_spec_enabled = true;
   int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
   int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)
+  int bs_ablate = 0;                  // profiling only: Bluestein kernels skip 1 loads, 2 FFTs, 4 post (wrong output)
   int rows_kernel = 3;                // 512-wide rows: 3 = k_rows512 (registers + one LDS transpose), 2 = k_fft_rows2
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
@@ -367,6 +372,116 @@ int next_pow2(int x) {
   return p;
 }
 
+// Room for `need` more float2 in the FFT table buffer; grows it (the offsets
+// stay valid) after draining the device, since launches in flight may read it.
+int tab_reserve(dctae_ctx* ctx, int64_t need) {
+  if (ctx->fft_tab_used + need <= ctx->fft_tab_cap) return 0;
+  const int64_t cap = std::max(2 * ctx->fft_tab_cap, ctx->fft_tab_used + need);
+  float2* t = nullptr;
+  if (hipMalloc((void**)&t, cap * sizeof(float2)) != hipSuccess) return -1;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(t, ctx->fft_tab, ctx->fft_tab_used * sizeof(float2), hipMemcpyDeviceToDevice) != hipSuccess) {
+    hipFree(t);
+    return -1;
+  }
+  hipFree(ctx->fft_tab);
+  ctx->fft_tab = t;
+  ctx->fft_tab_cap = cap;
+  return 0;
+}
+
+int64_t tab_put(dctae_ctx* ctx, const std::vector<float2>& h) {
+  if (tab_reserve(ctx, (int64_t)h.size())) return -1;
+  if (hipMemcpy(ctx->fft_tab + ctx->fft_tab_used, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice) !=
+      hipSuccess)
+    return -1;
+  const int64_t o = ctx->fft_tab_used;
+  ctx->fft_tab_used += (int64_t)h.size();
+  return o;
+}
+
+// in-place radix-2 FFT in float64 (host tables only), e^{-2 pi i nk / L}
+void fft_f64(std::vector<std::complex<double>>& a) {
+  const int L = (int)a.size();
+  for (int i = 1, j = 0; i < L; ++i) {
+    int bit = L >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) std::swap(a[i], a[j]);
+  }
+  const double pi = 3.14159265358979323846;
+  for (int len = 2; len <= L; len <<= 1)
+    for (int i = 0; i < L; i += len)
+      for (int k = 0; k < len / 2; ++k) {
+        const std::complex<double> w = std::polar(1.0, -2.0 * pi * k / len);
+        const std::complex<double> u = a[i + k], v = a[i + k + len / 2] * w;
+        a[i + k] = u + v;
+        a[i + k + len / 2] = u - v;
+      }
+}
+
+// Bluestein plan for length N (dctae_bluestein.hip): tables in float64 -> fp32;
+// -1 outside N in [32, 1024] or with the option off
+int bs_plan_for(dctae_ctx* ctx, int N, FftPlan* out) {
+  if (!ctx->fft_enabled || !ctx->bluestein || N < 32 || N > 1024) return -1;
+  auto it = ctx->bs_plans.find(N);
+  if (it != ctx->bs_plans.end()) {
+    *out = it->second;
+    return it->second.kind == 1 ? 0 : -1;
+  }
+  FftPlan p{};
+  p.N = N;
+  p.M = N / 2;
+  int L = 256;
+  while (L < 2 * N - 1) L <<= 1;
+  const double pi = 3.14159265358979323846;
+  auto bad = [&]() {
+    ctx->bs_plans[N] = p;  // kind 0: no Bluestein plan for N
+    return -1;
+  };
+  auto tw_it = ctx->bs_tw.find(L);
+  if (tw_it == ctx->bs_tw.end()) {
+    std::vector<float2> tw(L);
+    for (int m = 0; m < L; ++m) {
+      const double a = -2.0 * pi * m / L;
+      tw[m] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    const int64_t o = tab_put(ctx, tw);
+    if (o < 0) return bad();
+    tw_it = ctx->bs_tw.emplace(L, o).first;
+  }
+  std::vector<std::complex<double>> c(N), b(L, 0.0);
+  for (int n = 0; n < N; ++n) c[n] = std::polar(1.0, -pi * (double)(((int64_t)n * n) % (2 * N)) / N);
+  for (int m = 0; m < N; ++m) {
+    b[m] = std::conj(c[m]);
+    if (m) b[L - m] = std::conj(c[m]);
+  }
+  fft_f64(b);
+  std::vector<float2> h(2 * N + L);
+  for (int n = 0; n < N; ++n) h[n] = make_float2((float)c[n].real(), (float)c[n].imag());
+  for (int m = 0; m < L; ++m) h[N + m] = make_float2((float)(b[m].real() / L), (float)(b[m].imag() / L));
+  for (int k = 0; k < N; ++k) {
+    const double sk = (k == 0) ? std::sqrt(1.0 / N) : std::sqrt(2.0 / N);
+    const std::complex<double> e = std::polar(0.5 * sk, -pi * k / (2.0 * N));
+    h[N + L + k] = make_float2((float)e.real(), (float)e.imag());
+  }
+  const int64_t o = tab_put(ctx, h);
+  if (o < 0) return bad();
+  p.kind = 1;
+  p.bs_L = L;
+  p.npass = 1;
+  p.bs_tw_off = tw_it->second;
+  p.bs_chirp_off = o;
+  p.bs_bhat_off = o + N;
+  p.bs_post_off = o + N + L;
+  ctx->bs_plans[N] = p;
+  *out = p;
+  return 0;
+}
+
+int bs_lidx(int L) { return L == 256 ? 0 : L == 512 ? 1 : L == 1024 ? 2 : 3; }
+constexpr int kBsL[4] = {256, 512, 1024, 2048};
+
 // FFT plan for length N (Makhoul: M = N/2 point complex FFT); -1 if N has no plan
 int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   if (!ctx->fft_enabled || N < 4 || (N & 1) || N / 2 > 512) return -1;
@@ -403,7 +518,7 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   // rows per block of k_fft_rows: 2 (ping-pong) x rows x 3 jobs x (2M+1) floats <= 52 KiB
   p.rows_per_block = std::max(1, std::min(8, (int)(53248 / (24 * (2 * p.M + 1)))));
   const int64_t need = p.M + 2ll * (p.M + 1) + 2ll * p.M;
-  if (ctx->fft_tab_used + need > ctx->fft_tab_cap) {
+  if (tab_reserve(ctx, need)) {
     p.npass = 0;
     ctx->fft_plans[N] = p;
     return -1;
@@ -467,7 +582,9 @@ struct ChunkJob {
   int n_rows_tiles, n_cols_tiles;
   size_t pc_off;      // k_fft_cols7 list: the spec-1 images of the job (one tile-column count qw)
   int n_pc, pc_qw;
-  int max_T, any_gemm_rows, any_gemm_cols, fold_t;
+  int max_T, any_gemm_rows, any_gemm_cols, fold_t, any_bs_cols;
+  size_t br_off[4], bc_off[4];   // Bluestein row / column blocks per L = 256 .. 2048
+  int n_br[4], n_bc[4];
   int64_t max_hw;
   size_t lds_rows, lds_cols;
 };
@@ -596,11 +713,13 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   const std::string k(key);
   if (k == "fft") ctx->fft_enabled = value != 0;
   else if (k == "fft_spec") ctx->fft_spec_enabled = value != 0;
+  else if (k == "bluestein") ctx->bluestein = value != 0;
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
   else if (k == "t_alias" && value >= 0) ctx->t_alias = (int)value;
   else if (k == "rows_ablate" && value >= 0 && value <= 3) ctx->rows_ablate = (int)value;
+  else if (k == "bs_ablate" && value >= 0 && value <= 7) ctx->bs_ablate = (int)value;
   else if (k == "rows_kernel" && (value == 2 || value == 3)) ctx->rows_kernel = (int)value;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
@@ -711,7 +830,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     if (it != plan_idx.end()) return it->second;
     FftPlan p;
     int idx = -1;
-    if (fft_plan_for(ctx, N, P, &p) == 0) {
+    if (fft_plan_for(ctx, N, P, &p) == 0 || bs_plan_for(ctx, N, &p) == 0) {
       idx = (int)plans.size();
       plans.push_back(p);
     }
@@ -733,6 +852,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     }
     D[i].plan_w = plan_of(D[i].W);
     D[i].plan_h = plan_of(D[i].H);
+    D[i].bs = (D[i].plan_w >= 0 && plans[D[i].plan_w].kind == 1 ? 1 : 0) |
+              (D[i].plan_h >= 0 && plans[D[i].plan_h].kind == 1 ? 2 : 0);
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
@@ -742,7 +863,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   auto ws_of = [&](const ImgDesc& d) {
     int64_t w = 3ll * d.Kw * d.H + 64;
     if (d.plan_w < 0) w += 3ll * d.H * d.W + 64;
-    if (d.plan_h < 0) w += 3ll * d.Kh * d.Kw + 64;
+    if (d.plan_h < 0 || (d.bs & 2)) w += 3ll * d.Kh * d.Kw + 64;
     return w * 4;
   };
   auto st_of = [&](const ImgDesc& d) {
@@ -787,7 +908,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       d.ws_p = wsf;
       if (d.plan_w < 0) wsf += up(3ll * d.H * d.W);
       d.ws_y = wsf;
-      if (d.plan_h < 0) wsf += up(3ll * d.Kh * d.Kw);
+      if (d.plan_h < 0 || (d.bs & 2)) wsf += up(3ll * d.Kh * d.Kw);
       d.tok_off = full ? tok : tok_off_user[i];
       tok += d.T;
       j.max_T = std::max(j.max_T, d.T);
@@ -811,6 +932,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     std::vector<TileRef> rt, ct;
     std::vector<int2> fr[kVariants];
     std::vector<int4> fc[kVariants];
+    std::vector<int2> br[4];
+    std::vector<int4> bc[4];
     std::vector<int32_t> pc;
     int pc_qw = 0;
     bool pc_ok = true;
@@ -836,6 +959,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           probs.push_back(g);
         }
         j.any_gemm_rows = 1;
+      } else if (d.bs & 1) {
+        const int L = plans[d.plan_w].bs_L, rpb = bs_rows_per_block(L);
+        for (int y0 = 0; y0 < d.H; y0 += rpb) br[bs_lidx(L)].push_back(make_int2(li, y0));
       } else {
         const FftPlan& p = plans[d.plan_w];
         for (int y0 = 0; y0 < d.H; y0 += p.rows_per_block) fr[p.spec].push_back(make_int2(li, y0));
@@ -864,6 +990,11 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         }
         j.any_gemm_cols = 1;
         if (d.plan_w >= 0) j.fold_t = 1;
+      } else if (d.bs & 2) {
+        const int L = plans[d.plan_h].bs_L, cpb = bs_cols_per_block(L);
+        for (int c = 0; c < 3; ++c)
+          for (int kx0 = 0; kx0 < d.Kw; kx0 += cpb) bc[bs_lidx(L)].push_back(make_int4(li, c, kx0, 0));
+        j.any_bs_cols = 1;
       } else {
         const FftPlan& p = plans[d.plan_h];
         // generic kernel: one tile column per block; specialised: groups of
@@ -922,6 +1053,12 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.n_fr[v] = (int)fr[v].size();
       j.n_fc[v] = (int)fc[v].size();
     }
+    for (int l = 0; l < 4; ++l) {
+      j.br_off[l] = E.pb.add(br[l].data(), br[l].size());
+      j.bc_off[l] = E.pb.add(bc[l].data(), bc[l].size());
+      j.n_br[l] = (int)br[l].size();
+      j.n_bc[l] = (int)bc[l].size();
+    }
     j.n_rows_tiles = (int)rt.size();
     j.n_cols_tiles = (int)ct.size();
     // all spec-1 column items of the job in one persistent launch, when their qw agree
@@ -967,8 +1104,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.reserve(16 + 6ll * n + (full ? pack->n_rows : 0));
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
-                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 64 * ctx->t_alias +
-                             1024 * ctx->xcd_order,
+                         (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
+                             64 * ctx->t_alias + 1024 * ctx->xcd_order,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1057,6 +1194,12 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       Timer t(ctx, st, "gemm_rows");
       launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st);
     }
+    for (int l = 0; l < 4; ++l)
+      if (j.n_br[l]) {
+        Timer t(ctx, st, "bs_rows");
+        launch_bs_rows(kBsL[l], dd, plans_d, (const int2*)(pd + j.br_off[l]), j.n_br[l], imgs->rgb_dev, ctx->ws,
+                       ctx->fft_tab, ctx->cm, st, ctx->bs_ablate);
+      }
     if (j.n_fr[0]) {
       Timer t(ctx, st, "fft_rows");
       launch_fft_rows(dd, plans_d, (const int2*)(pd + j.fr_off[0]), j.n_fr[0], j.lds_rows, imgs->rgb_dev, ctx->ws,
@@ -1081,10 +1224,16 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         Timer t(ctx, st, "fold_t");
         launch_fold_t(dd, nj, j.max_hw, ctx->ws, st);
       }
-      {
-        Timer t(ctx, st, "gemm_cols");
-        launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st);
+      Timer t(ctx, st, "gemm_cols");
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st);
+    }
+    for (int l = 0; l < 4; ++l)
+      if (j.n_bc[l]) {
+        Timer t(ctx, st, "bs_cols");
+        launch_bs_cols(kBsL[l], dd, plans_d, (const int4*)(pd + j.bc_off[l]), j.n_bc[l], ctx->ws, ctx->fft_tab, st,
+                       ctx->bs_ablate);
       }
+    if (j.any_gemm_cols || j.any_bs_cols) {
       Timer t(ctx, st, "tile_epilogue");
       launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, st);
     }

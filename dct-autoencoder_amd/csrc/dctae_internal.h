@@ -30,7 +30,8 @@ struct ImgDesc {
   int32_t T;         // tokens = C*qh*qw
   int32_t row, col, k, local_id;  // packing
   int32_t plan_w, plan_h;         // FFT plan index for rows (length W) / cols (length H); -1 = GEMM
-  int32_t pad0, pad1;
+  int32_t bs;        // bit 0: rows, bit 1: columns on the Bluestein kernels (columns: Y + k_tile_epilogue)
+  int32_t pad1;
 };
 
 // Generic batched strided fp32 GEMM problem:
@@ -55,6 +56,12 @@ struct FftPlan {
   int64_t tw_off;    // float2 offset of W_M^k (k < M) in the FFT table buffer
   int64_t post_off;  // float2 offset of (alpha_k, beta_k), k = 0..M
   int64_t ipre_off;  // float2 offset of the DCT-III pre-processing table (conj a_k, conj b_k), k < M (dctae_idct.hip)
+  // Bluestein plans (kind 1, dctae_bluestein.hip): any N in [32, 1024], L = 2^ceil(log2(2N - 1)) >= 256
+  int32_t kind, bs_L;
+  int64_t bs_tw_off;     // W_L^m, m < L
+  int64_t bs_chirp_off;  // c[n] = e^{-i pi n^2 / N}, n < N
+  int64_t bs_bhat_off;   // FFT_L(conj c) / L
+  int64_t bs_post_off;   // e_k = s_k / 2 e^{-i pi k / (2N)}, k < N
 };
 
 struct TileRef {

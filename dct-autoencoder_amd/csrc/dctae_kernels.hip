@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict
                                                        TokenSinks sk) {
   __shared__ uint16_t rowbits[16 * kMaxP];
   const ImgDesc d = imgs[blockIdx.y];
-  if (d.plan_h >= 0) return;  // columns of this image run through k_fft_cols (epilogue fused there)
+  if (d.plan_h >= 0 && !(d.bs & 2)) return;  // columns on the Makhoul FFT kernels (epilogue fused there)
   const int g16 = threadIdx.x >> 4, j = threadIdx.x & 15;
   const float* Y = ws + d.ws_y;
   for (int pass = 0; pass < 4; ++pass) {
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restri
                                                          TokenSinks sk) {
   extern __shared__ float ys[];
   const ImgDesc d = imgs[blockIdx.y];
-  if (d.plan_h >= 0) return;
+  if (d.plan_h >= 0 && !(d.bs & 2)) return;
   const int c = blockIdx.x % 3, h = blockIdx.x / 3;
   if (h >= d.qh) return;
   const int Kw = d.Kw, ld = Kw + 1;

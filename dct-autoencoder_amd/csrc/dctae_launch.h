@@ -78,4 +78,13 @@ void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const
 
 int cols7_grid(int n_list, int qw, int ipb);
 
+// Bluestein DCT for lengths without a Makhoul plan (dctae_bluestein.hip)
+int bs_rows_per_block(int L);
+int bs_cols_per_block(int L);
+void launch_bs_rows(int L, const ImgDesc* imgs, const FftPlan* plans, const int2* blocks, int n_blocks,
+                    const float* rgb, float* ws, const float2* tabs, const ColorMats& cm, hipStream_t s,
+                    int ablate = 0);
+void launch_bs_cols(int L, const ImgDesc* imgs, const FftPlan* plans, const int4* blocks, int n_blocks, float* ws,
+                    const float2* tabs, hipStream_t s, int ablate = 0);
+
 }  // namespace dctae

@@ -359,11 +359,14 @@ def test_sq512_reference_codes(fe, pn, lfq, ref_tables):
     assert flips <= max(2, codes.numel() // 10000)
 
 
-@pytest.mark.parametrize("sizes", [[(1024, 1024)], [(1023, 997), (768, 1000)]])
+@pytest.mark.parametrize("sizes", [[(1024, 1024)], [(1023, 997), (768, 1000)], [(1021, 333), (997, 1021)],
+                                   [(30, 997), (997, 30), (262, 1000)]])
 def test_large_ragged_vs_oracle(fe, pn, lfq, ref_tables, sizes):
-    """Config 4's upper sizes: 1024 x 1024 (runtime-plan FFT rows / columns),
-    1023 x 997 (odd, no FFT plan: MFMA GEMM both ways), 768 x 1000 (7-smooth
-    FFT plans of other radices): tokens and codes vs the oracle."""
+    """Config 4's sizes: 1024 x 1024 (runtime-plan Makhoul FFT rows / columns),
+    768 x 1000 (7-smooth plans of other radices), odd and prime sides 1023,
+    997, 1021, 333 and 262 = 2 x 131 (no Makhoul plan: Bluestein FFT,
+    dctae_bluestein.hip), and sides below 32 (MFMA GEMM) mixed with Bluestein
+    ones both ways round: tokens and codes vs the oracle."""
     xs = rng.synth_images(97, sizes)
     ((dp, codes),) = fe.encode_batch([torch.from_numpy(a).to(DEV) for a in xs], pn, lfq, return_raw=True)
     raw, codes = dp.patches.cpu(), codes.cpu()
@@ -496,6 +499,38 @@ def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
         assert d <= 2e-6 * ymax, (d, ymax)
         mism = (c_f.cpu()[r, fj] != c_g.cpu()[r, gj]).sum().item()
         assert mism <= max(2, fj.numel() * 14 // 10000), mism
+
+
+@pytest.mark.parametrize("shape", [(333, 517), (1021, 997), (97, 1000), (1000, 97), (30, 997), (997, 30)])
+def test_bluestein_matches_gemm_path(fe, pn, lfq, shape):
+    """Sides without a Makhoul plan: the Bluestein FFT (default) and the MFMA
+    GEMM DCT (option bluestein=0) agree on the tokens within 2e-6 * max|Y| and
+    on the codes except inside the guard band; rows and columns each take
+    either path (sides < 32 stay on the GEMM)."""
+    ops = _ops()
+    x = torch.from_numpy(np.stack(rng.synth_images(37, [shape] * 2))).to(DEV)
+    ((dp_b, c_b),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_option("bluestein", 0)
+    try:
+        ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    finally:
+        ops.set_option("bluestein", 1)
+    kp = dp_b.key_pad_mask.cpu()
+    assert torch.equal(kp, dp_g.key_pad_mask.cpu())
+    rb, rg = dp_b.patches.cpu(), dp_g.patches.cpu()
+    for r in range(kp.shape[0]):
+        ids_g, ids_b = dp_g.batched_image_ids[r].tolist(), dp_b.batched_image_ids[r].tolist()
+        gm = {(ids_g[j],) + _key(c, p): j for j, (p, c) in
+              enumerate(zip(dp_g.patch_positions[r].tolist(), dp_g.patch_channels[r].tolist())) if not kp[r, j]}
+        bm = [(j, (ids_b[j],) + _key(c, p)) for j, (p, c) in
+              enumerate(zip(dp_b.patch_positions[r].tolist(), dp_b.patch_channels[r].tolist())) if not kp[r, j]]
+        bj = torch.tensor([j for j, _ in bm])
+        gj = torch.tensor([gm[k] for _, k in bm])
+        ymax = rg[r, gj].abs().max().item()
+        d = (rb[r, bj] - rg[r, gj]).abs().max().item()
+        assert d <= 2e-6 * ymax, (d, ymax)
+        mism = (c_b.cpu()[r, bj] != c_g.cpu()[r, gj]).sum().item()
+        assert mism <= max(2, bj.numel() * 14 // 10000), mism
 
 
 def test_threshold_bits_equal_normalised_bits(fe, pn, lfq):
