@@ -60,7 +60,12 @@ struct dctae_ctx {
   std::map<int, FftPlan> bs_plans;    // N -> Bluestein plan (kind 1; kind 0 = none)
   std::map<int, int64_t> bs_tw;       // L -> offset of W_L^m in fft_tab
   bool fft_enabled = true;
-  bool bluestein = true;              // lengths without a Makhoul plan: Bluestein FFT (else the MFMA GEMM)
+  // lengths without a Makhoul plan: Bluestein FFT (dctae_bluestein.hip) or the
+  // MFMA GEMM.  Default GEMM: on config 4 (1024 ragged images up to 1024^2)
+  // the Bluestein kernels measured 16.9 ms of device time against the GEMM
+  // path's 12.0 ms (the transform doubles the FFT length; the fp32 MFMA GEMM
+  // runs at ~60 TF/s at these sizes) -- DESIGN.md section "Bluestein".
+  bool bluestein = false;
   bool fft_spec_enabled = true;
   int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
   int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)

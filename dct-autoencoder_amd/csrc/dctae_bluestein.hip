@@ -87,10 +87,13 @@ __device__ __forceinline__ void bs_twiddles(float2 (&tw)[16], int tt, const BsTa
 // replaced by conj(X Bhat), the input of the inverse transform.  Table loads
 // are issued before the pass's barrier so their latency overlaps it.
 template <int L, int R, int NS, bool CHIRP_IN, bool BHAT_OUT>
-__device__ __forceinline__ void bs_pass(float2* __restrict__ buf, int tt, const BsTabs& t, int N,
+__device__ __forceinline__ void bs_pass(float2* __restrict__ buf2, int tt, const BsTabs& t, int N,
                                         const float2 (&tw)[16]) {
   constexpr int TPJ = L / 16, Q = 16 / R, S = L / R;
-  float2 v[16], bh[16];
+  // packed (re, im) pairs: complex adds are one v_pk_add_f32, products two packed FMAs
+  cf* buf = reinterpret_cast<cf*>(buf2);
+  cf v[16];
+  float2 bh[16];
   if (BHAT_OUT) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -104,10 +107,13 @@ __device__ __forceinline__ void bs_pass(float2* __restrict__ buf, int tt, const 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int n = tt + TPJ * q + r * S;
-      float2 x = buf[bsp(n)];
+      cf x = buf[bsp(n)];
       // no n < N predicate here (the compiler sank the loads into the branch:
       // 16 serialised load -> wait round trips): buf is zero at n >= N
-      if (CHIRP_IN) x = cmul(x, t.chirp[n < N ? n : N - 1]);
+      if (CHIRP_IN) {
+        const float2 c = t.chirp[n < N ? n : N - 1];
+        x = cmul_pk(x, (cf){c.x, c.y});
+      }
       v[q * R + r] = x;
     }
   __syncthreads();
@@ -115,38 +121,48 @@ __device__ __forceinline__ void bs_pass(float2* __restrict__ buf, int tt, const 
   for (int q = 0; q < Q; ++q) {
     const int j = tt + TPJ * q;
     const int k1 = j & (NS - 1);
-    float2* w = v + q * R;
+    cf* w = v + q * R;
     if (NS > 1) {
 #pragma unroll
-      for (int r = 1; r < R; ++r) w[r] = cmul(w[r], tw[q * R + r]);
+      for (int r = 1; r < R; ++r) w[r] = cmul_pk(w[r], (cf){tw[q * R + r].x, tw[q * R + r].y});
     }
-    DFT<R>::run(w);
+    DFTV<R>::run(w);
     const int base = (j - k1) * R + k1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      float2 x = w[r];
-      if (BHAT_OUT) x = conj2(cmul(x, bh[q * R + r]));
+      cf x = w[r];
+      if (BHAT_OUT) {
+        x = cmul_pk(x, (cf){bh[q * R + r].x, bh[q * R + r].y});
+        x.y = -x.y;
+      }
       buf[bsp(base + r * NS)] = x;
     }
   }
   __syncthreads();
 }
 
+// the thread's twiddles of passes 2 and 3, loaded once per block (measured:
+// loading them in each pass costs ~14 %)
+template <int L>
+struct BsTw {
+  float2 t2[16], t3[16];
+  __device__ __forceinline__ void load(int tt, const BsTabs& t) {
+    bs_twiddles<L, 16, 16>(t2, tt, t);
+    if constexpr (Bs<L>::R3 > 1) bs_twiddles<L, Bs<L>::R3, 256>(t3, tt, t);
+  }
+};
+
 // FFT_L of the job in place; FIRST: chirp on the way in, Bhat product (and the
-// conjugation of the inverse) on the way out.  Each pass loads its twiddles
-// (L2 hits) together with its LDS reads.
+// conjugation of the inverse) on the way out
 template <int L, bool FIRST>
-__device__ __forceinline__ void bs_fft(float2* buf, int tt, const BsTabs& t, int N) {
+__device__ __forceinline__ void bs_fft(float2* buf, int tt, const BsTabs& t, int N, const BsTw<L>& w) {
   constexpr int R3 = Bs<L>::R3;
-  float2 tw[16];
-  bs_pass<L, 16, 1, FIRST, false>(buf, tt, t, N, tw);
-  bs_twiddles<L, 16, 16>(tw, tt, t);
+  bs_pass<L, 16, 1, FIRST, false>(buf, tt, t, N, w.t2);
   if constexpr (R3 > 1) {
-    bs_pass<L, 16, 16, false, false>(buf, tt, t, N, tw);
-    bs_twiddles<L, R3, 256>(tw, tt, t);
-    bs_pass<L, R3, 256, false, FIRST>(buf, tt, t, N, tw);
+    bs_pass<L, 16, 16, false, false>(buf, tt, t, N, w.t2);
+    bs_pass<L, R3, 256, false, FIRST>(buf, tt, t, N, w.t3);
   } else {
-    bs_pass<L, 16, 16, false, FIRST>(buf, tt, t, N, tw);
+    bs_pass<L, 16, 16, false, FIRST>(buf, tt, t, N, w.t2);
   }
 }
 
@@ -177,7 +193,7 @@ __device__ __forceinline__ int makhoul_pos(int x, int N) { return (x & 1) ? (N -
 // inputs are loaded while the current item is transformed (the kernels are
 // latency-bound: measured 25 us per one-item block, ~1/3 of it the block's
 // serial descriptor -> plan -> table chain)
-constexpr int kBsItems = 8;
+constexpr int kBsItems = 1;
 
 // rows: block = kBsItems groups of 2G rows of one image from y0; per group the
 // jobs (row pair g, channel c)
@@ -199,6 +215,8 @@ __global__ __launch_bounds__(384) void k_bs_rows(const ImgDesc* __restrict__ img
   float* lf = reinterpret_cast<float*>(lds);
   const float gam = 0.430000007152557373046875f;
   const int job = tid0 / S::TPJ;
+  BsTw<L> tw;
+  tw.load(tid0 - job * S::TPJ, t);
   float rgbv[NR * PXI][3];
   auto load_rgb = [&](int yb, int tid) {
 #pragma unroll
@@ -243,8 +261,8 @@ __global__ __launch_bounds__(384) void k_bs_rows(const ImgDesc* __restrict__ img
     if (it + 1 < kBsItems && yb + NR < H) load_rgb(yb + NR, tid);
     __syncthreads();
     if (!(ablate & 2)) {
-      bs_fft<L, true>(buf, tt, ti, N);
-      bs_fft<L, false>(buf, tt, ti, N);
+      bs_fft<L, true>(buf, tt, ti, N, tw);
+      bs_fft<L, false>(buf, tt, ti, N, tw);
     }
     if (!(ablate & 4)) {
       // post: the thread's kept coefficients k for all jobs of the group
@@ -290,6 +308,8 @@ __global__ __launch_bounds__(384) void k_bs_cols(const ImgDesc* __restrict__ img
   float* Y = ws + d.ws_y + (int64_t)c * Kh * Kw;
   float* lf = reinterpret_cast<float*>(lds);
   const int job = tid0 / S::TPJ;
+  BsTw<L> tw;
+  tw.load(tid0 - job * S::TPJ, t);
   float tv[EI];
   auto load_t = [&](int kxb, int tid) {
 #pragma unroll
@@ -317,8 +337,8 @@ __global__ __launch_bounds__(384) void k_bs_cols(const ImgDesc* __restrict__ img
     if (it + 1 < kBsItems && kxb + NC < Kw) load_t(kxb + NC, tid);
     __syncthreads();
     if (!(ablate & 2)) {
-      bs_fft<L, true>(buf, tt, ti, N);
-      bs_fft<L, false>(buf, tt, ti, N);
+      bs_fft<L, true>(buf, tt, ti, N, tw);
+      bs_fft<L, false>(buf, tt, ti, N, tw);
     }
     const int kx = kxb + 2 * jj;
     if (!(ablate & 4) && kx < Kw) {

@@ -223,6 +223,37 @@ struct DFTV<4> {
 };
 
 template <>
+struct DFTV<2> {
+  static __device__ __forceinline__ void run(cf* v) {
+    const cf a = v[0], b = v[1];
+    v[0] = a + b;
+    v[1] = a - b;
+  }
+};
+
+template <>
+struct DFTV<8> {
+  static __device__ __forceinline__ void run(cf* v) {
+#pragma clang fp contract(fast)
+    cf e[4] = {v[0], v[2], v[4], v[6]};
+    cf o[4] = {v[1], v[3], v[5], v[7]};
+    DFTV<4>::run(e);
+    DFTV<4>::run(o);
+    const float c = 7.071067812e-01f;
+    const cf w1 = cmulv(o[1], (cf){c, -c});
+    const cf w3 = cmulv(o[3], (cf){-c, -c});
+    v[0] = e[0] + o[0];
+    v[4] = e[0] - o[0];
+    v[1] = e[1] + w1;
+    v[5] = e[1] - w1;
+    v[2] = add_mi(e[2], o[2]);   // e2 + (-i) o2
+    v[6] = sub_mi(e[2], o[2]);
+    v[3] = e[3] + w3;
+    v[7] = e[3] - w3;
+  }
+};
+
+template <>
 struct DFTV<16> {
   static __device__ __forceinline__ void run(cf* v) {
 #pragma clang fp contract(fast)

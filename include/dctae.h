@@ -291,8 +291,9 @@ int dctae_set_fft(dctae_ctx* ctx, int enable);
 int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
 
 /* Tuning / test knobs: "fft" (0/1), "fft_spec" (0/1: compile-time
- * specialised FFT kernels), "bluestein" (0/1: sides in [32, 1024] without a
- * Makhoul plan on the Bluestein FFT, else the MFMA GEMM), "chunk_bytes", "workspace_limit" (bytes),
+ * specialised FFT kernels), "bluestein" (0/1, default 0: sides in [32, 1024]
+ * without a Makhoul plan on the Bluestein FFT instead of the MFMA GEMM;
+ * measured slower at these sizes), "chunk_bytes", "workspace_limit" (bytes),
  * "rows_kernel" (3: k_rows512, 2: k_fft_rows2 for 512-wide rows),
  * "sort_kernel" (2: rocPRIM radix, 1: bitonic), "fft_decode" (0/1),
  * "xcd_order" (0/1); profiling only (outputs invalid): "rows_ablate",

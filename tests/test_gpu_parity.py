@@ -359,16 +359,23 @@ def test_sq512_reference_codes(fe, pn, lfq, ref_tables):
     assert flips <= max(2, codes.numel() // 10000)
 
 
+@pytest.mark.parametrize("bluestein", [0, 1])
 @pytest.mark.parametrize("sizes", [[(1024, 1024)], [(1023, 997), (768, 1000)], [(1021, 333), (997, 1021)],
                                    [(30, 997), (997, 30), (262, 1000)]])
-def test_large_ragged_vs_oracle(fe, pn, lfq, ref_tables, sizes):
+def test_large_ragged_vs_oracle(fe, pn, lfq, ref_tables, sizes, bluestein):
     """Config 4's sizes: 1024 x 1024 (runtime-plan Makhoul FFT rows / columns),
     768 x 1000 (7-smooth plans of other radices), odd and prime sides 1023,
     997, 1021, 333 and 262 = 2 x 131 (no Makhoul plan: Bluestein FFT,
-    dctae_bluestein.hip), and sides below 32 (MFMA GEMM) mixed with Bluestein
-    ones both ways round: tokens and codes vs the oracle."""
+    dctae_bluestein.hip, with option bluestein=1; the MFMA GEMM by default),
+    and sides below 32 (always the GEMM) mixed with those both ways round:
+    tokens and codes vs the oracle."""
     xs = rng.synth_images(97, sizes)
-    ((dp, codes),) = fe.encode_batch([torch.from_numpy(a).to(DEV) for a in xs], pn, lfq, return_raw=True)
+    ops = _ops()
+    ops.set_option("bluestein", bluestein)
+    try:
+        ((dp, codes),) = fe.encode_batch([torch.from_numpy(a).to(DEV) for a in xs], pn, lfq, return_raw=True)
+    finally:
+        ops.set_option("bluestein", 0)
     raw, codes = dp.patches.cpu(), codes.cpu()
     kp, ids = dp.key_pad_mask.cpu(), dp.batched_image_ids.cpu()
     slots = _image_slots(kp, ids)
@@ -503,18 +510,18 @@ def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
 
 @pytest.mark.parametrize("shape", [(333, 517), (1021, 997), (97, 1000), (1000, 97), (30, 997), (997, 30)])
 def test_bluestein_matches_gemm_path(fe, pn, lfq, shape):
-    """Sides without a Makhoul plan: the Bluestein FFT (default) and the MFMA
-    GEMM DCT (option bluestein=0) agree on the tokens within 2e-6 * max|Y| and
-    on the codes except inside the guard band; rows and columns each take
+    """Sides without a Makhoul plan: the Bluestein FFT (option bluestein=1)
+    and the MFMA GEMM DCT (default) agree on the tokens within 2e-6 * max|Y|
+    and on the codes except inside the guard band; rows and columns each take
     either path (sides < 32 stay on the GEMM)."""
     ops = _ops()
     x = torch.from_numpy(np.stack(rng.synth_images(37, [shape] * 2))).to(DEV)
-    ((dp_b, c_b),) = fe.encode_batch(x, pn, lfq, return_raw=True)
-    ops.set_option("bluestein", 0)
+    ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_option("bluestein", 1)
     try:
-        ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+        ((dp_b, c_b),) = fe.encode_batch(x, pn, lfq, return_raw=True)
     finally:
-        ops.set_option("bluestein", 1)
+        ops.set_option("bluestein", 0)
     kp = dp_b.key_pad_mask.cpu()
     assert torch.equal(kp, dp_g.key_pad_mask.cpu())
     rb, rg = dp_b.patches.cpu(), dp_g.patches.cpu()

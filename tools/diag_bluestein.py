@@ -30,5 +30,5 @@ for shape in shapes:
         err = (gp - toks[idx]).abs()
         worst = int(err.max(1).values.argmax())
         res.append((float(err.max()) / ymax, tuple(gpos[worst].tolist()), int(gch[worst])))
-    _ops.set_option("bluestein", 1)
+    _ops.set_option("bluestein", 0)
     print(shape, "bluestein", res[0], "gemm", res[1], flush=True)
