@@ -604,6 +604,7 @@ struct EncPlan {
   size_t rowlen_off = 0, plans_off = 0;
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
+  bool any_pad = true;   // some packed row shorter than max_seq_len
 };
 
 // ---------------------------------------------------------------------------
@@ -1074,6 +1075,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   E.plans_off = E.pb.add(plans.data(), plans.size());
   E.all_desc_off = E.pb.add(D.data(), D.size());
   if (full && pack->n_rows > 0) E.rowlen_off = E.pb.add(pack->row_len, pack->n_rows);
+  E.any_pad = false;
+  if (full)
+    for (int r = 0; r < pack->n_rows; ++r) E.any_pad = E.any_pad || pack->row_len[r] < S;
   E.ncb = ncb;
   return 0;
 }
@@ -1157,7 +1161,10 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     ps.patches = out->patches_dev;
     ps.raw = out->raw_patches_dev;
     ps.scores = out->scores_dev;
-    if (pack->n_rows > 0) {
+    ps.key_pad = out->key_pad_dev;
+    // rows filled to max_seq_len (e.g. one 512^2 image per row) have no pads:
+    // the sort kernel writes their key_pad zeros, no k_pad_fill launch
+    if (pack->n_rows > 0 && E.any_pad) {
       Timer t(ctx, s, "pad_fill");
       launch_pad_fill((const int32_t*)(pd + E.rowlen_off), pack->n_rows, ep, out->key_pad_dev, ps, s);
     }

@@ -98,6 +98,7 @@ struct PackSinks {
   float* patches;     // (R,S,PP) gathered from norm staging
   float* raw;         // (R,S,PP) gathered from raw staging
   float* scores;      // (R,S)
+  uint8_t* key_pad;   // (R,S): k_sort_pack* write 0 at their tokens (k_pad_fill writes the rows' pads)
 };
 
 struct DecodeArgs {

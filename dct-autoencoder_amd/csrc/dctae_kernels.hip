@@ -444,6 +444,7 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
     out.pos[2 * o + 1] = w;
     out.ch[o] = c;
     out.ids[o] = d.local_id;
+    if (out.key_pad) out.key_pad[o] = 0;
     if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
   }
   if (out.codes) {
@@ -500,6 +501,7 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     *reinterpret_cast<longlong2*>(out.pos + 2 * o) = make_longlong2(h, w);
     out.ch[o] = c;
     out.ids[o] = d.local_id;
+    if (out.key_pad) out.key_pad[o] = 0;
     if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
   }
   if (out.codes && ep.ncb == 14) {
