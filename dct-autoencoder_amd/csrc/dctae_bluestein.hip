@@ -40,10 +40,15 @@ __device__ __forceinline__ float2 conj2(float2 a) { return make_float2(a.x, -a.y
 
 template <int L>
 struct Bs {
-  static constexpr int TPJ = L / 16;    // threads per job
-  static constexpr int G = 128 / TPJ;   // sequence pairs per block and channel (rows) / per 3 (cols)
+  // points per thread: 32 for L <= 1024 (a job inside one wave, its passes
+  // synchronised by the wave alone; measured 25-30 % faster than 16 points
+  // with block barriers); 16 at L = 2048 (two waves per job, block barriers:
+  // 32 points need 256 VGPRs there and measured 17 % slower)
+  static constexpr int E = L == 2048 ? 16 : 32;
+  static constexpr int TPJ = L / E;     // threads per job
+  static constexpr int G = 2048 / L;    // sequence pairs per block and channel (rows)
   static constexpr int JOBS = 3 * G;
-  static constexpr int NT = JOBS * TPJ; // 384
+  static constexpr int NT = JOBS * TPJ; // 192 (L <= 1024) or 384 (L = 2048)
   static constexpr int LP = L + L / 16; // padded job length (float2)
   static constexpr int R3 = L / 256;    // radix of the last pass (1 = none)
 };
@@ -70,8 +75,8 @@ __device__ __forceinline__ int bs_opaque(int v) {
 // The thread's twiddles of the passes with NS > 1, loaded once per kernel and
 // shared by both transforms: tw[q R + r] = W_{NS R}^{r k1(q)}
 template <int L, int R, int NS>
-__device__ __forceinline__ void bs_twiddles(float2 (&tw)[16], int tt, const BsTabs& t) {
-  constexpr int TPJ = L / 16, Q = 16 / R;
+__device__ __forceinline__ void bs_twiddles(float2 (&tw)[32], int tt, const BsTabs& t) {
+  constexpr int TPJ = Bs<L>::TPJ, Q = Bs<L>::E / R;
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int k1 = (tt + TPJ * q) & (NS - 1);
@@ -86,22 +91,31 @@ __device__ __forceinline__ void bs_twiddles(float2 (&tw)[16], int tt, const BsTa
 // inputs are z[n] c[n] (buf is zero at n >= N); BHAT_OUT: the outputs are
 // replaced by conj(X Bhat), the input of the inverse transform.  Table loads
 // are issued before the pass's barrier so their latency overlaps it.
-template <int L, int R, int NS, bool CHIRP_IN, bool BHAT_OUT>
+// A job's lanes are all in one wave, so a pass needs no block barrier: its
+// reads precede its writes in the wave's in-order LDS stream, and the writes
+// precede the next pass's reads (bs_wave_sync keeps the compiler from moving
+// LDS accesses across the pass boundary).
+template <int L>
+__device__ __forceinline__ void bs_wave_sync() {
+  if constexpr (Bs<L>::TPJ > 64) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// IN = 1: the first transform's inputs z[n] c[n] (buf is zero at n >= N);
+// IN = 2: the second transform's inputs conj(Zhat[n] Bhat[n]) (the spectrum
+// product and the conjugation of the inverse, applied as the data is read)
+template <int L, int R, int NS, int IN>
 __device__ __forceinline__ void bs_pass(float2* __restrict__ buf2, int tt, const BsTabs& t, int N,
-                                        const float2 (&tw)[16]) {
-  constexpr int TPJ = L / 16, Q = 16 / R, S = L / R;
+                                        const float2 (&tw)[32]) {
+  constexpr int TPJ = Bs<L>::TPJ, Q = Bs<L>::E / R, S = L / R;
   // packed (re, im) pairs: complex adds are one v_pk_add_f32, products two packed FMAs
   cf* buf = reinterpret_cast<cf*>(buf2);
-  cf v[16];
-  float2 bh[16];
-  if (BHAT_OUT) {
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int j = tt + TPJ * q, k1 = j & (NS - 1);
-#pragma unroll
-      for (int r = 0; r < R; ++r) bh[q * R + r] = t.bhat[(j - k1) * R + k1 + r * NS];
-    }
-  }
+  cf v[32];
 #pragma unroll
   for (int q = 0; q < Q; ++q)
 #pragma unroll
@@ -110,13 +124,17 @@ __device__ __forceinline__ void bs_pass(float2* __restrict__ buf2, int tt, const
       cf x = buf[bsp(n)];
       // no n < N predicate here (the compiler sank the loads into the branch:
       // 16 serialised load -> wait round trips): buf is zero at n >= N
-      if (CHIRP_IN) {
+      if (IN == 1) {
         const float2 c = t.chirp[n < N ? n : N - 1];
         x = cmul_pk(x, (cf){c.x, c.y});
+      } else if (IN == 2) {
+        const float2 b = t.bhat[n];
+        x = cmul_pk(x, (cf){b.x, b.y});
+        x.y = -x.y;
       }
       v[q * R + r] = x;
     }
-  __syncthreads();
+  bs_wave_sync<L>();
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int j = tt + TPJ * q;
@@ -129,40 +147,46 @@ __device__ __forceinline__ void bs_pass(float2* __restrict__ buf2, int tt, const
     DFTV<R>::run(w);
     const int base = (j - k1) * R + k1;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      cf x = w[r];
-      if (BHAT_OUT) {
-        x = cmul_pk(x, (cf){bh[q * R + r].x, bh[q * R + r].y});
-        x.y = -x.y;
-      }
-      buf[bsp(base + r * NS)] = x;
-    }
+    for (int r = 0; r < R; ++r) buf[bsp(base + r * NS)] = w[r];
   }
-  __syncthreads();
+  bs_wave_sync<L>();
 }
 
-// the thread's twiddles of passes 2 and 3, loaded once per block (measured:
-// loading them in each pass costs ~14 %)
+// the thread's twiddles of passes 2 and 3, preloaded once per block at 16
+// points per thread (loading them per pass measured 14 % slower there); at
+// 32 points per thread they are loaded per pass (preloaded: 128 VGPRs)
 template <int L>
 struct BsTw {
-  float2 t2[16], t3[16];
+  static constexpr bool kPre = Bs<L>::E == 16;
+  float2 t2[kPre ? 32 : 1], t3[kPre ? 32 : 1];
   __device__ __forceinline__ void load(int tt, const BsTabs& t) {
-    bs_twiddles<L, 16, 16>(t2, tt, t);
-    if constexpr (Bs<L>::R3 > 1) bs_twiddles<L, Bs<L>::R3, 256>(t3, tt, t);
+    if constexpr (kPre) {
+      bs_twiddles<L, 16, 16>(t2, tt, t);
+      if constexpr (Bs<L>::R3 > 1) bs_twiddles<L, Bs<L>::R3, 256>(t3, tt, t);
+    }
   }
 };
 
-// FFT_L of the job in place; FIRST: chirp on the way in, Bhat product (and the
-// conjugation of the inverse) on the way out
+// FFT_L of the job in place; FIRST: chirp on the way in; second: Bhat product
+// and conjugation on the way in
 template <int L, bool FIRST>
 __device__ __forceinline__ void bs_fft(float2* buf, int tt, const BsTabs& t, int N, const BsTw<L>& w) {
   constexpr int R3 = Bs<L>::R3;
-  bs_pass<L, 16, 1, FIRST, false>(buf, tt, t, N, w.t2);
-  if constexpr (R3 > 1) {
-    bs_pass<L, 16, 16, false, false>(buf, tt, t, N, w.t2);
-    bs_pass<L, R3, 256, false, FIRST>(buf, tt, t, N, w.t3);
+  if constexpr (BsTw<L>::kPre) {
+    bs_pass<L, 16, 1, FIRST ? 1 : 2>(buf, tt, t, N, w.t2);
+    bs_pass<L, 16, 16, 0>(buf, tt, t, N, w.t2);
+    if constexpr (R3 > 1) bs_pass<L, R3, 256, 0>(buf, tt, t, N, w.t3);
   } else {
-    bs_pass<L, 16, 16, false, FIRST>(buf, tt, t, N, w.t2);
+    float2 tw[32];
+    bs_pass<L, 16, 1, FIRST ? 1 : 2>(buf, tt, t, N, tw);
+    bs_twiddles<L, 16, 16>(tw, tt, t);
+    if constexpr (R3 > 1) {
+      bs_pass<L, 16, 16, 0>(buf, tt, t, N, tw);
+      bs_twiddles<L, R3, 256>(tw, tt, t);
+      bs_pass<L, R3, 256, 0>(buf, tt, t, N, tw);
+    } else {
+      bs_pass<L, 16, 16, 0>(buf, tt, t, N, tw);
+    }
   }
 }
 
@@ -198,7 +222,7 @@ constexpr int kBsItems = 1;
 // rows: block = kBsItems groups of 2G rows of one image from y0; per group the
 // jobs (row pair g, channel c)
 template <int L>
-__global__ __launch_bounds__(384) void k_bs_rows(const ImgDesc* __restrict__ imgs, const FftPlan* __restrict__ plans,
+__global__ __launch_bounds__(Bs<L>::NT) void k_bs_rows(const ImgDesc* __restrict__ imgs, const FftPlan* __restrict__ plans,
                                                  const int2* __restrict__ blocks, const float* __restrict__ rgb,
                                                  float* __restrict__ ws, const float2* __restrict__ tabs, ColorMats cm,
                                                  int ablate) {
@@ -264,6 +288,7 @@ __global__ __launch_bounds__(384) void k_bs_rows(const ImgDesc* __restrict__ img
       bs_fft<L, true>(buf, tt, ti, N, tw);
       bs_fft<L, false>(buf, tt, ti, N, tw);
     }
+    __syncthreads();   // the post reads every wave's jobs
     if (!(ablate & 4)) {
       // post: the thread's kept coefficients k for all jobs of the group
 #pragma unroll
@@ -290,7 +315,7 @@ __global__ __launch_bounds__(384) void k_bs_rows(const ImgDesc* __restrict__ img
 // cols: block = kBsItems groups of NC = 2 JOBS columns of channel c of T from
 // kx0; per group the jobs are column pairs
 template <int L>
-__global__ __launch_bounds__(384) void k_bs_cols(const ImgDesc* __restrict__ imgs, const FftPlan* __restrict__ plans,
+__global__ __launch_bounds__(Bs<L>::NT) void k_bs_cols(const ImgDesc* __restrict__ imgs, const FftPlan* __restrict__ plans,
                                                  const int4* __restrict__ blocks, float* __restrict__ ws,
                                                  const float2* __restrict__ tabs, int ablate) {
   using S = Bs<L>;
@@ -340,6 +365,7 @@ __global__ __launch_bounds__(384) void k_bs_cols(const ImgDesc* __restrict__ img
       bs_fft<L, true>(buf, tt, ti, N, tw);
       bs_fft<L, false>(buf, tt, ti, N, tw);
     }
+    __syncthreads();   // the post reads every wave's jobs
     const int kx = kxb + 2 * jj;
     if (!(ablate & 4) && kx < Kw) {
       // post: thread = (coefficient row kk + KPR i, column pair jj)
@@ -360,17 +386,17 @@ __global__ __launch_bounds__(384) void k_bs_cols(const ImgDesc* __restrict__ img
 
 }  // namespace
 
-int bs_rows_per_block(int L) { return kBsItems * 2 * (128 / (L / 16)); }
-int bs_cols_per_block(int L) { return kBsItems * 2 * 3 * (128 / (L / 16)); }
+int bs_rows_per_block(int L) { return kBsItems * 2 * (2048 / L); }
+int bs_cols_per_block(int L) { return kBsItems * 2 * 3 * (2048 / L); }
 
 void launch_bs_rows(int L, const ImgDesc* imgs, const FftPlan* plans, const int2* blocks, int n_blocks,
                     const float* rgb, float* ws, const float2* tabs, const ColorMats& cm, hipStream_t s, int ablate) {
   if (n_blocks <= 0) return;
   switch (L) {
-    case 256: hipLaunchKernelGGL(k_bs_rows<256>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
-    case 512: hipLaunchKernelGGL(k_bs_rows<512>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
-    case 1024: hipLaunchKernelGGL(k_bs_rows<1024>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
-    case 2048: hipLaunchKernelGGL(k_bs_rows<2048>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
+    case 256: hipLaunchKernelGGL(k_bs_rows<256>, dim3(n_blocks), dim3(Bs<256>::NT), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
+    case 512: hipLaunchKernelGGL(k_bs_rows<512>, dim3(n_blocks), dim3(Bs<512>::NT), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
+    case 1024: hipLaunchKernelGGL(k_bs_rows<1024>, dim3(n_blocks), dim3(Bs<1024>::NT), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
+    case 2048: hipLaunchKernelGGL(k_bs_rows<2048>, dim3(n_blocks), dim3(Bs<2048>::NT), 0, s, imgs, plans, blocks, rgb, ws, tabs, cm, ablate); break;
     default: break;
   }
 }
@@ -379,10 +405,10 @@ void launch_bs_cols(int L, const ImgDesc* imgs, const FftPlan* plans, const int4
                     const float2* tabs, hipStream_t s, int ablate) {
   if (n_blocks <= 0) return;
   switch (L) {
-    case 256: hipLaunchKernelGGL(k_bs_cols<256>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
-    case 512: hipLaunchKernelGGL(k_bs_cols<512>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
-    case 1024: hipLaunchKernelGGL(k_bs_cols<1024>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
-    case 2048: hipLaunchKernelGGL(k_bs_cols<2048>, dim3(n_blocks), dim3(384), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
+    case 256: hipLaunchKernelGGL(k_bs_cols<256>, dim3(n_blocks), dim3(Bs<256>::NT), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
+    case 512: hipLaunchKernelGGL(k_bs_cols<512>, dim3(n_blocks), dim3(Bs<512>::NT), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
+    case 1024: hipLaunchKernelGGL(k_bs_cols<1024>, dim3(n_blocks), dim3(Bs<1024>::NT), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
+    case 2048: hipLaunchKernelGGL(k_bs_cols<2048>, dim3(n_blocks), dim3(Bs<2048>::NT), 0, s, imgs, plans, blocks, ws, tabs, ablate); break;
     default: break;
   }
 }
