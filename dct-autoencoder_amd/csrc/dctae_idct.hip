@@ -178,30 +178,18 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
       zk[i] = pre_z(yk, ynk, ymk, ymk2, pre_s[k]);
     }
   }
-  __syncthreads();
+  // ---- 3. forward FFT of conj Z (radix 16 x 16, Stockham).  Pass 1's item
+  // jj reads z[jj + 16 r] = this lane's zk[r]: it runs on the registers
+  // (no LDS round trip); its outputs go to z[16 jj + r] for pass 2.
+  if (on_col) DFTV<16>::run(zk);
+  __syncthreads();   // every wave's X reads (step 2) before z (aliased on X) is written
   const cf* zr = reinterpret_cast<const cf*>(L.z) + 15 * jj + col;   // z[jj + 16 r]
   if (on_col) {
-    cf* zw = reinterpret_cast<cf*>(L.z) + 15 * jj + col;
+    cf* zw = reinterpret_cast<cf*>(L.z) + S16 * jj + col;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) zw[S16 * i] = zk[i];
+    for (int r = 0; r < 16; ++r) zw[15 * r] = zk[r];
   }
   __syncthreads();
-  // ---- 3. forward FFT of conj Z (radix 16 x 16, Stockham)
-  {
-    cf v[16];
-    if (on_col) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = zr[S16 * r];
-      DFTV<16>::run(v);
-    }
-    __syncthreads();
-    if (on_col) {
-      cf* zw = reinterpret_cast<cf*>(L.z) + S16 * jj + col;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) zw[15 * r] = v[r];
-    }
-    __syncthreads();
-  }
   {
     cf v[16];
     if (on_col) {
