@@ -250,12 +250,19 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if os.environ.get("DCTAE_BENCH_SHARE_GPU"):   # rehearsal of N ranks on fewer GPUs (never in the driver's runs)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL refuses two ranks on one GPU: the shared-GPU rehearsal runs its
+        # collectives on gloo (the driver's N-GPU runs always use nccl = RCCL)
+        if os.environ.get("DCTAE_BENCH_SHARE_GPU") and torch.cuda.device_count() < world:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import _pkgload
     pkg = _pkgload.load()
