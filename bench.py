@@ -456,7 +456,8 @@ def main():
             "value": round(mpix_s, 2),
             "unit": "Mpix/s",
             "n_gpus": world,
-            "ranks": {"world": world, "backend": "nccl (RCCL)" if world > 1 else None},
+            "ranks": {"world": world, "backend": (("nccl (RCCL)" if dist.get_backend() == "nccl" else dist.get_backend())
+                                                  if world > 1 else None)},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
