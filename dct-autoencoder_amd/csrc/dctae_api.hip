@@ -588,6 +588,9 @@ struct ChunkJob {
   size_t pc_off;      // k_fft_cols7 list: the spec-1 images of the job (one tile-column count qw)
   int n_pc, pc_qw;
   int max_T, any_gemm_rows, any_gemm_cols, fold_t, any_bs_cols;
+  size_t fold_off;           // local indices of the images whose T k_fold_t folds
+  int n_fold;
+  int64_t fold_max_hw;
   size_t br_off[4], bc_off[4];   // Bluestein row / column blocks per L = 256 .. 2048
   int n_br[4], n_bc[4];
   int64_t max_hw;
@@ -940,6 +943,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     std::vector<int4> fc[kVariants];
     std::vector<int2> br[4];
     std::vector<int4> bc[4];
+    std::vector<int32_t> fold;
     std::vector<int32_t> pc;
     int pc_qw = 0;
     bool pc_ok = true;
@@ -995,7 +999,11 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           probs.push_back(g);
         }
         j.any_gemm_cols = 1;
-        if (d.plan_w >= 0) j.fold_t = 1;
+        if (d.plan_w >= 0) {
+          j.fold_t = 1;
+          fold.push_back(li);
+          j.fold_max_hw = std::max<int64_t>(j.fold_max_hw, (int64_t)d.H * d.W);
+        }
       } else if (d.bs & 2) {
         const int L = plans[d.plan_h].bs_L, cpb = bs_cols_per_block(L);
         for (int c = 0; c < 3; ++c)
@@ -1059,6 +1067,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.n_fr[v] = (int)fr[v].size();
       j.n_fc[v] = (int)fc[v].size();
     }
+    j.fold_off = E.pb.add(fold.data(), fold.size());
+    j.n_fold = (int)fold.size();
     for (int l = 0; l < 4; ++l) {
       j.br_off[l] = E.pb.add(br[l].data(), br[l].size());
       j.bc_off[l] = E.pb.add(bc[l].data(), bc[l].size());
@@ -1234,7 +1244,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     if (j.any_gemm_cols) {
       if (j.fold_t) {
         Timer t(ctx, st, "fold_t");
-        launch_fold_t(dd, nj, j.max_hw, ctx->ws, st);
+        launch_fold_t(dd, (const int32_t*)(pd + j.fold_off), j.n_fold, j.fold_max_hw, ctx->ws, st);
       }
       Timer t(ctx, st, "gemm_cols");
       launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st);

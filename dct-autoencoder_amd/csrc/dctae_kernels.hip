@@ -104,8 +104,10 @@ __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __re
 // T (3, H, Kw) of the images whose columns run through the GEMM DCT but rows
 // through the FFT, folded in place along y: T[m] <- T[m] + T[H-1-m],
 // T[H-1-m] <- T[m] - T[H-1-m] for m < floor(H/2) (middle row of an odd H kept).
-__global__ void k_fold_t(const ImgDesc* __restrict__ imgs, float* __restrict__ ws) {
-  const ImgDesc d = imgs[blockIdx.y];
+// Launched over the listed images only (grid.y = list entries): on the
+// ragged config 4 a grid over every image spent 0.23 ms exiting blocks.
+__global__ void k_fold_t(const ImgDesc* __restrict__ imgs, const int32_t* __restrict__ list, float* __restrict__ ws) {
+  const ImgDesc d = imgs[list[blockIdx.y]];
   if (d.plan_h >= 0 || d.plan_w < 0) return;  // GEMM rows: folded by k_rgb_to_ipt
   const int64_t n = (int64_t)(d.H / 2) * d.Kw;
   float* t = ws + d.ws_t;
@@ -121,9 +123,10 @@ __global__ void k_fold_t(const ImgDesc* __restrict__ imgs, float* __restrict__ w
   }
 }
 
-void launch_fold_t(const ImgDesc* imgs, int n_img, int64_t max_hw, float* ws, hipStream_t s) {
+void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, hipStream_t s) {
+  if (n_list <= 0) return;
   int gx = (int)std::min<int64_t>((3 * max_hw / 2 + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_fold_t, dim3(std::max(gx, 1), n_img), dim3(256), 0, s, imgs, ws);
+  hipLaunchKernelGGL(k_fold_t, dim3(std::max(gx, 1), n_list), dim3(256), 0, s, imgs, list, ws);
 }
 
 void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* rgb, float* ws,
@@ -543,9 +546,30 @@ void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& 
 // PatchNorm/LFQ on them like on any token (c = h = w = 0).
 __global__ void k_pad_fill(const int32_t* __restrict__ row_len, int n_rows, EncParams ep, uint8_t* key_pad,
                            PackSinks out) {
+  // the pad token (zeros at c = h = w = 0) normalises and quantises the same
+  // at every pad position: its patch and codes once per block, in LDS
+  __shared__ float pp[kMaxP * kMaxP];
+  __shared__ int64_t pcode[kMaxCodebooks];
   const int r = blockIdx.y;
   const int S = ep.S, PP = ep.P * ep.P;
   const int len = row_len[r];
+  if ((int)(blockIdx.x * blockDim.x) + (int)blockDim.x <= len) {   // no pads in this block's span
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < S; j += gridDim.x * blockDim.x)
+      key_pad[(int64_t)r * S + j] = 0;
+    if (gridDim.x * blockDim.x >= (unsigned)S) return;
+  }
+  if (out.patches || out.codes) {
+    for (int e = threadIdx.x; e < PP; e += blockDim.x)
+      pp[e] = pn_forward(0.0f, ep.median[e], ep.b[e], ep.eps, ep.min_val, ep.max_val);
+    __syncthreads();
+    if (out.codes)
+      for (int q = threadIdx.x; q < ep.ncb; q += blockDim.x) {
+        uint32_t code = 0;
+        for (int dd = 0; dd < ep.cb_dim; ++dd) code |= (pp[q * ep.cb_dim + dd] > 0.0f ? 1u : 0u) << (ep.cb_dim - 1 - dd);
+        pcode[q] = code;
+      }
+    __syncthreads();
+  }
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < S; j += gridDim.x * blockDim.x) {
     const int64_t o = (int64_t)r * S + j;
     key_pad[o] = (j >= len) ? 1 : 0;
@@ -558,19 +582,9 @@ __global__ void k_pad_fill(const int32_t* __restrict__ row_len, int n_rows, EncP
     if (out.raw)
       for (int e = 0; e < PP; ++e) out.raw[o * PP + e] = 0.0f;
     if (out.patches)
-      for (int e = 0; e < PP; ++e)
-        out.patches[o * PP + e] = pn_forward(0.0f, ep.median[e], ep.b[e], ep.eps, ep.min_val, ep.max_val);
-    if (out.codes) {
-      for (int q = 0; q < ep.ncb; ++q) {
-        uint32_t code = 0;
-        for (int dd = 0; dd < ep.cb_dim; ++dd) {
-          int e = q * ep.cb_dim + dd;
-          float y = pn_forward(0.0f, ep.median[e], ep.b[e], ep.eps, ep.min_val, ep.max_val);
-          code |= (y > 0.0f ? 1u : 0u) << (ep.cb_dim - 1 - dd);
-        }
-        out.codes[o * ep.ncb + q] = code;
-      }
-    }
+      for (int e = 0; e < PP; ++e) out.patches[o * PP + e] = pp[e];
+    if (out.codes)
+      for (int q = 0; q < ep.ncb; ++q) out.codes[o * ep.ncb + q] = pcode[q];
   }
 }
 

@@ -12,7 +12,7 @@ void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const flo
 void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* ws, float* out,
                        const ColorMats& cm, hipStream_t s);
 void launch_color(const float* x, float* y, int64_t hw, int n_img, int dir, const ColorMats& cm, hipStream_t s);
-void launch_fold_t(const ImgDesc* imgs, int n_img, int64_t max_hw, float* ws, hipStream_t s);
+void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, hipStream_t s);
 void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
