@@ -588,6 +588,8 @@ struct ChunkJob {
   size_t pc_off;      // k_fft_cols7 list: the spec-1 images of the job (one tile-column count qw)
   int n_pc, pc_qw;
   int max_T, any_gemm_rows, any_gemm_cols, fold_t, any_bs_cols;
+  size_t ipt_off;            // k_rgb_to_ipt blocks (local image, first group)
+  int n_ipt;
   size_t fold_off;           // local indices of the images whose T k_fold_t folds
   int n_fold;
   int64_t fold_max_hw;
@@ -944,6 +946,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     std::vector<int2> br[4];
     std::vector<int4> bc[4];
     std::vector<int32_t> fold;
+    std::vector<int2> ipt;
     std::vector<int32_t> pc;
     int pc_qw = 0;
     bool pc_ok = true;
@@ -969,6 +972,11 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           probs.push_back(g);
         }
         j.any_gemm_rows = 1;
+        {
+          // k_rgb_to_ipt's (x, y)-mirrored pixel groups of this image
+          const int64_t ng = (int64_t)(d.plan_h < 0 ? (d.H + 1) / 2 : d.H) * ((d.W + 1) / 2);
+          for (int64_t g0 = 0; g0 < ng; g0 += rgb_to_ipt_groups_per_block()) ipt.push_back(make_int2(li, (int)g0));
+        }
       } else if (d.bs & 1) {
         const int L = plans[d.plan_w].bs_L, rpb = bs_rows_per_block(L);
         for (int y0 = 0; y0 < d.H; y0 += rpb) br[bs_lidx(L)].push_back(make_int2(li, y0));
@@ -1067,6 +1075,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.n_fr[v] = (int)fr[v].size();
       j.n_fc[v] = (int)fc[v].size();
     }
+    j.ipt_off = E.pb.add(ipt.data(), ipt.size());
+    j.n_ipt = (int)ipt.size();
     j.fold_off = E.pb.add(fold.data(), fold.size());
     j.n_fold = (int)fold.size();
     for (int l = 0; l < 4; ++l) {
@@ -1211,7 +1221,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     if (j.any_gemm_rows) {
       {
         Timer t(ctx, st, "rgb_to_ipt");
-        launch_rgb_to_ipt(dd, nj, j.max_hw, imgs->rgb_dev, ctx->ws, ctx->cm, st);
+        launch_rgb_to_ipt(dd, (const int2*)(pd + j.ipt_off), j.n_ipt, imgs->rgb_dev, ctx->ws, ctx->cm, st);
       }
       Timer t(ctx, st, "gemm_rows");
       launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st);

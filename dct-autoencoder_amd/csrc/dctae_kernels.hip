@@ -50,10 +50,15 @@ void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_
 // holds p[m] + p[H-1-m] and row H-1-m holds p[m] - p[H-1-m]; the row DCT is
 // linear per row, so the row GEMM then yields T already folded for the
 // column GEMM.  One thread per group of up to 4 mirrored pixels.
-__global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
-                             float* __restrict__ ws, ColorMats cm) {
-  const ImgDesc d = imgs[blockIdx.y];
-  if (d.plan_w >= 0) return;  // rows of this image run through k_fft_rows (IPT fused there)
+// Blocks from a host list of (image, first group): kRgbGroups groups per
+// block (a grid over every image x the largest image's groups spent most of its
+// blocks exiting on the ragged config 4).
+constexpr int kRgbGroups = 256;
+
+__global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                             const float* __restrict__ rgb, float* __restrict__ ws, ColorMats cm) {
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
   const int64_t hw = (int64_t)d.H * d.W;
   const int Wh = (d.W + 1) / 2;
   const bool yfold = d.plan_h < 0;
@@ -75,8 +80,8 @@ __global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const float* __re
       if (pair) dst[c * hw + row + Wh + x] = a[c] - b[c];
     }
   };
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n_groups;
-       e += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t e_end = min(n_groups, (int64_t)jb.y + kRgbGroups);
+  for (int64_t e = (int64_t)jb.y + threadIdx.x; e < e_end; e += blockDim.x) {
     const int y = (int)(e / Wh);
     const int x = (int)(e - (int64_t)y * Wh), x2 = d.W - 1 - x, y2 = d.H - 1 - y;
     const bool xp = x2 != x, yp = yfold && y2 != y;
@@ -129,10 +134,11 @@ void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t
   hipLaunchKernelGGL(k_fold_t, dim3(std::max(gx, 1), n_list), dim3(256), 0, s, imgs, list, ws);
 }
 
-void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* rgb, float* ws,
+int rgb_to_ipt_groups_per_block() { return kRgbGroups; }
+
+void launch_rgb_to_ipt(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                        const ColorMats& cm, hipStream_t s) {
-  int gx = (int)std::min<int64_t>((max_hw / 2 + 256) / 256, 1024);
-  hipLaunchKernelGGL(k_rgb_to_ipt, dim3(gx, n_img), dim3(256), 0, s, imgs, rgb, ws, cm);
+  if (n_blocks > 0) hipLaunchKernelGGL(k_rgb_to_ipt, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, cm);
 }
 
 // ipt (3,H,W) in place -> rgb written to out (3,H,W)

@@ -7,7 +7,8 @@
 namespace dctae {
 
 void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_t W, float* out, hipStream_t s);
-void launch_rgb_to_ipt(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* rgb, float* ws,
+int rgb_to_ipt_groups_per_block();
+void launch_rgb_to_ipt(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                        const ColorMats& cm, hipStream_t s);
 void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* ws, float* out,
                        const ColorMats& cm, hipStream_t s);
