@@ -1224,7 +1224,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         launch_rgb_to_ipt(dd, (const int2*)(pd + j.ipt_off), j.n_ipt, imgs->rgb_dev, ctx->ws, ctx->cm, st);
       }
       Timer t(ctx, st, "gemm_rows");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st);
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st, 1);
     }
     for (int l = 0; l < 4; ++l)
       if (j.n_br[l]) {
@@ -1257,7 +1257,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         launch_fold_t(dd, (const int32_t*)(pd + j.fold_off), j.n_fold, j.fold_max_hw, ctx->ws, st);
       }
       Timer t(ctx, st, "gemm_cols");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st);
+      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st, 2);
     }
     for (int l = 0; l < 4; ++l)
       if (j.n_bc[l]) {
@@ -1368,8 +1368,10 @@ int dctae_dct2(dctae_ctx* ctx, const float* x, int32_t n_img, int32_t H, int32_t
   }
   {
     Timer t(ctx, s, "dct2_gemm");
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s);
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s);
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s,
+                gemm_share(probs[0]));
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s,
+                gemm_share(probs[1]));
   }
   if (direction == 1 && color) {
     Timer t(ctx, s, "ipt_to_rgb");
@@ -1954,11 +1956,11 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   }
   {
     Timer t(ctx, s, "idct_cols");
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s);
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s, 2);
   }
   {
     Timer t(ctx, s, "idct_rows");
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s);
+    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s, 1);
   }
   {
     Timer t(ctx, s, "ipt_to_rgb");

@@ -214,11 +214,18 @@ constexpr int GT = 64;      // tile edge
 constexpr int GK = 32;      // k chunk
 constexpr int GLD = GK + 4; // LDS row stride (floats), keeps float4 alignment
 
-template <int NC>
+// SH: which operand all channels share, known at compile time — 1: B (the DCT
+// matrix of a row transform), 2: A (of a column transform), 0: read from the
+// problem's strides.  Only the unshared operand is staged per channel (LDS
+// 37 KB instead of 55 KB at NC = 3), and the per-lane offsets are 32-bit on a
+// uniform per-channel base: the 64-bit address arithmetic of 48 loads had
+// taken the kernel to 256 VGPRs with spills (2 waves / SIMD).
+template <int NC, int SH>
 __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restrict__ probs,
                                                   const TileRef* __restrict__ tiles) {
-  __shared__ __attribute__((aligned(16))) float As[NC][GT * GLD];
-  __shared__ __attribute__((aligned(16))) float Bs[NC][GT * GLD];
+  constexpr int NA = SH == 2 ? 1 : NC, NB = SH == 1 ? 1 : NC;
+  __shared__ __attribute__((aligned(16))) float As[NA][GT * GLD];
+  __shared__ __attribute__((aligned(16))) float Bs[NB][GT * GLD];
   const TileRef tr = tiles[blockIdx.x];
   const GemmProblem p = probs[tr.problem];
   const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
@@ -226,7 +233,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int half = lane >> 5, l32 = lane & 31;
-  const bool a_shared = (p.sAc == 0), b_shared = (p.sBc == 0);
+  const bool a_shared = SH == 2 ? true : SH == 1 ? false : (p.sAc == 0);
+  const bool b_shared = SH == 1 ? true : SH == 2 ? false : (p.sBc == 0);
 
   floatx16 acc[NC];
 #pragma unroll
@@ -237,52 +245,58 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
   // ---- staging: the next K chunk is loaded into registers while the current
   //      one is multiplied (generic strides, zero-filled at the edges)
   constexpr int EPT = (GT * GK) / 256;   // elements per thread and operand tile
-  float ra[NC][EPT], rb[NC][EPT];
+  float ra[NA][EPT], rb[NB][EPT];
+  const bool akf = (p.sAk == 1), bkf = (p.sBk == 1);
+  const int sAm = (int)p.sAm, sAk = (int)p.sAk, sBn = (int)p.sBn, sBk = (int)p.sBk;
   auto load = [&](int k0) {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
+    for (int c = 0; c < NA; ++c) {
       if (c == 0 || !a_shared) {
         const float* A = p.A + (int64_t)c * p.sAc;
-        const bool kfast = (p.sAk == 1);
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
           const int e = tid + 256 * i;
-          const int mm = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          const int mm = akf ? (e >> 5) : (e & 63), kk = akf ? (e & 31) : (e >> 6);
           const int gm = m0 + mm, gk = k0 + kk;
-          ra[c][i] = (gm < p.M && gk < p.K) ? A[(int64_t)gm * p.sAm + (int64_t)gk * p.sAk] : 0.0f;
+          const bool ok = gm < p.M && gk < p.K;
+          ra[c][i] = ok ? A[ok ? gm * sAm + gk * sAk : 0] : 0.0f;
         }
       }
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
       if (c == 0 || !b_shared) {
         const float* B = p.B + (int64_t)c * p.sBc;
-        const bool kfast = (p.sBk == 1);
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
           const int e = tid + 256 * i;
-          const int nn = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          const int nn = bkf ? (e >> 5) : (e & 63), kk = bkf ? (e & 31) : (e >> 6);
           const int gn = n0 + nn, gk = k0 + kk;
-          rb[c][i] = (gn < p.N && gk < p.K) ? B[(int64_t)gn * p.sBn + (int64_t)gk * p.sBk] : 0.0f;
+          const bool ok = gn < p.N && gk < p.K;
+          rb[c][i] = ok ? B[ok ? gn * sBn + gk * sBk : 0] : 0.0f;
         }
       }
     }
   };
   auto store = [&]() {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
+    for (int c = 0; c < NA; ++c) {
       if (c == 0 || !a_shared) {
-        const bool kfast = (p.sAk == 1);
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
           const int e = tid + 256 * i;
-          const int mm = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          const int mm = akf ? (e >> 5) : (e & 63), kk = akf ? (e & 31) : (e >> 6);
           As[c][mm * GLD + kk] = ra[c][i];
         }
       }
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
       if (c == 0 || !b_shared) {
-        const bool kfast = (p.sBk == 1);
 #pragma unroll
         for (int i = 0; i < EPT; ++i) {
           const int e = tid + 256 * i;
-          const int nn = kfast ? (e >> 5) : (e & 63), kk = kfast ? (e & 31) : (e >> 6);
+          const int nn = bkf ? (e >> 5) : (e & 63), kk = bkf ? (e & 31) : (e >> 6);
           Bs[c][nn * GLD + kk] = rb[c][i];
         }
       }
@@ -301,7 +315,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
       float4 a4[NC], b4[NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
-        const int ca = a_shared ? 0 : c, cb = b_shared ? 0 : c;
+        const int ca = (NA == 1 || a_shared) ? 0 : c, cb = (NB == 1 || b_shared) ? 0 : c;
         a4[c] = *reinterpret_cast<const float4*>(&As[ca][(wm * 32 + l32) * GLD + kofs]);
         b4[c] = *reinterpret_cast<const float4*>(&Bs[cb][(wn * 32 + l32) * GLD + kofs]);
       }
@@ -332,12 +346,22 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
   }
 }
 
-void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s) {
+int gemm_share(const GemmProblem& g) {
+  if (g.C > 1 && g.sBc == 0 && g.sAc != 0) return 1;
+  if (g.C > 1 && g.sAc == 0 && g.sBc != 0) return 2;
+  return 0;
+}
+
+void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
   if (n_tiles <= 0) return;
-  if (nc == 3)
-    hipLaunchKernelGGL(k_gemm_f32<3>, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  if (nc == 3 && share == 1)
+    hipLaunchKernelGGL((k_gemm_f32<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else if (nc == 3 && share == 2)
+    hipLaunchKernelGGL((k_gemm_f32<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else if (nc == 3)
+    hipLaunchKernelGGL((k_gemm_f32<3, 0>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
   else
-    hipLaunchKernelGGL(k_gemm_f32<1>, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+    hipLaunchKernelGGL((k_gemm_f32<1, 0>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
 }
 
 // ---------------------------------------------------------------------------

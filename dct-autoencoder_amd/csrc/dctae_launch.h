@@ -14,7 +14,11 @@ void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const flo
                        const ColorMats& cm, hipStream_t s);
 void launch_color(const float* x, float* y, int64_t hw, int n_img, int dir, const ColorMats& cm, hipStream_t s);
 void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, hipStream_t s);
-void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s);
+// share: 1 = B shared by the channels (row transforms), 2 = A shared (column
+// transforms), 0 = from each problem's strides; must hold for every problem the
+// tiles reference (gemm_share of one of them)
+int gemm_share(const GemmProblem& g);
+void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share = 0);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
