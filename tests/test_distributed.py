@@ -89,7 +89,9 @@ def _worker(rank, world, port, case, q):
         pos = torch.stack([h, w], -1)
         n, med, b = _start_tables(start)
         n2, med2, b2 = D.fit_tables(n, med, b, x[sl], ch[sl], pos[sl], kp[sl], ops)
-        q.put((rank, n2, med2, b2))
+        # by value (numpy): a tensor sent through the queue is shared by file
+        # descriptor, and the parent's unpickling raced this process's exit
+        q.put((rank,) + tuple(t.detach().cpu().numpy() for t in (n2, med2, b2)))
     finally:
         dist.destroy_process_group()
 
@@ -105,7 +107,7 @@ def _run_once(world, case):
     try:
         for _ in range(world):
             r, *t = q.get(timeout=240)
-            res[r] = t
+            res[r] = [torch.from_numpy(a) for a in t]
     finally:
         for p in procs:
             p.join(timeout=60)
