@@ -76,6 +76,7 @@ struct dctae_ctx {
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
   int sort_kernel = 2;                // 1: bitonic in LDS (1024 threads), 2: rocPRIM block radix sort
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
+  int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
   int n_cu = 256;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
@@ -733,6 +734,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "bs_ablate" && value >= 0 && value <= 7) ctx->bs_ablate = (int)value;
   else if (k == "rows_kernel" && (value == 2 || value == 3)) ctx->rows_kernel = (int)value;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
+  else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -1831,7 +1833,10 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
   }
   {
     Timer t(ctx, s, "idct_rows");
-    launch_idct_rows_spec(1, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
+    if (ctx->dec_rows_kernel == 3 && D[0].qw == 32)
+      launch_idct_rows512(dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
+    else
+      launch_idct_rows_spec(1, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);

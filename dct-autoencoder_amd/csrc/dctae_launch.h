@@ -78,6 +78,8 @@ void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, cons
 void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,
                            float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 
+void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
+                         const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                     const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate = 0);
 
