@@ -189,7 +189,10 @@ def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
             for i, (h, w) in enumerate(hw)]
     fe.encode_batch(imgs, pn, lfq)
     torch.cuda.synchronize(dev)
-    n4 = max(1, min(steps, 3))
+    # back-to-back calls: each call's host planning / packing (~2.7 ms for
+    # these 1024 sizes) overlaps the previous call's kernels; the first call's
+    # is in the timed region too (the GPU idles for it), spread over n4 calls
+    n4 = max(1, min(steps, 10))
     t0 = time.perf_counter()
     for _ in range(n4):
         fe.encode_batch(imgs, pn, lfq)
