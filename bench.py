@@ -207,6 +207,48 @@ def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
     return out
 
 
+def config5_leg(enc, dev, rank, world, dist, shard):
+    """rank r encodes its shard of `shard` 512x512 images
+    (global images [r*shard, (r+1)*shard)), regenerated from the counter RNG in
+    1024-image chunks into one resident buffer; generation and encode timed
+    separately with HIP events on the stream, max over ranks.  The stats-fit
+    all-reduce step of config 5 is the `stats_fit` object."""
+    import ctypes as C
+    from importlib import import_module
+    lib = import_module("dct_autoencoder_amd._lib")
+    ctx = lib.context(dev)
+    B, H = enc.B if hasattr(enc, "B") else 1024, 512
+    n_chunks = max(1, shard // B)
+    x = torch.empty((B, 3, H, H), dtype=torch.float32, device=dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(n_chunks)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(n_chunks):
+        e = evs[i]
+        e[0].record()
+        rc = ctx.lib.dctae_synth_images(ctx.h, C.c_uint64(5), rank * shard + i * B, B, H, H,
+                                        C.c_void_p(x.data_ptr()), lib.stream_ptr(dev))
+        ctx.check(rc, "dctae_synth_images")
+        e[1].record()
+        enc(x)
+        e[2].record()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    gen = sum(e[0].elapsed_time(e[1]) for e in evs) / 1e3
+    encs = sum(e[1].elapsed_time(e[2]) for e in evs) / 1e3
+    t = torch.tensor([encs, gen, wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    encs, gen, wall = (float(v) for v in t.tolist())
+    imgs = n_chunks * B * world
+    return {"workload": f"config 5: {world} rank(s) x {n_chunks * B} images of 512x512 (RNG-regenerated in "
+                        f"{B}-image chunks), encode", "images": imgs,
+            "encode_s": round(encs, 4), "generation_s": round(gen, 4), "wall_s": round(wall, 4),
+            "value": round(imgs * H * H / encs / 1e6, 1), "unit": "Mpix/s (encode time, max over ranks)"}
+
+
 def kernel_times(ctx, fn, n):
     """Per-kernel device times of n calls of fn (HIP events around each launch
     on its own stream, dctae_set_timing), outside any timed region."""
@@ -242,6 +284,8 @@ def main():
     ap.add_argument("--model", action="store_true", help="also time the DCTAutoencoder transformer (SURVEY §8(f)4)")
     ap.add_argument("--no-model", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-configs", action="store_true", help="skip the config 2 / config 4 timings")
+    ap.add_argument("--config5-shard", type=int, default=131072,
+                    help="images per rank of the config-5 leg (0 = skip; SURVEY 8(d): 131,072 x 8 ranks)")
     ap.add_argument("--opt", action="append", default=[], help="library option key=value (dctae_set_option)")
     args = ap.parse_args()
 
@@ -435,6 +479,14 @@ def main():
             configs = config_legs(pkg, fe, pn, lfq, dev, rank, args.steps)
         except Exception as e:  # noqa: BLE001 — the encode line must still print
             configs = {"error": f"{type(e).__name__}: {e}"}
+
+    if args.config5_shard > 0 and B == 1024 and H == 512:
+        try:
+            c5 = config5_leg(enc, dev, rank, world, dist, args.config5_shard)
+        except Exception as e:  # noqa: BLE001 — the encode line must still print
+            c5 = {"error": f"{type(e).__name__}: {e}"}
+        configs = dict(configs or {})
+        configs["config5"] = c5
 
     # the DCTAutoencoder transformer forward (patch14-l, 4 rows x 3072 tokens)
     model = None
