@@ -212,11 +212,12 @@ __device__ __forceinline__ void bs_zero_tail(float2* lds, int N, int tid) {
 
 __device__ __forceinline__ int makhoul_pos(int x, int N) { return (x & 1) ? (N - 1 - (x >> 1)) : (x >> 1); }
 
-// items (row groups / column groups) per block: the image's descriptor, plan,
-// twiddles and post tables are loaded once per block, and the next item's
-// inputs are loaded while the current item is transformed (the kernels are
-// latency-bound: measured 25 us per one-item block, ~1/3 of it the block's
-// serial descriptor -> plan -> table chain)
+// items (row groups / column groups) per block: with more than one, the
+// image's descriptor, plan and twiddles are loaded once per block and the
+// next item's inputs while the current item is transformed.  Measured: 8
+// items per block ran 13 % slower than 1 (the prefetch buffers and the
+// loop-carried tables took the kernel to 210 VGPRs, one block per CU), so one
+// item per block; the loop stays for the shape of the code.
 constexpr int kBsItems = 1;
 
 // rows: block = kBsItems groups of 2G rows of one image from y0; per group the
