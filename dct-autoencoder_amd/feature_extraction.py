@@ -407,13 +407,16 @@ class DCTAutoencoderFeatureExtractor:
             ks = [self._k(h, w) for h, w in sizes]
         max_tok = self.max_patch_h * self.max_patch_w * self.channels
         plans = list(packing.iter_batch_plans([(ks, list(range(len(ks))))], self.max_seq_len, max_tok, batch_size))
-        norm = patchnorm.state(thresholds=not return_patches) if patchnorm is not None else None
-        lcfg = lfq.cfg() if lfq is not None else None
-        if lfq is not None:
-            if lfq.has_projections:
-                raise NotImplementedError("fused encode needs LFQ without projections (dim == codebook_dim*num_codebooks)")
-            if patchnorm is None:
-                raise AssertionError("LFQ codes need a PatchNorm")
+        if lfq is not None and patchnorm is None:
+            raise AssertionError("LFQ codes need a PatchNorm")
+        # LFQ with projections (dim != codebook_dim * num_codebooks, lfq.py:54-62,
+        # e.g. conf/patch14-l.json's 196 -> 16 x 13): the fused launch stops at the
+        # PatchNorm output, project_in (a plain fp32 GEMM) and the HIP sign / pack
+        # kernel follow on the same stream
+        proj = lfq is not None and lfq.has_projections
+        want_norm = return_patches or proj
+        norm = patchnorm.state(thresholds=not want_norm) if patchnorm is not None else None
+        lcfg = lfq.cfg() if lfq is not None and not proj else None
         outs = []
         for rows in plans:
             plan = packing.layout(rows, dict(enumerate(ks)))
@@ -422,9 +425,11 @@ class DCTAutoencoderFeatureExtractor:
                                         {j: ks[i] for j, i in enumerate(plan.images)}) \
                 if len(plan.images) != len(ks) else plan
             res = _ops.encode(sub, dev, self.params(), plan_local, plan.n_rows, self.max_seq_len, norm, lcfg,
-                              want_codes=lfq is not None, want_patches=return_patches, want_raw=return_raw,
+                              want_codes=lcfg is not None, want_patches=want_norm, want_raw=return_raw,
                               want_scores=return_scores)
-            pt = res.get("patches", res.get("raw"))
+            if proj:
+                _, res["codes"], _, _ = lfq(res["patches"], mask=~res["key_pad_mask"])
+            pt = res["patches"] if return_patches else res.get("raw")
             if pt is None:
                 pt = torch.empty((plan.n_rows, self.max_seq_len, 0), device=dev)
             dp = DCTPatches(patches=pt, key_pad_mask=res["key_pad_mask"], attn_mask=None,
@@ -475,9 +480,14 @@ class DCTAutoencoderFeatureExtractor:
     @torch.no_grad()
     def decode_batch(self, dct_patches: DCTPatches, codes: torch.Tensor, patchnorm, lfq) -> List[torch.Tensor]:
         """LFQ.indices_to_codes -> PatchNorm.inverse_norm -> postprocess, fused
-        (the decode half of SURVEY §3.4 without the transformer)."""
+        (the decode half of SURVEY §3.4 without the transformer).  With LFQ
+        projections the codes go through project_out (fp32 GEMM) and the HIP
+        inverse PatchNorm first, and the fused decode starts from the tokens."""
         if lfq.has_projections:
-            raise NotImplementedError("fused decode needs LFQ without projections")
+            dp = dct_patches.shallow_copy()
+            dp.patches = lfq.indices_to_codes(codes)
+            dp.patches = patchnorm.inverse_norm(dp)
+            return self.postprocess(dp)
         return _ops.decode(self.params(dct_patches.key_pad_mask.shape[1]), dct_patches.batched_image_ids,
                            dct_patches.key_pad_mask, dct_patches.patch_positions, dct_patches.patch_channels,
                            dct_patches.patch_sizes, dct_patches.original_sizes, codes=codes,
@@ -508,6 +518,8 @@ class BatchEncoder:
         self.k = k
         self.n_rows = self.plan.n_rows
         self.S = fe.max_seq_len
+        if lfq.has_projections:
+            raise NotImplementedError("BatchEncoder: LFQ with projections runs through encode_batch")
         self.norm = patchnorm.state(thresholds=not want_patches)
         self.lcfg = lfq.cfg()
         self.p = fe.params()

@@ -1,0 +1,105 @@
+"""LFQ with projections through the fused encode_batch / decode_batch
+(lfq.py:54-62: dim != codebook_dim * num_codebooks inserts Linear project_in /
+project_out; conf/patch14-l.json's 16 codebooks of 2^13 over 196-element
+tokens: 196 -> 208 -> 196), against the CPU oracle.  Run on an MI355X.
+
+Tolerances (stated per test):
+  * codes: given the GPU's own PatchNorm output y (bit-exact PatchNorm of
+    tokens test_gpu_parity already pins), a bit may differ from the oracle's
+    LFQ(project_in(y)) only where the oracle's projected value h lies inside
+    the fp32 GEMM rounding band |h| <= 4e-6 * (|W| |y| + |b|);
+  * decode: RGB within 1e-5 of the image range (+2e-5 relative) of the
+    oracle's decode of the same codes (project_out -> inverse PatchNorm ->
+    revert_patching -> IDCT -> IPT -> RGB).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_cpu, rng
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CFG = ref_cpu.FEConfig()
+LCFG = ref_cpu.LFQConfig(dim=196, codebook_size=2 ** 13, num_codebooks=16)
+
+
+@pytest.fixture(scope="module")
+def fe(pkg):
+    return pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, 32, 32, 3072)
+
+
+@pytest.fixture(scope="module")
+def pn(pkg, ref_tables):
+    m = pkg.PatchNorm(32, 32, 14, 3).to(DEV)
+    m.median.data.copy_(ref_tables.median)
+    m.b.data.copy_(ref_tables.b)
+    m.n.data.copy_(ref_tables.n)
+    m.frozen = True
+    return m.eval()
+
+
+@pytest.fixture(scope="module")
+def lfq_p(pkg):
+    torch.manual_seed(5)
+    m = pkg.LFQ(dim=196, codebook_size=2 ** 13, num_codebooks=16)
+    assert m.has_projections and LCFG.has_projections
+    return m.to(DEV).eval()
+
+
+def _w(lin):
+    return lin.weight.detach().cpu(), lin.bias.detach().cpu()
+
+
+def _images(seed, sizes):
+    return [torch.from_numpy(x).to(DEV) for x in rng.synth_images(seed, sizes)]
+
+
+@pytest.mark.parametrize("sizes", [[(224, 224), (300, 500), (97, 1000)], [(512, 512)]])
+def test_encode_batch_with_projections(fe, pn, lfq_p, sizes):
+    imgs = _images(77, sizes)
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p, return_patches=True)
+    R, S = dp.key_pad_mask.shape
+    assert codes.shape == (R, S, 16) and codes.dtype == torch.long
+    y = dp.patches.cpu()                       # PatchNorm output, pads included
+    W, b = _w(lfq_p.project_in)
+    h = F.linear(y, W, b)
+    _, oidx = ref_cpu.lfq_forward(y, LCFG, project_in=lambda t: F.linear(t, W, b))
+    g = codes.cpu()
+    diff = g != oidx
+    band = 4e-6 * F.linear(y.abs(), W.abs(), b.abs())
+    near = (h.abs() <= band).view(R, S, 16, 13).any(-1)
+    assert torch.all(near[diff]), "code mismatch outside the GEMM rounding band"
+    flips, n = int(diff.sum()), g.numel()
+    print(f"[{sizes}] projected-code mismatches inside the band: {flips} / {n}")
+    assert flips <= max(2, n // 1000)
+    # the codes do not depend on whether the normalised tokens are returned
+    ((dp2, codes2),) = fe.encode_batch(imgs, pn, lfq_p)
+    assert torch.equal(codes2.cpu(), g) and dp2.patches.shape[-1] == 0
+    assert torch.equal(dp2.key_pad_mask, dp.key_pad_mask) and torch.equal(dp2.patch_positions, dp.patch_positions)
+
+
+def test_decode_batch_with_projections(fe, pn, lfq_p, ref_tables):
+    imgs = _images(78, [(224, 224), (300, 500), (512, 512)])
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p)
+    out = fe.decode_batch(dp, codes, pn, lfq_p)
+    Wo, bo = _w(lfq_p.project_out)
+    q = ref_cpu.lfq_indices_to_codes(codes.cpu(), LCFG, project_out=lambda t: F.linear(t, Wo, bo))
+    kp, ids, pos, ch = (dp.key_pad_mask.cpu(), dp.batched_image_ids.cpu(), dp.patch_positions.cpu(),
+                        dp.patch_channels.cpu())
+    x = ref_cpu.norm_inverse(ref_tables, q, ch, pos[..., 0], pos[..., 1])
+    batch = ref_cpu.Batch(x, kp, None, ids, ch, pos, list(dp.patch_sizes), list(dp.original_sizes))
+    ref = ref_cpu.postprocess(batch, CFG)
+    assert len(out) == len(ref) == len(imgs)
+    for a, r in zip(out, ref):
+        assert a.shape == r.shape
+        scale = max(1.0, float(r.abs().max()))
+        d = (a.cpu() - r).abs()
+        assert torch.all(d <= 1e-5 * scale + 2e-5 * r.abs()), (float(d.max()), scale)
+
+
+def test_batch_encoder_refuses_projections(pkg, fe, pn, lfq_p):
+    from importlib import import_module
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    with pytest.raises(NotImplementedError):
+        fe_mod.BatchEncoder(fe, 2, 224, 224, pn, lfq_p, device=DEV)
