@@ -116,9 +116,10 @@ __device__ inline void token_epilogue(const EncParams& ep, int c, int h, int w, 
 // codebook per tile row (codebook_dim == P): lane j's code is its row's sign
 // bits in MSB-first order (lfq.py:187), i.e. a bit reversal — no exchange.
 // vals: this lane's row, thr: thresholds row (nullable -> PatchNorm values).
+// ny (optional): receives this lane's PatchNorm values (computed, not stored).
 template <int P>
 __device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int h, int w, int j,
-                                                 const float* vals, int64_t tok, TokenSinks sk) {
+                                                 const float* vals, int64_t tok, TokenSinks sk, float* ny = nullptr) {
   constexpr int PP = P * P;
   float amax = 0.0f;
   uint32_t bits = 0;
@@ -131,12 +132,13 @@ __device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int
       for (int p2 = 0; p2 < P; ++p2) sk.raw[tok * PP + j * P + p2] = vals[p2];
     }
     if (ep.median) {
-      if (sk.norm || !ep.thr) {
+      if (sk.norm || ny || !ep.thr) {
 #pragma unroll
         for (int p2 = 0; p2 < P; ++p2) {
           const float y = pn_forward(vals[p2], ep.median[tab + p2], ep.b[tab + p2], ep.eps, ep.min_val, ep.max_val);
           bits |= (y > 0.0f ? 1u : 0u) << p2;
           if (sk.norm) sk.norm[tok * PP + j * P + p2] = y;
+          if (ny) ny[p2] = y;
         }
       } else if ((P & 1) == 0) {
         const float2* t2 = reinterpret_cast<const float2*>(ep.thr + tab);

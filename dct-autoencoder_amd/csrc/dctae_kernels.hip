@@ -498,6 +498,32 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
   }
 }
 
+// packed-order copy of the staged tokens (PP floats each) of one image:
+// 16-byte pieces when PP % 4 == 0 and every base is 16-byte aligned (196 =
+// 49 x 4 at P = 14), 32-bit index math (k * PP <= 3072 * 196)
+__device__ __forceinline__ void gather_tokens(const ImgDesc& d, const uint16_t* order, int64_t base, int PP,
+                                              const TokenSinks& st, const PackSinks& out, int tid, int nt) {
+  const bool vec = (PP & 3) == 0 && ((reinterpret_cast<uintptr_t>(out.patches) | reinterpret_cast<uintptr_t>(out.raw) |
+                                      reinterpret_cast<uintptr_t>(st.norm) | reinterpret_cast<uintptr_t>(st.raw)) & 15) == 0;
+  if (vec) {
+    const uint32_t P4 = (uint32_t)PP >> 2, n = (uint32_t)d.k * P4;
+    for (uint32_t e = tid; e < n; e += nt) {
+      const uint32_t t = e / P4, q = e - t * P4;
+      const int64_t src = (d.tok_off + order[t]) * P4 + q, dst = (base + t) * P4 + q;
+      if (out.patches) reinterpret_cast<float4*>(out.patches)[dst] = reinterpret_cast<const float4*>(st.norm)[src];
+      if (out.raw) reinterpret_cast<float4*>(out.raw)[dst] = reinterpret_cast<const float4*>(st.raw)[src];
+    }
+    return;
+  }
+  const uint32_t n = (uint32_t)d.k * (uint32_t)PP;
+  for (uint32_t e = tid; e < n; e += nt) {
+    const uint32_t t = e / (uint32_t)PP, q = e - t * (uint32_t)PP;
+    const int64_t src = (d.tok_off + order[t]) * PP + q, dst = (base + t) * PP + q;
+    if (out.patches) out.patches[dst] = st.norm[src];
+    if (out.raw) out.raw[dst] = st.raw[src];
+  }
+}
+
 // Same contract with rocPRIM's block radix sort (LSD, stable): 32-bit score
 // keys sorted descending, flat indices as values; stability keeps equal
 // scores in ascending index order = the (score desc, index asc) order above.
@@ -553,14 +579,7 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
       out.codes[(base + t) * ncb + q] = st.codes[(d.tok_off + order[t]) * ncb + q];
     }
   }
-  if (out.patches || out.raw) {
-    for (int64_t e = tid; e < (int64_t)d.k * PP; e += kSortBS) {
-      const int t = (int)(e / PP), q = (int)(e % PP);
-      const uint32_t f = order[t];
-      if (out.patches) out.patches[(base + t) * PP + q] = st.norm[(d.tok_off + f) * PP + q];
-      if (out.raw) out.raw[(base + t) * PP + q] = st.raw[(d.tok_off + f) * PP + q];
-    }
-  }
+  if (out.patches || out.raw) gather_tokens(d, order, base, PP, st, out, tid, kSortBS);
 }
 
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,

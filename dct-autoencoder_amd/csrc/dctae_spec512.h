@@ -53,6 +53,18 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
   constexpr int KS = 14, EPR = 2;
   const int tid = opaque_tid();
   const int g16 = tid >> 4, jl = tid & 15;
+  // token outputs (raw DCT / PatchNorm) leave through LDS: tile h's 14 rows
+  // of 14 are the 196 contiguous floats X[196 h ..], the token's staged
+  // layout, so the whole block stores them as 16-byte pieces (49 per token)
+  // instead of 14 scattered 4-byte stores per lane
+  float* Xf = reinterpret_cast<float*>(const_cast<f2v*>(X2));
+  auto store_tokens = [&](float* dst) {
+    for (int e = tid; e < d.qh * 49; e += 256) {
+      const int h = e / 49, q = e - h * 49;
+      const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
+      reinterpret_cast<float4*>(dst + tok * (KS * KS))[q] = reinterpret_cast<const float4*>(Xf + KS * KS * h)[q];
+    }
+  };
   if (THR) {
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
@@ -73,20 +85,21 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
         const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
         if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
         if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
-        if (sk.raw && jl < KS) {
-#pragma unroll
-          for (int p = 0; p < KS / 2; ++p) {
-            const f2v v2 = row[p];
-            sk.raw[tok * KS * KS + jl * KS + 2 * p] = v2.x;
-            sk.raw[tok * KS * KS + jl * KS + 2 * p + 1] = v2.y;
-          }
-        }
       }
     }
+    if (sk.raw) store_tokens(sk.raw);
   } else {
+    const bool norm = sk.norm && ep.median;
+    if (sk.raw) {
+      store_tokens(sk.raw);
+      if (norm) __syncthreads();   // raw reads before the in-place PatchNorm below
+    }
+    TokenSinks sc = sk;
+    sc.raw = nullptr;
+    sc.norm = nullptr;
     for (int h = g16; h < d.qh; h += 16) {
       float vals[KS];
-      const f2v* row = X2 + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
+      f2v* row = reinterpret_cast<f2v*>(Xf) + (KS * h + (jl < KS ? jl : 0)) * (KS / 2);
 #pragma unroll
       for (int p = 0; p < KS / 2; ++p) {
         const f2v v2 = row[p];
@@ -94,7 +107,20 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
         vals[2 * p + 1] = v2.y;
       }
       const int f = (h * d.qw + strip) * ep.C + c;
-      token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sk);
+      if (norm) {   // scores, codes and the PatchNorm values (patchnorm.py:157-165), written back in place
+        float y[KS];
+        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sc, y);
+        if (jl < KS) {
+#pragma unroll
+          for (int p = 0; p < KS / 2; ++p) row[p] = (f2v){y[2 * p], y[2 * p + 1]};
+        }
+      } else {
+        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sc);   // scores, codes
+      }
+    }
+    if (norm) {
+      __syncthreads();
+      store_tokens(sk.norm);
     }
   }
 }

@@ -427,8 +427,8 @@ class DCTAutoencoderFeatureExtractor:
             res = _ops.encode(sub, dev, self.params(), plan_local, plan.n_rows, self.max_seq_len, norm, lcfg,
                               want_codes=lcfg is not None, want_patches=want_norm, want_raw=return_raw,
                               want_scores=return_scores)
-            if proj:
-                _, res["codes"], _, _ = lfq(res["patches"], mask=~res["key_pad_mask"])
+            if proj:   # codes only: lfq.py:136-187 without the quantized output's project_out
+                _, res["codes"] = _ops.lfq_forward(lfq.project_in(res["patches"]), lfq.cfg(), want_quantized=False)
             pt = res["patches"] if return_patches else res.get("raw")
             if pt is None:
                 pt = torch.empty((plan.n_rows, self.max_seq_len, 0), device=dev)
