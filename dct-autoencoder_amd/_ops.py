@@ -291,6 +291,39 @@ def lfq_codes(idx: torch.Tensor, cfg: LFQCfg) -> torch.Tensor:
     return out
 
 
+def lfq_project_in(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], cfg: LFQCfg) -> torch.Tensor:
+    """LFQ.forward's indices with project_in fused (dctae_lfq_project_in):
+    x (..., dim) -> (..., num_codebooks) int64.  w / b: project_in's fp32
+    weight (ncb*cd, dim) and bias on x's device."""
+    dev = _check_dev(x, w, b)
+    ctx = _lib.context(dev)
+    xs = x.float().contiguous()
+    dim = xs.shape[-1]
+    n = xs.numel() // dim
+    idx = torch.empty((*xs.shape[:-1], cfg.num_codebooks), dtype=torch.long, device=dev)
+    rc = ctx.lib.dctae_lfq_project_in(ctx.h, C.byref(cfg), ptr(xs), n, dim, ptr(w), ptr(b), ptr(idx),
+                                      _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_lfq_project_in")
+    return idx
+
+
+def lfq_project_out(idx: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], cfg: LFQCfg) -> torch.Tensor:
+    """LFQ.indices_to_codes with project_out fused (dctae_lfq_project_out):
+    idx (..., num_codebooks) -> (..., dim) fp32; w (dim, ncb*cd), b (dim)."""
+    dev = _check_dev(idx, w, b)
+    ctx = _lib.context(dev)
+    ii = idx.long().contiguous()
+    if ii.shape[-1] != cfg.num_codebooks:
+        raise AssertionError("last dim of indices must be num_codebooks")
+    dim = w.shape[0]
+    n = ii.numel() // cfg.num_codebooks
+    out = torch.empty((*ii.shape[:-1], dim), dtype=torch.float32, device=dev)
+    rc = ctx.lib.dctae_lfq_project_out(ctx.h, C.byref(cfg), ptr(ii), n, dim, ptr(w), ptr(b), ptr(out),
+                                       _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_lfq_project_out")
+    return out
+
+
 def vq_forward(cfg: VQCfg, x: torch.Tensor, mask: Optional[torch.Tensor], want_quantized=True):
     """x (n, dim) fp32 contiguous on the device; mask (n) bool or None.
     Returns quantize (n, dim) (None unless wanted) and indices (n, heads)."""

@@ -1622,6 +1622,42 @@ int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64
   return 0;
 }
 
+static int lfq_proj_check(dctae_ctx* ctx, const dctae_lfq* lfq, int64_t n, int32_t dim, const void* a,
+                          const float* w, const void* o) {
+  if (!lfq || lfq->codebook_dim < 1 || lfq->codebook_dim > 31 || lfq->num_codebooks < 1 || lfq->num_codebooks > 64)
+    return fail(ctx, DCTAE_EINVAL, "bad LFQ config (codebook_dim <= 31, num_codebooks <= 64)");
+  const int64_t cdims = (int64_t)lfq->codebook_dim * lfq->num_codebooks;
+  if (dim < 4 || dim > 256 || dim % 4 != 0 || cdims > 256 || cdims % 4 != 0)
+    return fail(ctx, DCTAE_EINVAL, "LFQ projections: dim and codebook_dim * num_codebooks must be multiples of 4 <= 256");
+  if (n < 0 || (n > 0 && (!a || !w || !o))) return fail(ctx, DCTAE_EINVAL, "bad LFQ projection tensors");
+  if (((uintptr_t)a | (uintptr_t)w) & 15) return fail(ctx, DCTAE_EINVAL, "LFQ projections need 16-byte aligned tensors");
+  return 0;
+}
+
+int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, int32_t dim,
+                         const float* w, const float* b, int64_t* idx, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (int rc = lfq_proj_check(ctx, lfq, n, dim, x, w, idx)) return rc;
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "lfq_project_in");
+  launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, idx, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
+int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* idx, int64_t n, int32_t dim,
+                          const float* w, const float* b, float* out, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (int rc = lfq_proj_check(ctx, lfq, n, dim, idx, w, out)) return rc;
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "lfq_project_out");
+  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out, s);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
 // ---- VectorQuantize inference (dctae_vq.hip) --------------------------------
 static int vq_check(dctae_ctx* ctx, const dctae_vq* vq) {
   if (!vq || vq->codebook_dim != 16 || vq->heads < 1 || vq->codebook_size < 1 || vq->dim < 1 || !vq->embed_dev)

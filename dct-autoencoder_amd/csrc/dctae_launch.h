@@ -31,6 +31,11 @@ void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t 
 void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float scale, float* q, int64_t* idx,
                         hipStream_t s);
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
+// dctae_lfq_proj.hip: LFQ with projections, fused project_in + sign + pack / codes + project_out
+void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
+                           int64_t* idx, hipStream_t s);
+void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
+                            float scale, float* out, hipStream_t s);
 // VectorQuantize inference (dctae_vq.hip)
 void launch_vq_bias(float* y, const float* bias, int64_t n, int cols, const uint8_t* mask, const float* orig,
                     hipStream_t s);

@@ -1,0 +1,200 @@
+// LFQ with projections (lfq.py:54-62: dim != codebook_dim * num_codebooks puts
+// nn.Linear project_in / project_out around the quantiser; conf/patch14-l.json:
+// 196-element tokens -> 16 codebooks x 13 bits = 208).  Both directions are one
+// fused kernel each on v_mfma_f32_16x16x4_f32 (f32 operands, f32 accumulate):
+//
+//  mode 0, encode (lfq.py:164 project_in, :175-187 sign + index packing):
+//    h = x W_in^T + b_in; bit = h > 0 (NaN -> 0); index of codebook c =
+//    sum_b bit[c cd + b] 2^(cd - 1 - b) (mask = 2^arange(cd-1..0), lfq.py:70).
+//    h never leaves the CU: four 16-bit sign ballots per 16x16 tile go to LDS
+//    and each lane assembles (token, codebook) indices from them.
+//  mode 1, decode (lfq.py:105-127 indices_to_codes + project_out):
+//    codes = +-scale from the index bits (bits * 2 scale - scale, lfq.py:117-124),
+//    built straight into the LDS A tile; out = codes W_out^T + b_out.
+//
+// Tile: 64 tokens per 256-thread block (16 per wave), all N <= 256 outputs per
+// wave (NT tiles of 16: NT x 4 accumulators), K in chunks of 16 with the next
+// chunk's global loads in flight during the current chunk's MFMAs.  Lane
+// (r = l & 15, q = l >> 4) reads float4 k = 4q .. 4q + 3 of its A row (token)
+// and B row (output feature); MFMA step s pairs k = 4q + s on both sides, so
+// the 16 k of a chunk are covered once (the order of the f32 sum differs from
+// torch's: results are not bit-equal to nn.Linear, see tests/test_gpu_lfq_proj.py).
+#include "dctae_device.h"
+#include "dctae_launch.h"
+
+namespace dctae {
+
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTok = 64;     // tokens per block
+constexpr int kKc = 16;      // k chunk
+constexpr int kLd = kKc + 4; // LDS row stride (floats)
+
+template <int NT, int MODE>
+__global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
+                                                 int64_t n, int K, int N, const float* __restrict__ w,
+                                                 const float* __restrict__ bias, int cd, int ncb, float scale,
+                                                 int64_t* __restrict__ idx_out, float* __restrict__ out) {
+  constexpr int NP = NT * 16;                      // padded output features
+  constexpr int WV = (NP * 4 + 255) / 256;         // W float4 per thread and chunk
+  __shared__ __attribute__((aligned(16))) float Ws[NP * kLd];
+  __shared__ __attribute__((aligned(16))) float As[kTok * kLd];
+  __shared__ int32_t Ix[MODE == 1 ? kTok * 64 : 1];            // mode 1: the block's indices (ncb <= 64)
+  __shared__ uint32_t Msk[MODE == 0 ? 4 * 16 * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t tok0 = (int64_t)blockIdx.x * kTok;
+  const int nt = n - tok0 < kTok ? (int)(n - tok0) : kTok;
+
+  if (MODE == 1) {
+    for (int e = tid; e < kTok * ncb; e += 256) {
+      const int t = e / ncb;
+      Ix[e] = t < nt ? (int32_t)idx_in[tok0 * ncb + e] : 0;   // lfq.py:117 indices.int()
+    }
+    __syncthreads();
+  }
+
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // A element (token at, k chunk piece aq): thread tid stages token tid >> 2, float4 tid & 3
+  const int at = tid >> 2, aq = tid & 3;
+  float4 ra, rw[WV];
+  auto load = [&](int k0) {
+    const int k = k0 + 4 * aq;
+    if (MODE == 0) {
+      ra = (at < nt && k < K) ? *reinterpret_cast<const float4*>(x + (tok0 + at) * K + k)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kk = k + e;
+        const int c = kk / cd, b = kk - c * cd;
+        const bool bit = kk < K && ((Ix[at * ncb + (kk < K ? c : 0)] >> (cd - 1 - b)) & 1);
+        v[e] = kk < K ? (bit ? scale : -scale) : 0.f;
+      }
+      ra = make_float4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < WV; ++i) {
+      const int e = tid + 256 * i;
+      const int row = e >> 2, kk = k0 + 4 * (e & 3);
+      rw[i] = (row < N && kk < K) ? *reinterpret_cast<const float4*>(w + (int64_t)row * K + kk)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&]() {
+    *reinterpret_cast<float4*>(&As[at * kLd + 4 * aq]) = ra;
+#pragma unroll
+    for (int i = 0; i < WV; ++i) {
+      const int e = tid + 256 * i;
+      if (e < NP * 4) *reinterpret_cast<float4*>(&Ws[(e >> 2) * kLd + 4 * (e & 3)]) = rw[i];
+    }
+  };
+
+  load(0);
+  store();
+  __syncthreads();
+  for (int k0 = 0; k0 < K; k0 += kKc) {
+    const bool more = k0 + kKc < K;
+    if (more) load(k0 + kKc);
+    const float4 a4 = *reinterpret_cast<const float4*>(&As[(wave * 16 + r) * kLd + 4 * q]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const float4 b4 = *reinterpret_cast<const float4*>(&Ws[(t * 16 + r) * kLd + 4 * q]);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, acc[t], 0, 0, 0);
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+
+  // C/D map: lane l, register v -> token 4 (l >> 4) + v of the wave, feature 16 t + (l & 15)
+  if (MODE == 0) {
+    uint32_t* msk = Msk + wave * 16 * (NT + 3);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + r;
+      const float bb = (bias && col < N) ? bias[col] : 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float h = acc[t][v] + bb;
+        const uint64_t m = __ballot(col < N && h > 0.0f);   // lfq.py:175 (NaN -> False)
+        if (lane < 4) msk[(4 * lane + v) * (NT + 3) + t] = (uint32_t)(m >> (16 * lane)) & 0xffffu;
+      }
+    }
+    if (lane < 16 * 3) msk[(lane / 3) * (NT + 3) + NT + lane % 3] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // (token i, codebook c) pairs of the wave, token-major: contiguous int64 stores
+    const int64_t wt0 = tok0 + wave * 16;
+    const int wn = n - wt0 <= 0 ? 0 : n - wt0 < 16 ? (int)(n - wt0) : 16;
+    for (int p = lane; p < wn * ncb; p += 64) {
+      const int i = p / ncb, c = p - i * ncb;
+      const int o0 = c * cd, pc = o0 >> 4, sh = o0 & 15;
+      const uint32_t* mi = msk + i * (NT + 3);
+      const uint64_t win = (uint64_t)mi[pc] | ((uint64_t)mi[pc + 1] << 16) | ((uint64_t)mi[pc + 2] << 32) |
+                           ((uint64_t)mi[pc + 3] << 48);
+      const uint32_t bits = (uint32_t)(win >> sh) & ((1u << cd) - 1u);   // bit b = feature o0 + b
+      idx_out[wt0 * ncb + p] = (int64_t)(__builtin_bitreverse32(bits) >> (32 - cd));
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + r;
+      if (col >= N) continue;
+      const float bb = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = wave * 16 + 4 * q + v;
+        if (row < nt) out[(tok0 + row) * N + col] = acc[t][v] + bb;
+      }
+    }
+  }
+}
+
+template <int MODE>
+void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
+               const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out) {
+#define DCTAE_LFQP(T) \
+  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE>), g, dim3(256), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out); break;
+  switch (nt) {
+    DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
+    DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
+    DCTAE_LFQP(14) DCTAE_LFQP(15) DCTAE_LFQP(16)
+    default: break;
+  }
+#undef DCTAE_LFQP
+}
+
+}  // namespace
+
+// x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
+void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
+                           int64_t* idx, hipStream_t s) {
+  const int N = cd * ncb;
+  if (n <= 0) return;
+  launch_nt<0>((N + 15) / 16, dim3((unsigned)((n + kTok - 1) / kTok)), s, x, nullptr, n, D, N, w, b, cd, ncb, 0.f,
+               idx, nullptr);
+}
+
+// indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)
+void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
+                            float scale, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  launch_nt<1>((D + 15) / 16, dim3((unsigned)((n + kTok - 1) / kTok)), s, nullptr, idx, n, cd * ncb, D, w, b, cd,
+               ncb, scale, nullptr, out);
+}
+
+}  // namespace dctae

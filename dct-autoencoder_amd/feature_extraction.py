@@ -411,8 +411,8 @@ class DCTAutoencoderFeatureExtractor:
             raise AssertionError("LFQ codes need a PatchNorm")
         # LFQ with projections (dim != codebook_dim * num_codebooks, lfq.py:54-62,
         # e.g. conf/patch14-l.json's 196 -> 16 x 13): the fused launch stops at the
-        # PatchNorm output, project_in (a plain fp32 GEMM) and the HIP sign / pack
-        # kernel follow on the same stream
+        # PatchNorm output and the fused project_in + sign + pack kernel
+        # (dctae_lfq_project_in) follows on the same stream
         proj = lfq is not None and lfq.has_projections
         want_norm = return_patches or proj
         norm = patchnorm.state(thresholds=not want_norm) if patchnorm is not None else None
@@ -428,7 +428,7 @@ class DCTAutoencoderFeatureExtractor:
                               want_codes=lcfg is not None, want_patches=want_norm, want_raw=return_raw,
                               want_scores=return_scores)
             if proj:   # codes only: lfq.py:136-187 without the quantized output's project_out
-                _, res["codes"] = _ops.lfq_forward(lfq.project_in(res["patches"]), lfq.cfg(), want_quantized=False)
+                res["codes"] = lfq.project_codes(res["patches"])   # fused project_in + sign + pack
             pt = res["patches"] if return_patches else res.get("raw")
             if pt is None:
                 pt = torch.empty((plan.n_rows, self.max_seq_len, 0), device=dev)
@@ -481,7 +481,7 @@ class DCTAutoencoderFeatureExtractor:
     def decode_batch(self, dct_patches: DCTPatches, codes: torch.Tensor, patchnorm, lfq) -> List[torch.Tensor]:
         """LFQ.indices_to_codes -> PatchNorm.inverse_norm -> postprocess, fused
         (the decode half of SURVEY §3.4 without the transformer).  With LFQ
-        projections the codes go through project_out (fp32 GEMM) and the HIP
+        projections the codes go through the fused codes -> project_out kernel and the HIP
         inverse PatchNorm first, and the fused decode starts from the tokens."""
         if lfq.has_projections:
             dp = dct_patches.shallow_copy()

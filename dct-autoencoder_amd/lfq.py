@@ -5,9 +5,13 @@ Same constructor arguments, buffers (``mask``, ``zero``, ``codebook``),
 ``indices_to_codes``.  The sign quantisation and index packing run as HIP
 kernels (dctae_lfq_forward / dctae_lfq_indices_to_codes).  When
 ``dim != codebook_dim * num_codebooks`` the reference inserts Linear
-projections; those are plain GEMMs and run through torch (hipBLASLt) around
-the kernels.  The training-only losses (commit / entropy, lfq.py:189-204) are
-out of scope of this build.
+projections (lfq.py:54-62); those run fused with the quantiser as MFMA
+kernels (dctae_lfq_project_in: project_in + sign + packing, the projected
+features never stored; dctae_lfq_project_out: index bits -> +-scale codes ->
+project_out).  The module's nn.Linear weights stay the parameters (state dicts
+interchange with the reference); the kernels read fp32 copies of them.
+The training-only losses (commit / entropy, lfq.py:189-204) are out of scope
+of this build.
 """
 from __future__ import annotations
 
@@ -58,6 +62,33 @@ class LFQ(nn.Module):
             bits = ((torch.arange(codebook_size)[..., None].int() & self.mask) != 0).float()
             self.register_buffer("codebook", bits * codebook_scale * 2 - codebook_scale, persistent=False)
 
+    def _fused_proj(self) -> bool:
+        cdims = self.codebook_dim * self.num_codebooks
+        return (self.has_projections and self.dim % 4 == 0 and 4 <= self.dim <= 256 and cdims % 4 == 0
+                and cdims <= 256 and self.codebook_dim <= 31 and self.num_codebooks <= 64)
+
+    def _proj_w(self, lin: nn.Linear, dev):
+        """fp32 contiguous copies of a projection's weight / bias on ``dev``
+        (cached per parameter version: a .half() model or an optimiser step
+        refreshes them)."""
+        key = (id(lin), dev, lin.weight._version, lin.weight.data_ptr(),
+               None if lin.bias is None else (lin.bias._version, lin.bias.data_ptr()))
+        cache = self.__dict__.setdefault("_proj_cache", {})
+        if cache.get(id(lin), (None,))[0] != key:
+            w = lin.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
+            b = None if lin.bias is None else lin.bias.detach().to(device=dev, dtype=torch.float32).contiguous()
+            cache[id(lin)] = (key, w, b)
+        return cache[id(lin)][1:]
+
+    def project_codes(self, x):
+        """Indices only (the encode path): x (..., dim) -> (..., num_codebooks),
+        project_in fused with the sign / packing when there are projections."""
+        if self._fused_proj():
+            w, b = self._proj_w(self.project_in, x.device)
+            return _ops.lfq_project_in(x, w, b, self.cfg())
+        _, idx = _ops.lfq_forward(self.project_in(x), self.cfg(), want_quantized=False)
+        return idx
+
     def cfg(self) -> LFQCfg:
         return LFQCfg(self.codebook_dim, self.num_codebooks, float(self.codebook_scale))
 
@@ -73,9 +104,13 @@ class LFQ(nn.Module):
         is_img_or_video = indices.ndim >= (3 + int(self.keep_num_codebooks_dim))
         if not self.keep_num_codebooks_dim:
             indices = rearrange(indices, "... -> ... 1")
-        codes = _ops.lfq_codes(indices, self.cfg()).to(self.dtype)
-        if project_out:
-            codes = self.project_out(codes)
+        if project_out and self._fused_proj():
+            w, b = self._proj_w(self.project_out, indices.device)
+            codes = _ops.lfq_project_out(indices, w, b, self.cfg()).to(self.project_out.weight.dtype)
+        else:
+            codes = _ops.lfq_codes(indices, self.cfg()).to(self.dtype)
+            if project_out:
+                codes = self.project_out(codes)
         if is_img_or_video:
             codes = rearrange(codes, "b ... d -> b d ...")
         return codes
@@ -93,9 +128,16 @@ class LFQ(nn.Module):
             shape = x.shape
             x = x.reshape(shape[0], -1, shape[-1])
         assert x.shape[-1] == self.dim, f"expected dimension of {self.dim} but received {x.shape[-1]}"
-        x = self.project_in(x)
-        q, indices = _ops.lfq_forward(x, self.cfg())
-        q = self.project_out(q.to(x.dtype))   # the reference keeps the input dtype (fp16 / bf16 models)
+        if self._fused_proj():
+            # eval: quantized = +-scale of the index bits, so project_out(quantized)
+            # is the decode kernel on the indices (lfq.py:164-212)
+            indices = self.project_codes(x)
+            w, b = self._proj_w(self.project_out, x.device)
+            q = _ops.lfq_project_out(indices, w, b, self.cfg()).to(x.dtype)
+        else:
+            x = self.project_in(x)
+            q, indices = _ops.lfq_forward(x, self.cfg())
+            q = self.project_out(q.to(x.dtype))   # the reference keeps the input dtype (fp16 / bf16 models)
         if is_img_or_video:
             q = q.reshape(*shape[:-1], q.shape[-1])
             q = rearrange(q, "b ... d -> b d ...")

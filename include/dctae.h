@@ -208,6 +208,21 @@ int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, 
 int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev,
                                int64_t n, float* codes_dev, void* stream);
 
+/* LFQ with projections (lfq.py:54-62, dim != codebook_dim * num_codebooks),
+ * encode direction: LFQ.forward's indices (lfq.py:164 project_in, :175-187
+ * sign + packing) in one fused MFMA kernel: x (n, dim) fp32, w_in (ncb*cd,
+ * dim) and b_in (ncb*cd, nullable) as nn.Linear stores them -> indices (n,
+ * ncb) int64.  dim % 4 == 0, ncb*cd <= 256, cd <= 31; 16-byte aligned x / w. */
+int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, int64_t n, int32_t dim,
+                         const float* w_in_dev, const float* b_in_dev, int64_t* indices_dev, void* stream);
+
+/* Decode direction: LFQ.indices_to_codes with project_out (lfq.py:105-127):
+ * indices (n, ncb) -> +-scale codes -> out (n, dim) = codes w_out^T + b_out,
+ * w_out (dim, ncb*cd), b_out (dim, nullable).  dim <= 256, ncb*cd % 4 == 0,
+ * ncb <= 64, cd <= 31. */
+int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev, int64_t n, int32_t dim,
+                          const float* w_out_dev, const float* b_out_dev, float* out_dev, void* stream);
+
 /* VectorQuantize (vector_quantize.py:675-1050) as the model builds it
  * (modeling_dct_autoencoder.py:76-77): euclidean codebook shared by the
  * heads, codebook_dim 16, kmeans-initialised, affine codebook parameters,

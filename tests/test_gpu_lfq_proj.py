@@ -103,3 +103,49 @@ def test_batch_encoder_refuses_projections(pkg, fe, pn, lfq_p):
     fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
     with pytest.raises(NotImplementedError):
         fe_mod.BatchEncoder(fe, 2, 224, 224, pn, lfq_p, device=DEV)
+
+
+@pytest.mark.parametrize("dim,cd,ncb,n,bias", [(196, 13, 16, 3072 * 3 + 5, True), (196, 13, 16, 1, True),
+                                               (256, 15, 16, 700, True), (64, 5, 4, 130, False),
+                                               (196, 14, 12, 257, True), (12, 31, 4, 64, True)])
+def test_project_kernels_vs_linear(pkg, dim, cd, ncb, n, bias):
+    """dctae_lfq_project_in / _out (the fused MFMA kernels) against torch fp32
+    nn.Linear on the CPU.  Tolerance: a code bit may differ only where the CPU's
+    projected value lies in the fp32 rounding band |h| <= 4e-6 (|W| |x| + |b|);
+    project_out within 2e-5 (|W| |codes| + |b|) (the f32 sum over <= 256 terms
+    in another order)."""
+    torch.manual_seed(dim + cd + n)
+    m = pkg.LFQ(dim=dim, codebook_size=2 ** cd, num_codebooks=ncb)
+    if not bias:
+        m.project_in.bias = None
+        m.project_out.bias = None
+    m = m.to(DEV).eval()
+    assert m._fused_proj()
+    cfg = ref_cpu.LFQConfig(dim=dim, codebook_size=2 ** cd, num_codebooks=ncb)
+    x = torch.randn(n, dim)
+    x[0, :3] = float("nan") if n > 1 else x[0, :3]
+    W, b = m.project_in.weight.detach().cpu(), m.project_in.bias
+    b = None if b is None else b.detach().cpu()
+    idx = m.project_codes(x.to(DEV)).cpu()
+    h = F.linear(x, W, b)
+    _, oidx = ref_cpu.lfq_forward(x[None], cfg, project_in=lambda t: F.linear(t, W, b))
+    oidx = oidx[0]
+    diff = idx != oidx
+    band = 4e-6 * F.linear(x.abs(), W.abs(), None if b is None else b.abs())
+    near = (h.abs() <= band).view(n, ncb, cd).any(-1)
+    if n > 1:   # the NaN row: every bit of a codebook touching a NaN feature is 0 on both sides
+        near[0] = True
+    assert torch.all(near[diff]), "code mismatch outside the fp32 rounding band"
+    assert int(diff.sum()) <= max(2, idx.numel() // 1000)
+    # decode direction, on the oracle's indices
+    Wo, bo = m.project_out.weight.detach().cpu(), m.project_out.bias
+    bo = None if bo is None else bo.detach().cpu()
+    got = m.indices_to_codes(oidx.to(DEV)).cpu()
+    codes = ref_cpu.lfq_indices_to_codes(oidx, cfg)
+    ref = F.linear(codes, Wo, bo)
+    tol = 2e-5 * F.linear(codes.abs(), Wo.abs(), None if bo is None else bo.abs())
+    assert got.shape == ref.shape and torch.all((got - ref).abs() <= tol), float((got - ref).abs().max())
+    # LFQ.forward = both kernels (eval quantized = +-scale of the index bits)
+    q, i2, _, _ = m(x.to(DEV), mask=torch.ones(n, dtype=torch.bool, device=DEV))
+    assert torch.equal(i2.cpu(), idx)
+    assert torch.equal(q.cpu(), m.indices_to_codes(idx.to(DEV)).cpu())
