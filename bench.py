@@ -204,6 +204,25 @@ def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
                       "ms_per_step": round(el * 1e3, 3), "value": round(pix / el / 1e6, 1), "unit": "Mpix/s",
                       "kernels": kern,
                       "device_ms": round(sum(v["total_ms"] for v in kern.values()), 3)}
+    # conf/patch14-l.json's LFQ (16 codebooks of 2^13 over 196-element tokens: project_in
+    # 196 -> 208, lfq.py:54-62) on the headline geometry: the fused encode stops at the
+    # PatchNorm output and dctae_lfq_project_in (project_in + sign + pack) follows
+    torch.manual_seed(0)
+    lfq_p = type(lfq)(dim=196, codebook_size=2 ** 13, num_codebooks=16).to(dev).eval()
+    x3 = ops.synth_images(1024, 512, 512, seed=1234, first_index=rank * 1024, device=dev)
+    encp = fe_mod.BatchEncoder(fe, 1024, 512, 512, pn, lfq_p, device=dev)
+    encp(x3)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        encp(x3)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    out["lfq_projections"] = {"workload": "1024 x 512x512 encode with conf/patch14-l.json's LFQ (16 x 2^13, "
+                                          "project_in 196 -> 208 fused with sign / packing)",
+                              "ms_per_step": round(el * 1e3, 4), "value": round(1024 * 512 * 512 / el / 1e6, 1),
+                              "unit": "Mpix/s", "kernels": kernel_times(lib.context(dev), lambda: encp(x3), 5)}
+    del x3, encp
     return out
 
 

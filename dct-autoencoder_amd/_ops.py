@@ -295,12 +295,18 @@ def lfq_project_in(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     """LFQ.forward's indices with project_in fused (dctae_lfq_project_in):
     x (..., dim) -> (..., num_codebooks) int64.  w / b: project_in's fp32
     weight (ncb*cd, dim) and bias on x's device."""
+    return lfq_project_in_into(x, w, b, cfg, None)
+
+
+def lfq_project_in_into(x, w, b, cfg: LFQCfg, idx: Optional[torch.Tensor]) -> torch.Tensor:
     dev = _check_dev(x, w, b)
     ctx = _lib.context(dev)
     xs = x.float().contiguous()
     dim = xs.shape[-1]
     n = xs.numel() // dim
-    idx = torch.empty((*xs.shape[:-1], cfg.num_codebooks), dtype=torch.long, device=dev)
+    shape = (*xs.shape[:-1], cfg.num_codebooks)
+    if idx is None or idx.shape != shape or idx.dtype != torch.long or not idx.is_contiguous() or idx.device != dev:
+        idx = torch.empty(shape, dtype=torch.long, device=dev)
     rc = ctx.lib.dctae_lfq_project_in(ctx.h, C.byref(cfg), ptr(xs), n, dim, ptr(w), ptr(b), ptr(idx),
                                       _lib.stream_ptr(dev))
     ctx.check(rc, "dctae_lfq_project_in")

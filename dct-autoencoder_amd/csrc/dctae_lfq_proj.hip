@@ -28,21 +28,22 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kTok = 64;     // tokens per block
+constexpr int kTokW = 16;    // tokens per wave and M tile
 constexpr int kKc = 16;      // k chunk
 constexpr int kLd = kKc + 4; // LDS row stride (floats)
 
-template <int NT, int MODE>
+template <int NT, int MODE, int MT>
 __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ w,
                                                  const float* __restrict__ bias, int cd, int ncb, float scale,
                                                  int64_t* __restrict__ idx_out, float* __restrict__ out) {
+  constexpr int kTok = 64 * MT;                    // tokens per block (MT 16-token tiles per wave)
   constexpr int NP = NT * 16;                      // padded output features
   constexpr int WV = (NP * 4 + 255) / 256;         // W float4 per thread and chunk
   __shared__ __attribute__((aligned(16))) float Ws[NP * kLd];
   __shared__ __attribute__((aligned(16))) float As[kTok * kLd];
-  __shared__ int32_t Ix[MODE == 1 ? kTok * 64 : 1];            // mode 1: the block's indices (ncb <= 64)
-  __shared__ uint32_t Msk[MODE == 0 ? 4 * 16 * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
+  __shared__ int32_t Ix[MODE == 1 ? kTok * 64 : 1];   // mode 1: the block's indices (ncb <= 64)
+  __shared__ uint32_t Msk[MODE == 0 ? 4 * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
@@ -57,28 +58,34 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     __syncthreads();
   }
 
-  floatx4 acc[NT];
+  floatx4 acc[MT][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[m][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // A element (token at, k chunk piece aq): thread tid stages token tid >> 2, float4 tid & 3
+  // A staging: thread tid owns float4 tid & 3 of tokens (tid >> 2) + 64 m
   const int at = tid >> 2, aq = tid & 3;
-  float4 ra, rw[WV];
+  float4 ra[MT], rw[WV];
   auto load = [&](int k0) {
     const int k = k0 + 4 * aq;
-    if (MODE == 0) {
-      ra = (at < nt && k < K) ? *reinterpret_cast<const float4*>(x + (tok0 + at) * K + k)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
-      float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kk = k + e;
-        const int c = kk / cd, b = kk - c * cd;
-        const bool bit = kk < K && ((Ix[at * ncb + (kk < K ? c : 0)] >> (cd - 1 - b)) & 1);
-        v[e] = kk < K ? (bit ? scale : -scale) : 0.f;
+    for (int m = 0; m < MT; ++m) {
+      const int tk = at + 64 * m;
+      if (MODE == 0) {
+        ra[m] = (tk < nt && k < K) ? *reinterpret_cast<const float4*>(x + (tok0 + tk) * K + k)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = k + e;
+          const int c = kk / cd, b = kk - c * cd;
+          const bool bit = kk < K && ((Ix[tk * ncb + (kk < K ? c : 0)] >> (cd - 1 - b)) & 1);
+          v[e] = kk < K ? (bit ? scale : -scale) : 0.f;
+        }
+        ra[m] = make_float4(v[0], v[1], v[2], v[3]);
       }
-      ra = make_float4(v[0], v[1], v[2], v[3]);
     }
 #pragma unroll
     for (int i = 0; i < WV; ++i) {
@@ -89,7 +96,8 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     }
   };
   auto store = [&]() {
-    *reinterpret_cast<float4*>(&As[at * kLd + 4 * aq]) = ra;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) *reinterpret_cast<float4*>(&As[(at + 64 * m) * kLd + 4 * aq]) = ra[m];
 #pragma unroll
     for (int i = 0; i < WV; ++i) {
       const int e = tid + 256 * i;
@@ -97,20 +105,27 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     }
   };
 
+  // wave w owns tokens [16 (w + 4 m), + 16) of the block for m < MT
   load(0);
   store();
   __syncthreads();
   for (int k0 = 0; k0 < K; k0 += kKc) {
     const bool more = k0 + kKc < K;
     if (more) load(k0 + kKc);
-    const float4 a4 = *reinterpret_cast<const float4*>(&As[(wave * 16 + r) * kLd + 4 * q]);
+    float4 a4[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      a4[m] = *reinterpret_cast<const float4*>(&As[((wave + 4 * m) * kTokW + r) * kLd + 4 * q]);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const float4 b4 = *reinterpret_cast<const float4*>(&Ws[(t * 16 + r) * kLd + 4 * q]);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, acc[t], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].x, b4.x, acc[m][t], 0, 0, 0);
+        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].y, b4.y, acc[m][t], 0, 0, 0);
+        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].z, b4.z, acc[m][t], 0, 0, 0);
+        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].w, b4.w, acc[m][t], 0, 0, 0);
+      }
     }
     __syncthreads();
     if (more) {
@@ -119,56 +134,59 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     }
   }
 
-  // C/D map: lane l, register v -> token 4 (l >> 4) + v of the wave, feature 16 t + (l & 15)
-  if (MODE == 0) {
-    uint32_t* msk = Msk + wave * 16 * (NT + 3);
+  // C/D map: lane l, register v -> token 4 (l >> 4) + v of the M tile, feature 16 t + (l & 15)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = 16 * t + r;
-      const float bb = (bias && col < N) ? bias[col] : 0.f;
+  for (int m = 0; m < MT; ++m) {
+    const int64_t wt0 = tok0 + (wave + 4 * m) * kTokW;   // first token of this M tile
+    if (MODE == 0) {
+      uint32_t* msk = Msk + (wave * MT + m) * 16 * (NT + 3);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float h = acc[t][v] + bb;
-        const uint64_t m = __ballot(col < N && h > 0.0f);   // lfq.py:175 (NaN -> False)
-        if (lane < 4) msk[(4 * lane + v) * (NT + 3) + t] = (uint32_t)(m >> (16 * lane)) & 0xffffu;
+      for (int t = 0; t < NT; ++t) {
+        const int col = 16 * t + r;
+        const float bb = (bias && col < N) ? bias[col] : 0.f;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float h = acc[m][t][v] + bb;
+          const uint64_t mk = __ballot(col < N && h > 0.0f);   // lfq.py:175 (NaN -> False)
+          if (lane < 4) msk[(4 * lane + v) * (NT + 3) + t] = (uint32_t)(mk >> (16 * lane)) & 0xffffu;
+        }
       }
-    }
-    if (lane < 16 * 3) msk[(lane / 3) * (NT + 3) + NT + lane % 3] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // (token i, codebook c) pairs of the wave, token-major: contiguous int64 stores
-    const int64_t wt0 = tok0 + wave * 16;
-    const int wn = n - wt0 <= 0 ? 0 : n - wt0 < 16 ? (int)(n - wt0) : 16;
-    for (int p = lane; p < wn * ncb; p += 64) {
-      const int i = p / ncb, c = p - i * ncb;
-      const int o0 = c * cd, pc = o0 >> 4, sh = o0 & 15;
-      const uint32_t* mi = msk + i * (NT + 3);
-      const uint64_t win = (uint64_t)mi[pc] | ((uint64_t)mi[pc + 1] << 16) | ((uint64_t)mi[pc + 2] << 32) |
-                           ((uint64_t)mi[pc + 3] << 48);
-      const uint32_t bits = (uint32_t)(win >> sh) & ((1u << cd) - 1u);   // bit b = feature o0 + b
-      idx_out[wt0 * ncb + p] = (int64_t)(__builtin_bitreverse32(bits) >> (32 - cd));
-    }
-  } else {
+      if (lane < 16 * 3) msk[(lane / 3) * (NT + 3) + NT + lane % 3] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // (token i, codebook c) pairs of the tile, token-major: contiguous int64 stores
+      const int wn = n - wt0 <= 0 ? 0 : n - wt0 < kTokW ? (int)(n - wt0) : kTokW;
+      for (int p = lane; p < wn * ncb; p += 64) {
+        const int i = p / ncb, c = p - i * ncb;
+        const int o0 = c * cd, pc = o0 >> 4, sh = o0 & 15;
+        const uint32_t* mi = msk + i * (NT + 3);
+        const uint64_t win = (uint64_t)mi[pc] | ((uint64_t)mi[pc + 1] << 16) | ((uint64_t)mi[pc + 2] << 32) |
+                             ((uint64_t)mi[pc + 3] << 48);
+        const uint32_t bits = (uint32_t)(win >> sh) & ((1u << cd) - 1u);   // bit b = feature o0 + b
+        idx_out[wt0 * ncb + p] = (int64_t)(__builtin_bitreverse32(bits) >> (32 - cd));
+      }
+    } else {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = 16 * t + r;
-      if (col >= N) continue;
-      const float bb = bias ? bias[col] : 0.f;
+      for (int t = 0; t < NT; ++t) {
+        const int col = 16 * t + r;
+        if (col >= N) continue;
+        const float bb = bias ? bias[col] : 0.f;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = wave * 16 + 4 * q + v;
-        if (row < nt) out[(tok0 + row) * N + col] = acc[t][v] + bb;
+        for (int v = 0; v < 4; ++v) {
+          const int64_t row = wt0 + 4 * q + v;
+          if (row < n) out[row * N + col] = acc[m][t][v] + bb;
+        }
       }
     }
   }
 }
 
-template <int MODE>
+template <int MODE, int MT>
 void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out) {
 #define DCTAE_LFQP(T) \
-  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE>), g, dim3(256), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out); break;
+  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, MT>), g, dim3(256), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out); break;
   switch (nt) {
     DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
     DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
@@ -180,21 +198,27 @@ void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx
 
 }  // namespace
 
+template <int MODE>
+static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
+                        const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out) {
+  // MT = 1: 16 tokens per wave (106 VGPRs + 52 AGPRs at NT = 13, 3 waves / SIMD).
+  // MT = 2 (32 tokens per wave, half the W LDS reads per MFMA) measured slower:
+  // 1 wave / SIMD, project_in 3.91 vs 2.83 ms, project_out 5.37 vs 3.29 ms
+  launch_nt<MODE, 1>(nt, dim3((unsigned)((n + 63) / 64)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out);
+}
+
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                            int64_t* idx, hipStream_t s) {
-  const int N = cd * ncb;
   if (n <= 0) return;
-  launch_nt<0>((N + 15) / 16, dim3((unsigned)((n + kTok - 1) / kTok)), s, x, nullptr, n, D, N, w, b, cd, ncb, 0.f,
-               idx, nullptr);
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, idx, nullptr);
 }
 
 // indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                             float scale, float* out, hipStream_t s) {
   if (n <= 0) return;
-  launch_nt<1>((D + 15) / 16, dim3((unsigned)((n + kTok - 1) / kTok)), s, nullptr, idx, n, cd * ncb, D, w, b, cd,
-               ncb, scale, nullptr, out);
+  launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out);
 }
 
 }  // namespace dctae

@@ -518,9 +518,15 @@ class BatchEncoder:
         self.k = k
         self.n_rows = self.plan.n_rows
         self.S = fe.max_seq_len
-        if lfq.has_projections:
-            raise NotImplementedError("BatchEncoder: LFQ with projections runs through encode_batch")
-        self.norm = patchnorm.state(thresholds=not want_patches)
+        # LFQ with projections (lfq.py:54-62): the fused launch stops at the
+        # PatchNorm output and dctae_lfq_project_in (project_in + sign + pack)
+        # writes the codes on the same stream
+        self.lfq = lfq
+        self.proj = lfq.has_projections
+        if self.proj and not lfq._fused_proj():
+            raise NotImplementedError("BatchEncoder: LFQ projections of this shape run through encode_batch")
+        want_norm = want_patches or self.proj
+        self.norm = patchnorm.state(thresholds=not want_norm)
         self.lcfg = lfq.cfg()
         self.p = fe.params()
         per = 3 * height * width
@@ -536,10 +542,10 @@ class BatchEncoder:
             "image_ids": torch.empty((R, S), dtype=torch.long, device=self.dev),
             "key_pad_mask": torch.empty((R, S), dtype=torch.bool, device=self.dev),
         }
-        if want_patches:
+        if want_norm:
             self.out["patches"] = torch.empty((R, S, fe.patch_size ** 2), dtype=torch.float32, device=self.dev)
         o = self.out
-        self.po = PackedOut(ptr(o["codes"]), ptr(o["positions"]), ptr(o["channels"]), ptr(o["image_ids"]),
+        self.po = PackedOut(ptr(None if self.proj else o["codes"]), ptr(o["positions"]), ptr(o["channels"]), ptr(o["image_ids"]),
                             ptr(o["key_pad_mask"]), ptr(o.get("patches")), None, None)
         self._ncfg = self.norm.c()
         self._cfg = self.p.c(S)
@@ -554,8 +560,13 @@ class BatchEncoder:
         imgs = Images(C.c_void_p(x.data_ptr()), C.cast(self._keep[0], C.POINTER(C.c_int64)),
                       C.cast(self._keep[1], C.POINTER(C.c_int32)), self.B)
         rc = self.ctx.lib.dctae_encode(self.ctx.h, C.byref(self._cfg), C.byref(imgs), C.byref(self.packing),
-                                       C.byref(self._ncfg), C.byref(self.lcfg), C.byref(self.po), stream_ptr(self.dev))
+                                       C.byref(self._ncfg), None if self.proj else C.byref(self.lcfg),
+                                       C.byref(self.po), stream_ptr(self.dev))
         self.ctx.check(rc, "dctae_encode")
+        if self.proj:
+            w, b = self.lfq._proj_w(self.lfq.project_in, self.dev)
+            from . import _ops
+            self.out["codes"] = _ops.lfq_project_in_into(self.out["patches"], w, b, self.lcfg, self.out["codes"])
         return self.out
 
 

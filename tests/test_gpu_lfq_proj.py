@@ -98,11 +98,18 @@ def test_decode_batch_with_projections(fe, pn, lfq_p, ref_tables):
         assert torch.all(d <= 1e-5 * scale + 2e-5 * r.abs()), (float(d.max()), scale)
 
 
-def test_batch_encoder_refuses_projections(pkg, fe, pn, lfq_p):
+@pytest.mark.parametrize("B,H", [(3, 224), (2, 512)])
+def test_batch_encoder_with_projections(pkg, fe, pn, lfq_p, B, H):
+    """The pre-planned BatchEncoder (bench path) with projections equals
+    encode_batch bit for bit (same kernels, same plan)."""
     from importlib import import_module
     fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
-    with pytest.raises(NotImplementedError):
-        fe_mod.BatchEncoder(fe, 2, 224, 224, pn, lfq_p, device=DEV)
+    enc = fe_mod.BatchEncoder(fe, B, H, H, pn, lfq_p, device=DEV)
+    imgs = _images(79, [(H, H)] * B)
+    out = enc(torch.stack(imgs).contiguous())
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p)
+    assert torch.equal(out["codes"], codes) and torch.equal(out["key_pad_mask"], dp.key_pad_mask)
+    assert torch.equal(out["positions"], dp.patch_positions)
 
 
 @pytest.mark.parametrize("dim,cd,ncb,n,bias", [(196, 13, 16, 3072 * 3 + 5, True), (196, 13, 16, 1, True),
