@@ -78,6 +78,8 @@ _SIGS = {
     "dctae_set_color_matrices": ([_P, _P, _P, _P, _P], C.c_int),
     "dctae_encode": ([_P, C.POINTER(FECfg), C.POINTER(Images), C.POINTER(Packing), C.POINTER(Norm),
                       C.POINTER(LFQCfg), C.POINTER(PackedOut), _P], C.c_int),
+    "dctae_encode_lfq_proj": ([_P, C.POINTER(FECfg), C.POINTER(Images), C.POINTER(Packing), C.POINTER(Norm),
+                               C.POINTER(LFQCfg), _P, _P, C.POINTER(PackedOut), _P], C.c_int),
     "dctae_spectrum_tokens": ([_P, C.POINTER(FECfg), C.POINTER(Images), C.POINTER(C.c_int64), _P, _P, _P],
                               C.c_int),
     "dctae_dct2": ([_P, _P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, _P, _P], C.c_int),

@@ -1107,7 +1107,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
 static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
                        const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
                        const dctae_packed_out* out, const int64_t* tok_off_user, float* tokens_dev,
-                       float* scores_dev, hipStream_t s) {
+                       float* scores_dev, hipStream_t s, const float* proj_w = nullptr,
+                       const float* proj_b = nullptr) {
   int rc = check_cfg(ctx, cfg);
   if (rc) return rc;
   if (!imgs || imgs->n_img < 0 || (imgs->n_img > 0 && (!imgs->rgb_dev || !imgs->img_off || !imgs->hw)))
@@ -1120,7 +1121,12 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     if (!out || !out->positions_dev || !out->channels_dev || !out->image_ids_dev || !out->key_pad_dev)
       return fail(ctx, DCTAE_EINVAL, "packed outputs positions/channels/image_ids/key_pad are required");
     if ((want_codes || out->patches_dev) && !norm) return fail(ctx, DCTAE_EINVAL, "codes/patches need PatchNorm tables");
-    if (want_codes && (rc = check_lfq(ctx, lfq, PP))) return rc;
+    if (want_codes && !proj_w && (rc = check_lfq(ctx, lfq, PP))) return rc;
+    if (proj_w && (!want_codes || !lfq || lfq->codebook_dim < 1 || lfq->codebook_dim > 16 ||
+                   lfq->num_codebooks < 1 || lfq->num_codebooks > 64 || PP % 4 != 0 ||
+                   lfq->codebook_dim * lfq->num_codebooks > 256 || ((uintptr_t)proj_w & 15)))
+      return fail(ctx, DCTAE_EUNSUP, "fused LFQ projections: codes output, codebook_dim <= 16, ncb * cd <= 256, "
+                                     "P*P % 4 == 0, 16-byte aligned weights");
     if (pack->n_rows < 0 || (n > 0 && (!pack->row || !pack->col || !pack->k || !pack->local_id)) ||
         (pack->n_rows > 0 && !pack->row_len))
       return fail(ctx, DCTAE_EINVAL, "bad packing descriptor");
@@ -1128,7 +1134,10 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   if (norm && (!norm->median_dev || !norm->b_dev)) return fail(ctx, DCTAE_EINVAL, "PatchNorm tables are NULL");
   const int ncb = want_codes ? lfq->num_codebooks : 0;
   const bool want_raw = (full && out->raw_patches_dev) || (!full && tokens_dev);
-  const bool want_norm = full && out->patches_dev;
+  // LFQ with projections: the column epilogues stage the PatchNorm output,
+  // dctae_lfq_project_in turns the staged tokens into staged u16 codes, and the
+  // sort / pack gathers those as usual
+  const bool want_norm = full && (out->patches_dev || proj_w);
 
   // ---- plan cache key: every input that shapes the launch sequence
   std::vector<int64_t> key;
@@ -1167,12 +1176,14 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     ctx->enc_key = key;
   }
   EncPlan& E = *ctx->enc_plan;
+  if (proj_w && E.any_pad)
+    return fail(ctx, DCTAE_EUNSUP, "fused LFQ projections need rows without padding (the pad token's codes)");
   order_after_previous(ctx, s);
   if ((rc = upload_plan(ctx, E.pb, s, E.id))) return rc;
   uint8_t* pd = ctx->plan_dev;
   const FftPlan* plans_d = (const FftPlan*)(pd + E.plans_off);
 
-  EncParams ep = enc_params(cfg, norm, want_codes ? lfq : nullptr);
+  EncParams ep = enc_params(cfg, norm, want_codes && !proj_w ? lfq : nullptr);
   if (norm && !want_norm) ep.thr = norm_thr(norm);
   PackSinks ps{};
   if (full) {
@@ -1216,6 +1227,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   }
   EncParams epj = ep;
   if (!full) epj.median = nullptr;
+  TokenSinks skc = sk;   // the column kernels' sinks (codes come from the projection kernel)
+  if (proj_w) skc.codes = nullptr;
   // row half / column half of a chunk job on a stream
   auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
     const int nj = j.i1 - j.i0;
@@ -1269,18 +1282,18 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       }
     if (j.any_gemm_cols || j.any_bs_cols) {
       Timer t(ctx, st, "tile_epilogue");
-      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, sk, st);
+      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, skc, st);
     }
     if (j.n_fc[0]) {
       Timer t(ctx, st, "fft_cols");
       launch_fft_cols(dd, plans_d, (const int4*)(pd + j.fc_off[0]), j.n_fc[0], j.lds_cols, ctx->ws, ctx->fft_tab,
-                      epj, sk, st);
+                      epj, skc, st);
     }
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fc[v]) {
         Timer t(ctx, st, "fft_cols");
         launch_fft_cols_spec(v, dd, (const int4*)(pd + j.fc_off[v]), j.n_fc[v], ctx->ws, ctx->fft_tab + j.tw_off_c[v],
-                             ctx->fft_tab + j.post_off_c[v], epj, sk, st,
+                             ctx->fft_tab + j.post_off_c[v], epj, skc, st,
                              v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr, v == 1 ? j.n_pc : 0, j.pc_qw);
       }
   };
@@ -1288,9 +1301,15 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     do_rows(j, s);
     do_cols(j, s);
   }
+  if (proj_w && E.n_tok > 0) {
+    Timer t(ctx, s, "lfq_project_in");
+    launch_lfq_project_in16(sk.norm, E.n_tok, PP, proj_w, proj_b, lfq->codebook_dim, lfq->num_codebooks, sk.codes, s);
+  }
   if (full && E.n_img > 0) {
     Timer t(ctx, s, "sort_pack");
-    launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), ep, sk, ps, s,
+    EncParams eps = ep;
+    if (proj_w) eps.ncb = lfq->num_codebooks;
+    launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), eps, sk, ps, s,
                      ctx->sort_kernel, E.max_T);
   }
   HIPCHK(ctx, hipGetLastError());
@@ -1304,6 +1323,17 @@ int dctae_encode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* im
   if (!pack) return fail(ctx, DCTAE_EINVAL, "packing descriptor is NULL");
   hipSetDevice(ctx->device);
   return encode_impl(ctx, cfg, imgs, pack, norm, lfq, out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int dctae_encode_lfq_proj(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                          const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
+                          const float* w_in_dev, const float* b_in_dev, const dctae_packed_out* out, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!pack) return fail(ctx, DCTAE_EINVAL, "packing descriptor is NULL");
+  if (!w_in_dev || !out || !out->codes_dev) return fail(ctx, DCTAE_EINVAL, "project_in weight and codes output required");
+  hipSetDevice(ctx->device);
+  return encode_impl(ctx, cfg, imgs, pack, norm, lfq, out, nullptr, nullptr, nullptr, (hipStream_t)stream, w_in_dev,
+                     b_in_dev);
 }
 
 int dctae_spectrum_tokens(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs, const int64_t* tok_off,
@@ -1623,9 +1653,10 @@ int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64
 }
 
 static int lfq_proj_check(dctae_ctx* ctx, const dctae_lfq* lfq, int64_t n, int32_t dim, const void* a,
-                          const float* w, const void* o) {
-  if (!lfq || lfq->codebook_dim < 1 || lfq->codebook_dim > 31 || lfq->num_codebooks < 1 || lfq->num_codebooks > 64)
-    return fail(ctx, DCTAE_EINVAL, "bad LFQ config (codebook_dim <= 31, num_codebooks <= 64)");
+                          const float* w, const void* o, int max_ncb) {
+  if (!lfq || lfq->codebook_dim < 1 || lfq->codebook_dim > 31 || lfq->num_codebooks < 1 ||
+      lfq->num_codebooks > max_ncb)
+    return fail(ctx, DCTAE_EINVAL, "bad LFQ config (codebook_dim <= 31, num_codebooks <= " + std::to_string(max_ncb) + ")");
   const int64_t cdims = (int64_t)lfq->codebook_dim * lfq->num_codebooks;
   if (dim < 4 || dim > 256 || dim % 4 != 0 || cdims > 256 || cdims % 4 != 0)
     return fail(ctx, DCTAE_EINVAL, "LFQ projections: dim and codebook_dim * num_codebooks must be multiples of 4 <= 256");
@@ -1637,7 +1668,7 @@ static int lfq_proj_check(dctae_ctx* ctx, const dctae_lfq* lfq, int64_t n, int32
 int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, int32_t dim,
                          const float* w, const float* b, int64_t* idx, void* stream) {
   if (!ctx) return DCTAE_EINVAL;
-  if (int rc = lfq_proj_check(ctx, lfq, n, dim, x, w, idx)) return rc;
+  if (int rc = lfq_proj_check(ctx, lfq, n, dim, x, w, idx, 64)) return rc;
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   Timer t(ctx, s, "lfq_project_in");
@@ -1649,7 +1680,7 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, i
 int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* idx, int64_t n, int32_t dim,
                           const float* w, const float* b, float* out, void* stream) {
   if (!ctx) return DCTAE_EINVAL;
-  if (int rc = lfq_proj_check(ctx, lfq, n, dim, idx, w, out)) return rc;
+  if (int rc = lfq_proj_check(ctx, lfq, n, dim, idx, w, out, 32)) return rc;
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   Timer t(ctx, s, "lfq_project_out");

@@ -13,8 +13,8 @@
 //    built straight into the LDS A tile; out = codes W_out^T + b_out.
 //
 // Tile: 64 tokens per 256-thread block (16 per wave), all N <= 256 outputs per
-// wave (NT tiles of 16: NT x 4 accumulators), K in chunks of 16 with the next
-// chunk's global loads in flight during the current chunk's MFMAs.  Lane
+// wave (NT tiles of 16: NT x 4 accumulators), K in chunks of 16 (double-buffered in LDS, one barrier per chunk) with the
+// next chunk's global loads in flight during the current chunk's MFMAs.  Lane
 // (r = l & 15, q = l >> 4) reads float4 k = 4q .. 4q + 3 of its A row (token)
 // and B row (output feature); MFMA step s pairs k = 4q + s on both sides, so
 // the 16 k of a chunk are covered once (the order of the f32 sum differs from
@@ -36,13 +36,14 @@ template <int NT, int MODE, int MT>
 __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ w,
                                                  const float* __restrict__ bias, int cd, int ncb, float scale,
-                                                 int64_t* __restrict__ idx_out, float* __restrict__ out) {
+                                                 int64_t* __restrict__ idx_out, float* __restrict__ out,
+                                                 uint16_t* __restrict__ idx16) {
   constexpr int kTok = 64 * MT;                    // tokens per block (MT 16-token tiles per wave)
   constexpr int NP = NT * 16;                      // padded output features
   constexpr int WV = (NP * 4 + 255) / 256;         // W float4 per thread and chunk
-  __shared__ __attribute__((aligned(16))) float Ws[NP * kLd];
-  __shared__ __attribute__((aligned(16))) float As[kTok * kLd];
-  __shared__ int32_t Ix[MODE == 1 ? kTok * 64 : 1];   // mode 1: the block's indices (ncb <= 64)
+  __shared__ __attribute__((aligned(16))) float Ws[2][NP * kLd];   // double-buffered K chunks
+  __shared__ __attribute__((aligned(16))) float As[2][kTok * kLd];
+  __shared__ int32_t Ix[MODE == 1 ? kTok * 32 : 1];   // mode 1: the block's indices (ncb <= 32)
   __shared__ uint32_t Msk[MODE == 0 ? 4 * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -95,30 +96,34 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  auto store = [&]() {
+  auto store = [&](int bf) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) *reinterpret_cast<float4*>(&As[(at + 64 * m) * kLd + 4 * aq]) = ra[m];
+    for (int m = 0; m < MT; ++m) *reinterpret_cast<float4*>(&As[bf][(at + 64 * m) * kLd + 4 * aq]) = ra[m];
 #pragma unroll
     for (int i = 0; i < WV; ++i) {
       const int e = tid + 256 * i;
-      if (e < NP * 4) *reinterpret_cast<float4*>(&Ws[(e >> 2) * kLd + 4 * (e & 3)]) = rw[i];
+      if (e < NP * 4) *reinterpret_cast<float4*>(&Ws[bf][(e >> 2) * kLd + 4 * (e & 3)]) = rw[i];
     }
   };
 
   // wave w owns tokens [16 (w + 4 m), + 16) of the block for m < MT
+  // one barrier per chunk: chunk c is read from buffer c & 1 while chunk c + 1
+  // is written to the other one (whose last readers, chunk c - 1, all passed
+  // the previous barrier)
   load(0);
-  store();
+  store(0);
   __syncthreads();
-  for (int k0 = 0; k0 < K; k0 += kKc) {
+  int bf = 0;
+  for (int k0 = 0; k0 < K; k0 += kKc, bf ^= 1) {
     const bool more = k0 + kKc < K;
     if (more) load(k0 + kKc);
     float4 a4[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
-      a4[m] = *reinterpret_cast<const float4*>(&As[((wave + 4 * m) * kTokW + r) * kLd + 4 * q]);
+      a4[m] = *reinterpret_cast<const float4*>(&As[bf][((wave + 4 * m) * kTokW + r) * kLd + 4 * q]);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const float4 b4 = *reinterpret_cast<const float4*>(&Ws[(t * 16 + r) * kLd + 4 * q]);
+      const float4 b4 = *reinterpret_cast<const float4*>(&Ws[bf][(t * 16 + r) * kLd + 4 * q]);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].x, b4.x, acc[m][t], 0, 0, 0);
@@ -127,11 +132,8 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
         acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].w, b4.w, acc[m][t], 0, 0, 0);
       }
     }
+    if (more) store(bf ^ 1);
     __syncthreads();
-    if (more) {
-      store();
-      __syncthreads();
-    }
   }
 
   // C/D map: lane l, register v -> token 4 (l >> 4) + v of the M tile, feature 16 t + (l & 15)
@@ -164,7 +166,11 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
         const uint64_t win = (uint64_t)mi[pc] | ((uint64_t)mi[pc + 1] << 16) | ((uint64_t)mi[pc + 2] << 32) |
                              ((uint64_t)mi[pc + 3] << 48);
         const uint32_t bits = (uint32_t)(win >> sh) & ((1u << cd) - 1u);   // bit b = feature o0 + b
-        idx_out[wt0 * ncb + p] = (int64_t)(__builtin_bitreverse32(bits) >> (32 - cd));
+        const uint32_t code = __builtin_bitreverse32(bits) >> (32 - cd);
+        if (idx16)
+          idx16[wt0 * ncb + p] = (uint16_t)code;   // encode staging (cd <= 16), gathered by k_sort_pack2
+        else
+          idx_out[wt0 * ncb + p] = (int64_t)code;
       }
     } else {
 #pragma unroll
@@ -184,9 +190,10 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
 
 template <int MODE, int MT>
 void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
-               const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out) {
+               const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
+               uint16_t* idx16) {
 #define DCTAE_LFQP(T) \
-  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, MT>), g, dim3(256), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out); break;
+  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, MT>), g, dim3(256), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16); break;
   switch (nt) {
     DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
     DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
@@ -200,11 +207,12 @@ void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx
 
 template <int MODE>
 static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
-                        const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out) {
+                        const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
+                        uint16_t* idx16 = nullptr) {
   // MT = 1: 16 tokens per wave (106 VGPRs + 52 AGPRs at NT = 13, 3 waves / SIMD).
   // MT = 2 (32 tokens per wave, half the W LDS reads per MFMA) measured slower:
   // 1 wave / SIMD, project_in 3.91 vs 2.83 ms, project_out 5.37 vs 3.29 ms
-  launch_nt<MODE, 1>(nt, dim3((unsigned)((n + 63) / 64)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out);
+  launch_nt<MODE, 1>(nt, dim3((unsigned)((n + 63) / 64)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16);
 }
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
@@ -212,6 +220,13 @@ void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, con
                            int64_t* idx, hipStream_t s) {
   if (n <= 0) return;
   launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, idx, nullptr);
+}
+
+// the same into the encode's u16 token staging (cd <= 16)
+void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
+                             uint16_t* idx, hipStream_t s) {
+  if (n <= 0) return;
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, nullptr, nullptr, idx);
 }
 
 // indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)

@@ -518,14 +518,17 @@ class BatchEncoder:
         self.k = k
         self.n_rows = self.plan.n_rows
         self.S = fe.max_seq_len
-        # LFQ with projections (lfq.py:54-62): the fused launch stops at the
-        # PatchNorm output and dctae_lfq_project_in (project_in + sign + pack)
-        # writes the codes on the same stream
+        # LFQ with projections (lfq.py:54-62): with every packed row full,
+        # dctae_encode_lfq_proj runs project_in + sign + pack on the staged
+        # PatchNorm output before the sort / pack; otherwise the fused launch
+        # stops at the packed PatchNorm output and dctae_lfq_project_in follows
         self.lfq = lfq
         self.proj = lfq.has_projections
         if self.proj and not lfq._fused_proj():
             raise NotImplementedError("BatchEncoder: LFQ projections of this shape run through encode_batch")
-        want_norm = want_patches or self.proj
+        self.proj_staged = (self.proj and all(n == fe.max_seq_len for n in self.plan.row_len)
+                            and lfq.codebook_dim <= 16 and (fe.patch_size ** 2) % 4 == 0)
+        want_norm = want_patches or (self.proj and not self.proj_staged)
         self.norm = patchnorm.state(thresholds=not want_norm)
         self.lcfg = lfq.cfg()
         self.p = fe.params()
@@ -545,7 +548,7 @@ class BatchEncoder:
         if want_norm:
             self.out["patches"] = torch.empty((R, S, fe.patch_size ** 2), dtype=torch.float32, device=self.dev)
         o = self.out
-        self.po = PackedOut(ptr(None if self.proj else o["codes"]), ptr(o["positions"]), ptr(o["channels"]), ptr(o["image_ids"]),
+        self.po = PackedOut(ptr(None if self.proj and not self.proj_staged else o["codes"]), ptr(o["positions"]), ptr(o["channels"]), ptr(o["image_ids"]),
                             ptr(o["key_pad_mask"]), ptr(o.get("patches")), None, None)
         self._ncfg = self.norm.c()
         self._cfg = self.p.c(S)
@@ -554,11 +557,18 @@ class BatchEncoder:
 
     def __call__(self, x: torch.Tensor):
         import ctypes as C
-        from ._lib import Images, stream_ptr
+        from ._lib import Images, ptr, stream_ptr
         assert x.shape == (self.B, 3, self.H, self.W) and x.dtype == torch.float32 and x.is_contiguous()
         assert x.device == self.dev
         imgs = Images(C.c_void_p(x.data_ptr()), C.cast(self._keep[0], C.POINTER(C.c_int64)),
                       C.cast(self._keep[1], C.POINTER(C.c_int32)), self.B)
+        if self.proj_staged:
+            w, b = self.lfq._proj_w(self.lfq.project_in, self.dev)
+            rc = self.ctx.lib.dctae_encode_lfq_proj(self.ctx.h, C.byref(self._cfg), C.byref(imgs),
+                                                    C.byref(self.packing), C.byref(self._ncfg), C.byref(self.lcfg),
+                                                    ptr(w), ptr(b), C.byref(self.po), stream_ptr(self.dev))
+            self.ctx.check(rc, "dctae_encode_lfq_proj")
+            return self.out
         rc = self.ctx.lib.dctae_encode(self.ctx.h, C.byref(self._cfg), C.byref(imgs), C.byref(self.packing),
                                        C.byref(self._ncfg), None if self.proj else C.byref(self.lcfg),
                                        C.byref(self.po), stream_ptr(self.dev))

@@ -65,7 +65,7 @@ class LFQ(nn.Module):
     def _fused_proj(self) -> bool:
         cdims = self.codebook_dim * self.num_codebooks
         return (self.has_projections and self.dim % 4 == 0 and 4 <= self.dim <= 256 and cdims % 4 == 0
-                and cdims <= 256 and self.codebook_dim <= 31 and self.num_codebooks <= 64)
+                and cdims <= 256 and self.codebook_dim <= 31 and self.num_codebooks <= 32)
 
     def _proj_w(self, lin: nn.Linear, dev):
         """fp32 contiguous copies of a projection's weight / bias on ``dev``

@@ -208,6 +208,17 @@ int dctae_lfq_forward(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, 
 int dctae_lfq_indices_to_codes(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev,
                                int64_t n, float* codes_dev, void* stream);
 
+/* dctae_encode for an LFQ with projections (lfq.py:54-62; conf/patch14-l.json:
+ * 196 -> 16 x 13): the column epilogues stage the PatchNorm output, the fused
+ * project_in + sign + pack kernel (below) turns the staged tokens into staged
+ * codes, and the sort / pack writes them like dctae_encode's.  w_in (ncb*cd,
+ * P*P) / b_in (ncb*cd, nullable) fp32 as nn.Linear stores them.  codebook_dim
+ * <= 16, ncb*cd <= 256; rows without padding (every packed row full, e.g. the
+ * fixed-geometry BatchEncoder), else DCTAE_EUNSUP. */
+int dctae_encode_lfq_proj(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_images* imgs,
+                          const dctae_packing* pack, const dctae_norm* norm, const dctae_lfq* lfq,
+                          const float* w_in_dev, const float* b_in_dev, const dctae_packed_out* out, void* stream);
+
 /* LFQ with projections (lfq.py:54-62, dim != codebook_dim * num_codebooks),
  * encode direction: LFQ.forward's indices (lfq.py:164 project_in, :175-187
  * sign + packing) in one fused MFMA kernel: x (n, dim) fp32, w_in (ncb*cd,
@@ -219,7 +230,7 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_de
 /* Decode direction: LFQ.indices_to_codes with project_out (lfq.py:105-127):
  * indices (n, ncb) -> +-scale codes -> out (n, dim) = codes w_out^T + b_out,
  * w_out (dim, ncb*cd), b_out (dim, nullable).  dim <= 256, ncb*cd % 4 == 0,
- * ncb <= 64, cd <= 31. */
+ * ncb <= 32, cd <= 31. */
 int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev, int64_t n, int32_t dim,
                           const float* w_out_dev, const float* b_out_dev, float* out_dev, void* stream);
 

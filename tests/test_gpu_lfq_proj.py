@@ -105,11 +105,15 @@ def test_batch_encoder_with_projections(pkg, fe, pn, lfq_p, B, H):
     from importlib import import_module
     fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
     enc = fe_mod.BatchEncoder(fe, B, H, H, pn, lfq_p, device=DEV)
+    # 512^2 rows are full (3072 tokens): dctae_encode_lfq_proj (projection on the
+    # staged tokens before the sort / pack); 224^2 rows hold pads: the packed path
+    assert enc.proj_staged == (H == 512)
     imgs = _images(79, [(H, H)] * B)
     out = enc(torch.stack(imgs).contiguous())
-    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p)
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p, return_patches=True)
     assert torch.equal(out["codes"], codes) and torch.equal(out["key_pad_mask"], dp.key_pad_mask)
     assert torch.equal(out["positions"], dp.patch_positions)
+    assert torch.equal(out["image_ids"], dp.batched_image_ids)
 
 
 @pytest.mark.parametrize("dim,cd,ncb,n,bias", [(196, 13, 16, 3072 * 3 + 5, True), (196, 13, 16, 1, True),
