@@ -12,7 +12,7 @@
 //    codes = +-scale from the index bits (bits * 2 scale - scale, lfq.py:117-124),
 //    built straight into the LDS A tile; out = codes W_out^T + b_out.
 //
-// Tile: 64 tokens per 256-thread block (16 per wave), all N <= 256 outputs per
+// Tile: 128 tokens per 512-thread block (16 per wave), all N <= 256 outputs per
 // wave (NT tiles of 16: NT x 4 accumulators), K in chunks of 16 (double-buffered in LDS, one barrier per chunk) with the
 // next chunk's global loads in flight during the current chunk's MFMAs.  Lane
 // (r = l & 15, q = l >> 4) reads float4 k = 4q .. 4q + 3 of its A row (token)
@@ -32,19 +32,21 @@ constexpr int kTokW = 16;    // tokens per wave and M tile
 constexpr int kKc = 16;      // k chunk
 constexpr int kLd = kKc + 4; // LDS row stride (floats)
 
-template <int NT, int MODE, int MT>
-__global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
+template <int NT, int MODE, int WB>
+__global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ w,
                                                  const float* __restrict__ bias, int cd, int ncb, float scale,
                                                  int64_t* __restrict__ idx_out, float* __restrict__ out,
                                                  uint16_t* __restrict__ idx16) {
-  constexpr int kTok = 64 * MT;                    // tokens per block (MT 16-token tiles per wave)
+  constexpr int MT = 1;                            // 16-token M tiles per wave (2 measured slower, see launch_mode)
+  constexpr int kThr = 64 * WB;                    // WB waves per block
+  constexpr int kTok = kTokW * WB * MT;            // tokens per block
   constexpr int NP = NT * 16;                      // padded output features
-  constexpr int WV = (NP * 4 + 255) / 256;         // W float4 per thread and chunk
+  constexpr int WV = (NP * 4 + kThr - 1) / kThr;   // W float4 per thread and chunk
   __shared__ __attribute__((aligned(16))) float Ws[2][NP * kLd];   // double-buffered K chunks
   __shared__ __attribute__((aligned(16))) float As[2][kTok * kLd];
   __shared__ int32_t Ix[MODE == 1 ? kTok * 32 : 1];   // mode 1: the block's indices (ncb <= 32)
-  __shared__ uint32_t Msk[MODE == 0 ? 4 * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
+  __shared__ uint32_t Msk[MODE == 0 ? WB * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
@@ -52,7 +54,7 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
   const int nt = n - tok0 < kTok ? (int)(n - tok0) : kTok;
 
   if (MODE == 1) {
-    for (int e = tid; e < kTok * ncb; e += 256) {
+    for (int e = tid; e < kTok * ncb; e += kThr) {
       const int t = e / ncb;
       Ix[e] = t < nt ? (int32_t)idx_in[tok0 * ncb + e] : 0;   // lfq.py:117 indices.int()
     }
@@ -72,7 +74,7 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     const int k = k0 + 4 * aq;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int tk = at + 64 * m;
+      const int tk = at + kTokW * WB * m;
       if (MODE == 0) {
         ra[m] = (tk < nt && k < K) ? *reinterpret_cast<const float4*>(x + (tok0 + tk) * K + k)
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     }
 #pragma unroll
     for (int i = 0; i < WV; ++i) {
-      const int e = tid + 256 * i;
+      const int e = tid + kThr * i;
       const int row = e >> 2, kk = k0 + 4 * (e & 3);
       rw[i] = (row < N && kk < K) ? *reinterpret_cast<const float4*>(w + (int64_t)row * K + kk)
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -98,10 +100,10 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
   };
   auto store = [&](int bf) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) *reinterpret_cast<float4*>(&As[bf][(at + 64 * m) * kLd + 4 * aq]) = ra[m];
+    for (int m = 0; m < MT; ++m) *reinterpret_cast<float4*>(&As[bf][(at + kTokW * WB * m) * kLd + 4 * aq]) = ra[m];
 #pragma unroll
     for (int i = 0; i < WV; ++i) {
-      const int e = tid + 256 * i;
+      const int e = tid + kThr * i;
       if (e < NP * 4) *reinterpret_cast<float4*>(&Ws[bf][(e >> 2) * kLd + 4 * (e & 3)]) = rw[i];
     }
   };
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
     float4 a4[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
-      a4[m] = *reinterpret_cast<const float4*>(&As[bf][((wave + 4 * m) * kTokW + r) * kLd + 4 * q]);
+      a4[m] = *reinterpret_cast<const float4*>(&As[bf][((wave + WB * m) * kTokW + r) * kLd + 4 * q]);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const float4 b4 = *reinterpret_cast<const float4*>(&Ws[bf][(t * 16 + r) * kLd + 4 * q]);
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
   // C/D map: lane l, register v -> token 4 (l >> 4) + v of the M tile, feature 16 t + (l & 15)
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int64_t wt0 = tok0 + (wave + 4 * m) * kTokW;   // first token of this M tile
+    const int64_t wt0 = tok0 + (wave + WB * m) * kTokW;   // first token of this M tile
     if (MODE == 0) {
       uint32_t* msk = Msk + (wave * MT + m) * 16 * (NT + 3);
 #pragma unroll
@@ -188,12 +190,12 @@ __global__ __launch_bounds__(256) void k_lfq_proj(const float* __restrict__ x, c
   }
 }
 
-template <int MODE, int MT>
+template <int MODE, int WB>
 void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
                uint16_t* idx16) {
 #define DCTAE_LFQP(T) \
-  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, MT>), g, dim3(256), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16); break;
+  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16); break;
   switch (nt) {
     DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
     DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
@@ -209,10 +211,13 @@ template <int MODE>
 static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                         const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
                         uint16_t* idx16 = nullptr) {
-  // MT = 1: 16 tokens per wave (106 VGPRs + 52 AGPRs at NT = 13, 3 waves / SIMD).
-  // MT = 2 (32 tokens per wave, half the W LDS reads per MFMA) measured slower:
-  // 1 wave / SIMD, project_in 3.91 vs 2.83 ms, project_out 5.37 vs 3.29 ms
-  launch_nt<MODE, 1>(nt, dim3((unsigned)((n + 63) / 64)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16);
+  // 8 waves x 16 tokens per block (the W chunk in LDS shared by 128 tokens; 2
+  // blocks / CU by LDS, 4 waves / SIMD).  Measured on 3,145,728 tokens (196 ->
+  // 208): project_in 2.45 ms / project_out 2.80 ms; 4 waves per block 2.73 /
+  // 3.05; 16 waves 2.51 / 3.23; MT = 2 (32 tokens per wave, half the W LDS
+  // reads per MFMA) at 4 waves: 1 wave / SIMD, 3.91 / 5.37
+  launch_nt<MODE, 8>(nt, dim3((unsigned)((n + 127) / 128)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out,
+                     idx16);
 }
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
