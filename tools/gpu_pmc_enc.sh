@@ -4,9 +4,11 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc_enc
+OUT=${PMC_OUT:-gpurun_out/pmc_enc}
 rm -rf $OUT; mkdir -p $OUT
-BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-stats --no-model --no-configs --no-decode ${BENCH_ARGS:-}"
+# DECODE=1: the config-3 decode leg runs too (its kernels land in the same passes)
+DEC="--no-decode"; [ -n "${DECODE:-}" ] && DEC=""
+BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-stats --no-model --no-configs $DEC ${BENCH_ARGS:-}"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
