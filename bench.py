@@ -222,7 +222,21 @@ def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
                                           "project_in 196 -> 208 fused with sign / packing)",
                               "ms_per_step": round(el * 1e3, 4), "value": round(1024 * 512 * 512 / el / 1e6, 1),
                               "unit": "Mpix/s", "kernels": kernel_times(lib.context(dev), lambda: encp(x3), 5)}
-    del x3, encp
+    # and its decode: codes -> project_out (fused) -> inverse PatchNorm -> decode from tokens
+    packed = encp(x3)
+    decp = fe_mod.BatchDecoder(encp, pn, lfq_p)
+    decp(packed)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        decp(packed)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / steps
+    out["lfq_projections"]["decode"] = {
+        "workload": "decode of those codes: codes -> project_out -> inverse PatchNorm in one kernel, IDCT -> RGB",
+        "ms_per_step": round(el * 1e3, 4), "value": round(1024 * 512 * 512 / el / 1e6, 1), "unit": "Mpix/s",
+        "kernels": kernel_times(lib.context(dev), lambda: decp(packed), 5)}
+    del x3, encp, decp, packed
     return out
 
 

@@ -330,6 +330,32 @@ def lfq_project_out(idx: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor
     return out
 
 
+def lfq_project_out_inverse_norm(idx: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], cfg: LFQCfg,
+                                 norm: NormState, p: FEParams, channels: torch.Tensor,
+                                 positions: torch.Tensor) -> torch.Tensor:
+    """LFQ.indices_to_codes (project_out) + PatchNorm.inverse_norm in one kernel
+    (dctae_lfq_project_out_inverse_norm): idx (..., ncb) -> (..., P*P) fp32."""
+    dev = _check_dev(idx, w, b, channels, positions, norm.median, norm.b)
+    ctx = _lib.context(dev)
+    ii = idx.long().contiguous()
+    if ii.shape[-1] != cfg.num_codebooks:
+        raise AssertionError("last dim of indices must be num_codebooks")
+    dim = w.shape[0]
+    if dim != p.patch_size ** 2:
+        raise AssertionError(f"project_out dim {dim} != patch_size**2")
+    n = ii.numel() // cfg.num_codebooks
+    ch = channels.long().contiguous()
+    pos = positions.long().contiguous()
+    if ch.numel() != n or pos.numel() != 2 * n:
+        raise AssertionError("channels/positions do not match the indices")
+    out = torch.empty((*ii.shape[:-1], dim), dtype=torch.float32, device=dev)
+    rc = ctx.lib.dctae_lfq_project_out_inverse_norm(ctx.h, C.byref(cfg), ptr(ii), n, dim, ptr(w), ptr(b),
+                                                    C.byref(norm.c()), p.max_patch_h, p.max_patch_w, ptr(ch),
+                                                    ptr(pos), ptr(out), _lib.stream_ptr(dev))
+    ctx.check(rc, "dctae_lfq_project_out_inverse_norm")
+    return out
+
+
 def vq_forward(cfg: VQCfg, x: torch.Tensor, mask: Optional[torch.Tensor], want_quantized=True):
     """x (n, dim) fp32 contiguous on the device; mask (n) bool or None.
     Returns quantize (n, dim) (None unless wanted) and indices (n, heads)."""

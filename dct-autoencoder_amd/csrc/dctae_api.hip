@@ -1689,6 +1689,25 @@ int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* i
   return 0;
 }
 
+int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* idx, int64_t n,
+                                       int32_t dim, const float* w, const float* b, const dctae_norm* norm,
+                                       int32_t max_patch_h, int32_t max_patch_w, const int64_t* channels,
+                                       const int64_t* positions, float* out, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (int rc = lfq_proj_check(ctx, lfq, n, dim, idx, w, out, 32)) return rc;
+  if (!norm || !norm->median_dev || !norm->b_dev || max_patch_h < 1 || max_patch_w < 1 ||
+      (n > 0 && (!channels || !positions)))
+    return fail(ctx, DCTAE_EINVAL, "inverse PatchNorm needs tables, max_patch_h/w and channels / positions");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  Timer t(ctx, s, "lfq_project_out");
+  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out, s,
+                         channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h, max_patch_w,
+                         ctx->err_dev);
+  HIPCHK(ctx, hipGetLastError());
+  return 0;
+}
+
 // ---- VectorQuantize inference (dctae_vq.hip) --------------------------------
 static int vq_check(dctae_ctx* ctx, const dctae_vq* vq) {
   if (!vq || vq->codebook_dim != 16 || vq->heads < 1 || vq->codebook_size < 1 || vq->dim < 1 || !vq->embed_dev)

@@ -37,7 +37,9 @@ void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, con
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                              uint16_t* idx, hipStream_t s);
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                            float scale, float* out, hipStream_t s);
+                            float scale, float* out, hipStream_t s, const int64_t* ch = nullptr,
+                            const int64_t* pos = nullptr, const float* med = nullptr, const float* nb = nullptr,
+                            float eps = 0.f, int maxph = 0, int maxpw = 0, int* err = nullptr);
 // VectorQuantize inference (dctae_vq.hip)
 void launch_vq_bias(float* y, const float* bias, int64_t n, int cols, const uint8_t* mask, const float* orig,
                     hipStream_t s);

@@ -28,6 +28,18 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// optional inverse PatchNorm fused into mode 1's epilogue (patchnorm.py:167-177:
+// y * (b sqrt 2 + eps) + median at the token's (channel, h, w) table row)
+struct InvNorm {
+  const int64_t* ch;    // (n) channels of the tokens, or null: no inverse
+  const int64_t* pos;   // (n, 2)
+  const float* med;     // (3, maxph, maxpw, D)
+  const float* b;
+  float eps;
+  int maxph, maxpw;
+  int* err;             // bit 1: a table index out of range (the reference raises IndexError)
+};
+
 constexpr int kTokW = 16;    // tokens per wave and M tile
 constexpr int kKc = 16;      // k chunk
 constexpr int kLd = kKc + 4; // LDS row stride (floats)
@@ -37,7 +49,7 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
                                                  int64_t n, int K, int N, const float* __restrict__ w,
                                                  const float* __restrict__ bias, int cd, int ncb, float scale,
                                                  int64_t* __restrict__ idx_out, float* __restrict__ out,
-                                                 uint16_t* __restrict__ idx16) {
+                                                 uint16_t* __restrict__ idx16, InvNorm inv) {
   constexpr int MT = 1;                            // 16-token M tiles per wave (2 measured slower, see launch_mode)
   constexpr int kThr = 64 * WB;                    // WB waves per block
   constexpr int kTok = kTokW * WB * MT;            // tokens per block
@@ -175,6 +187,18 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
           idx_out[wt0 * ncb + p] = (int64_t)code;
       }
     } else {
+      int64_t tab[4];   // inverse PatchNorm table row of the lane's 4 tokens (-1: out of range)
+      if (inv.ch) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int64_t row = wt0 + 4 * q + v;
+          const int64_t rr = row < n ? row : 0;
+          const int64_t c = inv.ch[rr], h = inv.pos[2 * rr], w = inv.pos[2 * rr + 1];
+          const bool ok = c >= 0 && c < 3 && h >= 0 && h < inv.maxph && w >= 0 && w < inv.maxpw;
+          if (!ok && row < n && r == 0) atomicOr(inv.err, 1);
+          tab[v] = ok ? ((c * inv.maxph + h) * inv.maxpw + w) * N : -1;
+        }
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int col = 16 * t + r;
@@ -183,7 +207,12 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int64_t row = wt0 + 4 * q + v;
-          if (row < n) out[row * N + col] = acc[m][t][v] + bb;
+          if (row >= n) continue;
+          float y = acc[m][t][v] + bb;
+          if (inv.ch)
+            y = tab[v] >= 0 ? pn_inverse(y, inv.med[tab[v] + col], inv.b[tab[v] + col], inv.eps)
+                            : __int_as_float(0x7fc00000);
+          out[row * N + col] = y;
         }
       }
     }
@@ -193,9 +222,9 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
 template <int MODE, int WB>
 void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-               uint16_t* idx16) {
+               uint16_t* idx16, InvNorm inv) {
 #define DCTAE_LFQP(T) \
-  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16); break;
+  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv); break;
   switch (nt) {
     DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
     DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
@@ -210,14 +239,14 @@ void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx
 template <int MODE>
 static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                         const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-                        uint16_t* idx16 = nullptr) {
+                        uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}) {
   // 8 waves x 16 tokens per block (the W chunk in LDS shared by 128 tokens; 2
   // blocks / CU by LDS, 4 waves / SIMD).  Measured on 3,145,728 tokens (196 ->
   // 208): project_in 2.45 ms / project_out 2.80 ms; 4 waves per block 2.73 /
   // 3.05; 16 waves 2.51 / 3.23; MT = 2 (32 tokens per wave, half the W LDS
   // reads per MFMA) at 4 waves: 1 wave / SIMD, 3.91 / 5.37
   launch_nt<MODE, 8>(nt, dim3((unsigned)((n + 127) / 128)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out,
-                     idx16);
+                     idx16, inv);
 }
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
@@ -236,9 +265,11 @@ void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, c
 
 // indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                            float scale, float* out, hipStream_t s) {
+                            float scale, float* out, hipStream_t s, const int64_t* ch, const int64_t* pos,
+                            const float* med, const float* nb, float eps, int maxph, int maxpw, int* err) {
   if (n <= 0) return;
-  launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out);
+  launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out, nullptr,
+                 InvNorm{ch, pos, med, nb, eps, maxph, maxpw, err});
 }
 
 }  // namespace dctae

@@ -485,8 +485,13 @@ class DCTAutoencoderFeatureExtractor:
         inverse PatchNorm first, and the fused decode starts from the tokens."""
         if lfq.has_projections:
             dp = dct_patches.shallow_copy()
-            dp.patches = lfq.indices_to_codes(codes)
-            dp.patches = patchnorm.inverse_norm(dp)
+            if lfq._fused_proj() and lfq.dim == self.patch_size ** 2:
+                w, b = lfq._proj_w(lfq.project_out, codes.device)
+                dp.patches = _ops.lfq_project_out_inverse_norm(codes, w, b, lfq.cfg(), patchnorm.state(thresholds=False),
+                                                               self.params(), dp.patch_channels, dp.patch_positions)
+            else:
+                dp.patches = lfq.indices_to_codes(codes)
+                dp.patches = patchnorm.inverse_norm(dp)
             return self.postprocess(dp)
         return _ops.decode(self.params(dct_patches.key_pad_mask.shape[1]), dct_patches.batched_image_ids,
                            dct_patches.key_pad_mask, dct_patches.patch_positions, dct_patches.patch_channels,
@@ -606,6 +611,11 @@ class BatchDecoder:
         self.norm = patchnorm.state(thresholds=False)
         self._ncfg = self.norm.c()
         self.lcfg = lfq.cfg()
+        self.lfq, self.patchnorm = lfq, patchnorm
+        # LFQ with projections (lfq.py:54-62): codes -> project_out (fused MFMA
+        # kernel, dctae_lfq_project_out) -> inverse PatchNorm (dctae_norm_inverse)
+        # -> the fused decode from tokens
+        self.proj = lfq.has_projections
         self.out = torch.empty((enc.B, 3, H, W), dtype=torch.float32, device=enc.dev)
 
     def __call__(self, packed) -> torch.Tensor:
@@ -613,6 +623,22 @@ class BatchDecoder:
         import ctypes as C
         e = self.enc
         lut, hw, offs, phw = self._ptr
+        if self.proj:
+            from . import _ops
+            if self.lfq._fused_proj():
+                w, b = self.lfq._proj_w(self.lfq.project_out, e.dev)
+                x = _ops.lfq_project_out_inverse_norm(packed["codes"], w, b, self.lcfg, self.norm, e.fe.params(),
+                                                      packed["channels"], packed["positions"])
+            else:
+                x = self.lfq.indices_to_codes(packed["codes"]).float()
+                x = _ops.norm_apply(x, packed["channels"], packed["positions"], self.norm, e.fe.params(),
+                                    inverse=True)
+            rc = e.ctx.lib.dctae_decode(e.ctx.h, C.byref(e._cfg), e.n_rows, lut, self.lut_w, e.B, hw, offs, phw,
+                                        ptr(packed["image_ids"]), ptr(packed["key_pad_mask"]),
+                                        ptr(packed["positions"]), ptr(packed["channels"]), None, None, None, ptr(x),
+                                        ptr(self.out), stream_ptr(e.dev))
+            e.ctx.check(rc, "dctae_decode")
+            return self.out
         rc = e.ctx.lib.dctae_decode(e.ctx.h, C.byref(e._cfg), e.n_rows, lut, self.lut_w, e.B, hw, offs, phw,
                                     ptr(packed["image_ids"]), ptr(packed["key_pad_mask"]), ptr(packed["positions"]),
                                     ptr(packed["channels"]), C.byref(self._ncfg), C.byref(self.lcfg),

@@ -234,6 +234,17 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_de
 int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev, int64_t n, int32_t dim,
                           const float* w_out_dev, const float* b_out_dev, float* out_dev, void* stream);
 
+/* The same with PatchNorm.inverse_norm (patchnorm.py:167-177) fused into the
+ * epilogue: out = inverse_norm(codes w_out^T + b_out) at each token's
+ * (channel, h, w) table row; dim = P*P.  Out-of-range table indices write NaN
+ * and set the device error flag (dctae_check_device_errors), like
+ * dctae_norm_inverse. */
+int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* indices_dev, int64_t n,
+                                       int32_t dim, const float* w_out_dev, const float* b_out_dev,
+                                       const dctae_norm* norm, int32_t max_patch_h, int32_t max_patch_w,
+                                       const int64_t* channels_dev, const int64_t* positions_dev, float* out_dev,
+                                       void* stream);
+
 /* VectorQuantize (vector_quantize.py:675-1050) as the model builds it
  * (modeling_dct_autoencoder.py:76-77): euclidean codebook shared by the
  * heads, codebook_dim 16, kmeans-initialised, affine codebook parameters,

@@ -160,3 +160,42 @@ def test_project_kernels_vs_linear(pkg, dim, cd, ncb, n, bias):
     q, i2, _, _ = m(x.to(DEV), mask=torch.ones(n, dtype=torch.bool, device=DEV))
     assert torch.equal(i2.cpu(), idx)
     assert torch.equal(q.cpu(), m.indices_to_codes(idx.to(DEV)).cpu())
+
+
+def test_batch_decoder_with_projections(pkg, fe, pn, lfq_p):
+    """BatchDecoder with projections (fused project_out -> inverse PatchNorm ->
+    decode from tokens) equals decode_batch on the same codes (same kernels)."""
+    from importlib import import_module
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    enc = fe_mod.BatchEncoder(fe, 2, 512, 512, pn, lfq_p, device=DEV)
+    imgs = _images(80, [(512, 512)] * 2)
+    out = enc(torch.stack(imgs).contiguous())
+    got = fe_mod.BatchDecoder(enc, pn, lfq_p)(out)
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p)
+    ref = fe.decode_batch(dp, codes, pn, lfq_p)
+    assert got.shape == (2, 3, 512, 512)
+    for i in range(2):
+        assert torch.equal(got[i], ref[i]), float((got[i] - ref[i]).abs().max())
+
+
+def test_project_out_inverse_norm_fused(pkg, fe, pn, lfq_p):
+    """dctae_lfq_project_out_inverse_norm == project_out kernel then the
+    dctae_norm_inverse kernel, bit for bit (same fp32 ops, no FMA)."""
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    imgs = _images(81, [(224, 224), (300, 500)])
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p)
+    w, b = lfq_p._proj_w(lfq_p.project_out, codes.device)
+    fused = ops.lfq_project_out_inverse_norm(codes, w, b, lfq_p.cfg(), pn.state(thresholds=False), fe.params(),
+                                             dp.patch_channels, dp.patch_positions)
+    d2 = dp.shallow_copy()
+    d2.patches = lfq_p.indices_to_codes(codes)
+    two = pn.inverse_norm(d2)
+    assert torch.equal(fused, two)
+    bad = dp.patch_positions.clone()
+    bad[0, 0, 0] = 99                                   # out-of-range table row: NaN + device error flag
+    out = ops.lfq_project_out_inverse_norm(codes, w, b, lfq_p.cfg(), pn.state(thresholds=False), fe.params(),
+                                           dp.patch_channels, bad)
+    assert torch.isnan(out[0, 0]).all() and torch.equal(out[0, 1:], fused[0, 1:])
+    with pytest.raises(Exception):
+        ops.check_device_errors(codes.device)
