@@ -57,6 +57,7 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
   constexpr int WV = (NP * 4 + kThr - 1) / kThr;   // W float4 per thread and chunk
   __shared__ __attribute__((aligned(16))) float Ws[2][NP * kLd];   // double-buffered K chunks
   __shared__ __attribute__((aligned(16))) float As[2][kTok * kLd];
+  __shared__ int64_t Tb[MODE == 1 ? 32 : 1];   // mode 1 + inverse: table rows of a round's 32 tokens
   __shared__ int32_t Ix[MODE == 1 ? kTok * 32 : 1];   // mode 1: the block's indices (ncb <= 32)
   __shared__ uint32_t Msk[MODE == 0 ? WB * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
 
@@ -187,32 +188,69 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
           idx_out[wt0 * ncb + p] = (int64_t)code;
       }
     } else {
-      int64_t tab[4];   // inverse PatchNorm table row of the lane's 4 tokens (-1: out of range)
       if (inv.ch) {
+        // inverse PatchNorm: the output tiles go through the freed W buffers, 2
+        // waves per round, so the table gathers and the stores run as 16-byte
+        // pieces along each token's 196 contiguous floats (same fp32 ops as
+        // dctae_norm_inverse on the stored projection: bit-equal)
+        constexpr int WPR = 2;
+        float* stg = &Ws[0][0];   // 2 NP kLd floats >= WPR x 16 x N
+        const int N4 = N >> 2;
+        for (int rd = 0; rd < WB / WPR; ++rd) {
+          __syncthreads();   // the previous round's (or the K loop's) LDS reads are done
+          const int wl = wave - rd * WPR;
+          if (wl >= 0 && wl < WPR) {
+            float* tl = stg + wl * kTokW * N;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int64_t row = wt0 + 4 * q + v;
-          const int64_t rr = row < n ? row : 0;
-          const int64_t c = inv.ch[rr], h = inv.pos[2 * rr], w = inv.pos[2 * rr + 1];
-          const bool ok = c >= 0 && c < 3 && h >= 0 && h < inv.maxph && w >= 0 && w < inv.maxpw;
-          if (!ok && row < n && r == 0) atomicOr(inv.err, 1);
-          tab[v] = ok ? ((c * inv.maxph + h) * inv.maxpw + w) * N : -1;
+            for (int t = 0; t < NT; ++t) {
+              const int col = 16 * t + r;
+              if (col >= N) continue;
+              const float bb = bias ? bias[col] : 0.f;
+#pragma unroll
+              for (int v = 0; v < 4; ++v) tl[(4 * q + v) * N + col] = acc[m][t][v] + bb;
+            }
+          }
+          const int64_t rt0 = tok0 + (int64_t)rd * WPR * kTokW;   // first token of the round
+          if (tid < WPR * kTokW) {
+            const int64_t row = rt0 + tid;
+            int64_t tb = -2;   // -2: past n, -1: out-of-range table index
+            if (row < n) {
+              const int64_t c = inv.ch[row], h = inv.pos[2 * row], w = inv.pos[2 * row + 1];
+              const bool ok = c >= 0 && c < 3 && h >= 0 && h < inv.maxph && w >= 0 && w < inv.maxpw;
+              if (!ok) atomicOr(inv.err, 1);
+              tb = ok ? ((c * inv.maxph + h) * inv.maxpw + w) * N : -1;
+            }
+            Tb[tid] = tb;
+          }
+          __syncthreads();
+          for (int e = tid; e < WPR * kTokW * N4; e += kThr) {
+            const int i = e / N4, c4 = e - i * N4;
+            const int64_t tb = Tb[i];
+            if (tb == -2) continue;
+            float4 y = *reinterpret_cast<const float4*>(stg + i * N + 4 * c4);
+            if (tb >= 0) {
+              const float4 md = *reinterpret_cast<const float4*>(inv.med + tb + 4 * c4);
+              const float4 bd = *reinterpret_cast<const float4*>(inv.b + tb + 4 * c4);
+              y = make_float4(pn_inverse(y.x, md.x, bd.x, inv.eps), pn_inverse(y.y, md.y, bd.y, inv.eps),
+                              pn_inverse(y.z, md.z, bd.z, inv.eps), pn_inverse(y.w, md.w, bd.w, inv.eps));
+            } else {
+              const float qn = __int_as_float(0x7fc00000);
+              y = make_float4(qn, qn, qn, qn);
+            }
+            *reinterpret_cast<float4*>(out + (rt0 + i) * N + 4 * c4) = y;
+          }
         }
-      }
+      } else {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int col = 16 * t + r;
-        if (col >= N) continue;
-        const float bb = bias ? bias[col] : 0.f;
+        for (int t = 0; t < NT; ++t) {
+          const int col = 16 * t + r;
+          if (col >= N) continue;
+          const float bb = bias ? bias[col] : 0.f;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const int64_t row = wt0 + 4 * q + v;
-          if (row >= n) continue;
-          float y = acc[m][t][v] + bb;
-          if (inv.ch)
-            y = tab[v] >= 0 ? pn_inverse(y, inv.med[tab[v] + col], inv.b[tab[v] + col], inv.eps)
-                            : __int_as_float(0x7fc00000);
-          out[row * N + col] = y;
+          for (int v = 0; v < 4; ++v) {
+            const int64_t row = wt0 + 4 * q + v;
+            if (row < n) out[row * N + col] = acc[m][t][v] + bb;
+          }
         }
       }
     }
