@@ -348,6 +348,10 @@ def lfq_project_out_inverse_norm(idx: torch.Tensor, w: torch.Tensor, b: Optional
     pos = positions.long().contiguous()
     if ch.numel() != n or pos.numel() != 2 * n:
         raise AssertionError("channels/positions do not match the indices")
+    tshape = (3, p.max_patch_h, p.max_patch_w, dim)
+    for t in (norm.median, norm.b):
+        if tuple(t.shape) != tshape or not t.is_contiguous() or t.dtype != torch.float32:
+            raise AssertionError(f"PatchNorm tables must be contiguous fp32 {tshape}, got {tuple(t.shape)}")
     out = torch.empty((*ii.shape[:-1], dim), dtype=torch.float32, device=dev)
     rc = ctx.lib.dctae_lfq_project_out_inverse_norm(ctx.h, C.byref(cfg), ptr(ii), n, dim, ptr(w), ptr(b),
                                                     C.byref(norm.c()), p.max_patch_h, p.max_patch_w, ptr(ch),

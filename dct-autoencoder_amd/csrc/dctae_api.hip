@@ -368,6 +368,10 @@ EncParams enc_params(const dctae_fe_cfg* cfg, const dctae_norm* norm, const dcta
     ep.cb_dim = lfq->codebook_dim;
     ep.ncb = lfq->num_codebooks;
     ep.scale = lfq->codebook_scale;
+    uint64_t pos, neg;
+    lfq_index_masks(ep.scale, ep.cb_dim, &pos, &neg);
+    ep.code_pos = (uint32_t)pos;
+    ep.code_neg = (uint32_t)neg;
   }
   return ep;
 }
@@ -729,9 +733,17 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "chunk_bytes" && value >= (1 << 20)) ctx->chunk_bytes = value;
   else if (k == "xcd_order") ctx->xcd_order = value != 0;
   else if (k == "workspace_limit" && value >= (1 << 20)) ctx->ws_limit = value;
+#ifdef DCTAE_PROFILING
+  // profiling switches: they make dctae_encode write WRONG outputs (shared T
+  // slots, skipped loads / stores) and exist only in a profiling build
+  // (`make PROFILING=1`, a separate library), never in the shipped one
   else if (k == "t_alias" && value >= 0) ctx->t_alias = (int)value;
   else if (k == "rows_ablate" && value >= 0 && value <= 3) ctx->rows_ablate = (int)value;
   else if (k == "bs_ablate" && value >= 0 && value <= 7) ctx->bs_ablate = (int)value;
+#else
+  else if (k == "t_alias" || k == "rows_ablate" || k == "bs_ablate")
+    return fail(ctx, DCTAE_EUNSUP, "option " + k + " exists only in a profiling build (make PROFILING=1)");
+#endif
   else if (k == "rows_kernel" && (value == 2 || value == 3)) ctx->rows_kernel = (int)value;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
@@ -1672,7 +1684,7 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, i
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   Timer t(ctx, s, "lfq_project_in");
-  launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, idx, s);
+  launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, idx, s);
   HIPCHK(ctx, hipGetLastError());
   return 0;
 }
@@ -1698,6 +1710,10 @@ int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, con
   if (!norm || !norm->median_dev || !norm->b_dev || max_patch_h < 1 || max_patch_w < 1 ||
       (n > 0 && (!channels || !positions)))
     return fail(ctx, DCTAE_EINVAL, "inverse PatchNorm needs tables, max_patch_h/w and channels / positions");
+  // the fused inverse reads the (3, max_patch_h, max_patch_w, dim) tables and
+  // writes out as float4 pieces along each token's dim floats
+  if (((uintptr_t)norm->median_dev | (uintptr_t)norm->b_dev | (uintptr_t)out) & 15)
+    return fail(ctx, DCTAE_EINVAL, "fused inverse PatchNorm needs 16-byte aligned median / b / out");
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   Timer t(ctx, s, "lfq_project_out");

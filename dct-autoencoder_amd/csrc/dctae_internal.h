@@ -81,7 +81,24 @@ struct EncParams {
   // LFQ
   int32_t cb_dim, ncb;
   float scale;
+  // index rule masks (lfq_index_bits): the staged u16 codes hold the raw sign
+  // bits x > 0; the packing kernels map them (code_pos/code_neg: cb_dim bits)
+  uint32_t code_pos, code_neg;
 };
+
+// The reference's LFQ index bit (lfq.py:174-187) is taken from the QUANTIZED
+// value: q = where(x > 0, +s, -s), bit = q > 0.  With b = (x > 0) (NaN -> 0):
+// bit = b ? (s > 0) : (-s > 0), i.e. b for s > 0, !b for s < 0 (NaN x -> 1),
+// 0 for s == 0.  pos / neg = all-ones masks of the cb_dim code bits when
+// s > 0 / -s > 0 (fp32 s, as the reference's ones_like(x) * s), else 0.
+__host__ __device__ inline uint64_t lfq_index_bits(uint64_t b, uint64_t pos, uint64_t neg) {
+  return (b & pos) | (~b & neg);
+}
+inline void lfq_index_masks(float s, int cb_dim, uint64_t* pos, uint64_t* neg) {
+  const uint64_t full = cb_dim >= 64 ? ~0ull : ((1ull << cb_dim) - 1ull);
+  *pos = s > 0.0f ? full : 0ull;
+  *neg = -s > 0.0f ? full : 0ull;
+}
 
 struct TokenSinks {
   uint16_t* codes;   // (T, ncb) or null

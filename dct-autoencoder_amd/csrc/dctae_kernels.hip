@@ -485,7 +485,8 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
     for (int e = tid; e < d.k * ncb; e += nt) {
       const int t = e / ncb, q = e % ncb;
       const uint32_t f = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu);
-      out.codes[(base + t) * ncb + q] = st.codes[(d.tok_off + f) * ncb + q];
+      out.codes[(base + t) * ncb + q] = (int64_t)lfq_index_bits(st.codes[(d.tok_off + f) * ncb + q], ep.code_pos,
+                                                                ep.code_neg);
     }
   }
   if (out.patches || out.raw) {
@@ -567,16 +568,18 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     // two codes per lane: one u32 of the u16 staging -> one 16-byte int64 pair (coalesced)
     const uint32_t* src = reinterpret_cast<const uint32_t*>(st.codes);
     longlong2* dst = reinterpret_cast<longlong2*>(out.codes);
+    const uint32_t pos2 = ep.code_pos | (ep.code_pos << 16), neg2 = ep.code_neg | (ep.code_neg << 16);
     for (int e = tid; e < d.k * 7; e += kSortBS) {
       const int t = e / 7, q = e - t * 7;
-      const uint32_t v = src[(d.tok_off + order[t]) * 7 + q];
+      const uint32_t v = (uint32_t)lfq_index_bits(src[(d.tok_off + order[t]) * 7 + q], pos2, neg2);
       dst[(base + t) * 7 + q] = make_longlong2(v & 0xFFFFu, v >> 16);
     }
   } else if (out.codes) {
     const int ncb = ep.ncb;
     for (int e = tid; e < d.k * ncb; e += kSortBS) {
       const int t = e / ncb, q = e - t * ncb;
-      out.codes[(base + t) * ncb + q] = st.codes[(d.tok_off + order[t]) * ncb + q];
+      out.codes[(base + t) * ncb + q] =
+          (int64_t)lfq_index_bits(st.codes[(d.tok_off + order[t]) * ncb + q], ep.code_pos, ep.code_neg);
     }
   }
   if (out.patches || out.raw) gather_tokens(d, order, base, PP, st, out, tid, kSortBS);
@@ -615,7 +618,7 @@ __global__ void k_pad_fill(const int32_t* __restrict__ row_len, int n_rows, EncP
       for (int q = threadIdx.x; q < ep.ncb; q += blockDim.x) {
         uint32_t code = 0;
         for (int dd = 0; dd < ep.cb_dim; ++dd) code |= (pp[q * ep.cb_dim + dd] > 0.0f ? 1u : 0u) << (ep.cb_dim - 1 - dd);
-        pcode[q] = code;
+        pcode[q] = (int64_t)lfq_index_bits(code, ep.code_pos, ep.code_neg);
       }
     __syncthreads();
   }
@@ -680,7 +683,7 @@ void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t 
 
 // LFQ forward: one thread per (token, codebook)
 __global__ void k_lfq_forward(const float* __restrict__ x, int64_t n, int cb_dim, int ncb, float scale,
-                              float* __restrict__ q, int64_t* __restrict__ idx) {
+                              uint64_t code_pos, uint64_t code_neg, float* __restrict__ q, int64_t* __restrict__ idx) {
   const int64_t total = n * ncb;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * blockDim.x) {
@@ -691,7 +694,7 @@ __global__ void k_lfq_forward(const float* __restrict__ x, int64_t n, int cb_dim
       code += pos ? ((int64_t)1 << (cb_dim - 1 - d)) : 0;
       if (q) q[e * cb_dim + d] = pos ? scale : -scale;
     }
-    idx[e] = code;
+    idx[e] = (int64_t)lfq_index_bits((uint64_t)code, code_pos, code_neg);   // lfq.py:187 (quantized > 0)
   }
 }
 
@@ -700,7 +703,9 @@ void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float sc
   int64_t total = n * ncb;
   int gx = (int)std::min<int64_t>((total + 255) / 256, 8192);
   if (gx <= 0) return;
-  hipLaunchKernelGGL(k_lfq_forward, dim3(gx), dim3(256), 0, s, x, n, cb_dim, ncb, scale, q, idx);
+  uint64_t pos, neg;
+  lfq_index_masks(scale, cb_dim, &pos, &neg);
+  hipLaunchKernelGGL(k_lfq_forward, dim3(gx), dim3(256), 0, s, x, n, cb_dim, ncb, scale, pos, neg, q, idx);
 }
 
 // LFQ.indices_to_codes: bits * scale * 2 - scale

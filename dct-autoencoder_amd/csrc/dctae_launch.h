@@ -33,7 +33,7 @@ void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float sc
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
 // dctae_lfq_proj.hip: LFQ with projections, fused project_in + sign + pack / codes + project_out
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                           int64_t* idx, hipStream_t s);
+                           float scale, int64_t* idx, hipStream_t s);
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                              uint16_t* idx, hipStream_t s);
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,

@@ -184,8 +184,9 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
         const uint32_t code = __builtin_bitreverse32(bits) >> (32 - cd);
         if (idx16)
           idx16[wt0 * ncb + p] = (uint16_t)code;   // encode staging (cd <= 16), gathered by k_sort_pack2
-        else
-          idx_out[wt0 * ncb + p] = (int64_t)code;
+        else   // lfq.py:187: the bit of the quantized value (the staging above keeps the raw sign bits)
+          idx_out[wt0 * ncb + p] = (int64_t)lfq_index_bits(code, scale > 0.0f ? ~0ull : 0ull, -scale > 0.0f ? ~0ull : 0ull) &
+                                   ((1ll << cd) - 1);
       }
     } else {
       if (inv.ch) {
@@ -289,9 +290,9 @@ static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* id
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                           int64_t* idx, hipStream_t s) {
+                           float scale, int64_t* idx, hipStream_t s) {
   if (n <= 0) return;
-  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, idx, nullptr);
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, scale, idx, nullptr);
 }
 
 // the same into the encode's u16 token staging (cd <= 16)

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "dctae_model.h"
+#include "dctae_internal.h"
 
 namespace dctae {
 
@@ -601,7 +602,9 @@ __global__ void k_lfq_codes(LfqArgs a) {
     if (a.q_bf16) a.q_bf16[m * a.ldq + j * a.cbd + d] = f2bf(q);
     if (a.q_f32) a.q_f32[m * a.ldq + j * a.cbd + d] = q;
   }
-  a.codes[i] = code;
+  // lfq.py:187: the index bit of the quantized value (any codebook_scale sign)
+  a.codes[i] = (int64_t)lfq_index_bits((uint64_t)code, a.scale > 0.0f ? ~0ull : 0ull, -a.scale > 0.0f ? ~0ull : 0ull) &
+               ((1ll << a.cbd) - 1);
   if (a.q_bf16 && j == a.ncb - 1)
     for (int k = a.ncb * a.cbd; k < a.ldq; ++k) a.q_bf16[m * a.ldq + k] = 0;
 }

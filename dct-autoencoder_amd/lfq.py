@@ -63,38 +63,51 @@ class LFQ(nn.Module):
             self.register_buffer("codebook", bits * codebook_scale * 2 - codebook_scale, persistent=False)
 
     def _fused_proj(self) -> bool:
+        """The fused MFMA projection kernels compute in fp32: they serve fp32
+        projection weights only.  fp16 / bf16 models keep the reference's
+        nn.Linear in the model dtype (then the HIP sign / packing kernel), so
+        the sign bits are those of the model-dtype projection."""
         cdims = self.codebook_dim * self.num_codebooks
         return (self.has_projections and self.dim % 4 == 0 and 4 <= self.dim <= 256 and cdims % 4 == 0
-                and cdims <= 256 and self.codebook_dim <= 31 and self.num_codebooks <= 32)
+                and cdims <= 256 and self.codebook_dim <= 31 and self.num_codebooks <= 32
+                and self.project_in.weight.dtype == torch.float32
+                and self.project_out.weight.dtype == torch.float32)
 
-    def _proj_w(self, lin: nn.Linear, dev):
-        """fp32 contiguous copies of a projection's weight / bias on ``dev``
-        (cached per parameter version: a .half() model or an optimiser step
-        refreshes them)."""
-        key = (id(lin), dev, lin.weight._version, lin.weight.data_ptr(),
-               None if lin.bias is None else (lin.bias._version, lin.bias.data_ptr()))
-        cache = self.__dict__.setdefault("_proj_cache", {})
-        if cache.get(id(lin), (None,))[0] != key:
-            w = lin.weight.detach().to(device=dev, dtype=torch.float32).contiguous()
-            b = None if lin.bias is None else lin.bias.detach().to(device=dev, dtype=torch.float32).contiguous()
-            cache[id(lin)] = (key, w, b)
-        return cache[id(lin)][1:]
+    @staticmethod
+    def _proj_w(lin: nn.Linear, dev):
+        """A projection's fp32 weight / bias on ``dev``, contiguous.  No cache:
+        the parameters themselves are used when they already are that (the
+        usual case), so in-place updates (``weight.data.copy_``) are always
+        seen; otherwise a fresh copy is made per call (a few hundred KB)."""
+        def f32(t):
+            return None if t is None else t.detach().to(device=dev, dtype=torch.float32).contiguous()
+        return f32(lin.weight), f32(lin.bias)
 
     def project_codes(self, x):
         """Indices only (the encode path): x (..., dim) -> (..., num_codebooks),
         project_in fused with the sign / packing when there are projections."""
         if self._fused_proj():
             w, b = self._proj_w(self.project_in, x.device)
-            return _ops.lfq_project_in(x, w, b, self.cfg())
-        _, idx = _ops.lfq_forward(self.project_in(x), self.cfg(), want_quantized=False)
+            return _ops.lfq_project_in(x, w, b, self.cfg(self.project_in.weight.dtype))
+        h = self.project_in(x)
+        _, idx = _ops.lfq_forward(h, self.cfg(h.dtype), want_quantized=False)
         return idx
 
-    def cfg(self) -> LFQCfg:
-        return LFQCfg(self.codebook_dim, self.num_codebooks, float(self.codebook_scale))
+    def cfg(self, dtype=None) -> LFQCfg:
+        """Kernel config.  ``dtype``: the dtype the reference forms
+        ``ones_like(x) * codebook_scale`` in (lfq.py:174): the index bit is the
+        sign of that rounded scale (lfq.py:187), so the scale is rounded to it."""
+        s = float(self.codebook_scale)
+        if dtype is not None and dtype.is_floating_point and dtype != torch.float64:
+            s = float(torch.tensor(s, dtype=dtype))
+        return LFQCfg(self.codebook_dim, self.num_codebooks, s)
 
     @property
     def dtype(self):
-        return self.mask.dtype if not hasattr(self, "codebook") else self.codebook.dtype
+        """The codebook's float dtype (lfq.py:101-103).  Codebooks above 2**16
+        entries are not materialised; the float buffer ``zero`` follows the same
+        module casts (.half(), .to(dtype)), so its dtype stands in."""
+        return self.codebook.dtype if hasattr(self, "codebook") else self.zero.dtype
 
     def bits_to_codes(self, bits):
         return bits * self.codebook_scale * 2 - self.codebook_scale
@@ -136,7 +149,7 @@ class LFQ(nn.Module):
             q = _ops.lfq_project_out(indices, w, b, self.cfg()).to(x.dtype)
         else:
             x = self.project_in(x)
-            q, indices = _ops.lfq_forward(x, self.cfg())
+            q, indices = _ops.lfq_forward(x, self.cfg(x.dtype))
             q = self.project_out(q.to(x.dtype))   # the reference keeps the input dtype (fp16 / bf16 models)
         if is_img_or_video:
             q = q.reshape(*shape[:-1], q.shape[-1])

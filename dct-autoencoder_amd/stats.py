@@ -10,10 +10,11 @@ scatter_add_ passes.  Here the whole update is one C-ABI call
         -> running-median merge -> sum |x - median| in batch order
         -> running-b merge -> n += batch_n -> pads zeroed
 
-Results are bit-exact with the reference (tests/test_gpu_parity.py::
-test_train_step_*): the per-cell lists keep batch order, which is the
-reference's scatter_add_ accumulation order, and every fp32 op is rounded
-like the reference's separate torch ops.
+Results are bit-exact with the reference (tests/test_gpu_stats.py::
+test_train_step_reproduces_reference_fit / test_train_step_matches_oracle):
+the per-cell lists keep batch order, which is the reference's scatter_add_
+accumulation order, and every fp32 op is rounded like the reference's
+separate torch ops.
 
 Like the reference, the update replaces the tables (``.data = new``) rather
 than mutating the tensors a caller may hold.

@@ -214,3 +214,29 @@ def test_vq_oracle_matches_reference():
         assert torch.allclose(st.batch_variance, torch.from_numpy(g[f"batch_variance{step}"]), atol=1e-7, rtol=1e-6)
     codes = ref_cpu.vq_codes_from_indices(st, torch.from_numpy(g["indices0"]))
     assert torch.equal(codes, torch.from_numpy(g["codes_from_indices0"]))
+
+
+@pytest.mark.parametrize("proj", [False, True])
+def test_lfq_scale_rule_matches_reference(proj):
+    """lfq.py:174-187 at codebook_scale 1, 0.5, 0, -1, -0.25: the index bit is
+    that of the QUANTIZED value (s < 0 inverts every bit, NaN inputs included;
+    s == 0 gives 0).  Fixture: the reference's own LFQ (gen_lfq_scale_golden.py)."""
+    import torch.nn.functional as F
+    g = golden("lfq_scale_ref.npz")
+    x = torch.from_numpy(g["x"])
+    tag = "p" if proj else "n"
+    for si, s in enumerate(g["scales"]):
+        if proj:
+            cfg = ref_cpu.LFQConfig(dim=196, codebook_size=2 ** 13, num_codebooks=16, codebook_scale=float(s))
+            win, bin_ = torch.from_numpy(g["w_in"]), torch.from_numpy(g["b_in"])
+            wout, bout = torch.from_numpy(g["w_out"]), torch.from_numpy(g["b_out"])
+            q, idx = ref_cpu.lfq_forward(x, cfg, project_in=lambda t: F.linear(t, win, bin_),
+                                         project_out=lambda t: F.linear(t, wout, bout))
+            codes = ref_cpu.lfq_indices_to_codes(idx, cfg, project_out=lambda t: F.linear(t, wout, bout))
+        else:
+            cfg = ref_cpu.LFQConfig(codebook_scale=float(s))
+            q, idx = ref_cpu.lfq_forward(x, cfg)
+            codes = ref_cpu.lfq_indices_to_codes(idx, cfg)
+        assert torch.equal(idx, torch.from_numpy(g[f"{tag}{si}_idx"])), s
+        torch.testing.assert_close(q, torch.from_numpy(g[f"{tag}{si}_q"]), rtol=0, atol=0, equal_nan=True)
+        torch.testing.assert_close(codes, torch.from_numpy(g[f"{tag}{si}_codes"]), rtol=0, atol=0)

@@ -2,6 +2,9 @@
 # Bluestein kernel ablation on the config-4 encode: per library option set,
 # rocprofv3 kernel stats of the k_bs_* kernels (profiling only; outputs invalid
 # under bs_ablate).   bash tools/gpu_cfg4_ablate.sh "bs_ablate=0" "bs_ablate=2" ...
+# The switches exist only in a profiling build: first (in the build container)
+#   make -C dct-autoencoder_amd/csrc PROFILING=1 LIB=../../_ablate/libdctae_prof.so OBJDIR=../../_ablate/obj
+# and run with DCTAE_LIBRARY=_ablate/libdctae_prof.so.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
