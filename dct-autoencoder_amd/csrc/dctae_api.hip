@@ -1320,7 +1320,14 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   if (full && E.n_img > 0) {
     Timer t(ctx, s, "sort_pack");
     EncParams eps = ep;
-    if (proj_w) eps.ncb = lfq->num_codebooks;
+    if (proj_w) {   // the projection kernel staged raw sign bits: the pack maps them (lfq_index_bits)
+      eps.ncb = lfq->num_codebooks;
+      eps.cb_dim = lfq->codebook_dim;
+      uint64_t pos, neg;
+      lfq_index_masks(lfq->codebook_scale, lfq->codebook_dim, &pos, &neg);
+      eps.code_pos = (uint32_t)pos;
+      eps.code_neg = (uint32_t)neg;
+    }
     launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), eps, sk, ps, s,
                      ctx->sort_kernel, E.max_T);
   }
