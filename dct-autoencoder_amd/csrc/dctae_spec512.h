@@ -3,6 +3,7 @@
 // epilogue.
 #pragma once
 #include "dctae_device.h"
+#include "dctae_fft_common.h"
 
 namespace dctae {
 
@@ -134,6 +135,9 @@ __device__ __forceinline__ int cols7_j2(int w, int g) {
   return base;
 }
 
+// AUX: buffer-load cache policy (16 = sc1: served by the XCD's L2, never by
+// a possibly stale L1 line — the persistent encode's same-XCD hand-off)
+template <int AUX = 0>
 __device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
                                            float (&va)[16], float (&vb)[16]) {
   constexpr int N = 512;
@@ -147,7 +151,7 @@ __device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, c
   const int lo = (4 * j1 * rs + col) * 4;
   const int hi = ((2 * N - 1 - 4 * j1 - 64 * 15) * rs + col) * 4;   // r = 15: lowest row of the upper half
   const int step = 64 * rs * 4, two = 2 * rs * 4;
-  constexpr int aux = 0;
+  constexpr int aux = AUX;
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo, r * step, aux));
@@ -159,5 +163,124 @@ __device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, c
     vb[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, hi - two, (15 - r) * step, aux));
   }
 }
+
+// ---------------------------------------------------------------------------
+// cols7 (N = 512): the column FFT with ONE LDS exchange.  Lane (w, g, col) =
+// (wave, 16-lane row, column of the strip; col 14, 15 idle).
+//  * pass 1: butterfly j1 = 4w + g reads z[j1 + 16 r] straight from T in
+//    global memory (Makhoul pairs (x[4m], x[4m+2]) / (x[2N-1-4m], x[2N-3-4m]),
+//    14 consecutive floats of a T row per 16-lane row), DFT16 in registers,
+//    writes z[16 j1 + r] to LDS;
+//  * pass 2: butterfly j2 (wave w owns the pairs j2 / 16 - j2) reads
+//    z[j2 + 16 r], twiddles, DFT16: Z[j2 + 16 r] in registers;
+//  * Makhoul post needs Z[M - k] = the partner row's Z[(16 - j2) + 16 (15 - i)]:
+//    a v_permlane16_swap between rows g and g ^ 1 (j2 = 0 and 8 pair with
+//    themselves), no LDS;
+//  * X (448 x 14 kept coefficients) -> LDS -> the cols5 token epilogue.
+// LDS slot of complex element m, column col: 16 m' + col, m' = m ^ bit3(m)
+// (a permutation): the two 16-lane rows of a ds_read_b64 half-wave
+// (j2 = a, 16 - a: bit 3 differs) fall on opposite 32-bank halves.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float partner_row(float x, bool even_row) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(even_row ? r[1] : r[0]);
+}
+
+// X aliases z (one more barrier, 37 KB instead of 62 KB: 4 workgroups per CU)
+union Cols7Lds {
+  float2 z[256 * 16];
+  float X[448 * 14];
+};
+
+// Makhoul post of cols7 for one lane: v = Z[j2 + 16 i]; writes X[k], X[N - k]
+// (Kh = 448: X[N - k] kept for k > 64) and X[M] (j2 = 0).  W0: wave 0, whose
+// rows 0 and 1 (j2 = 0, 8) pair with themselves.
+template <bool W0>
+__device__ __forceinline__ void cols7_post(const cf (&v)[16], int j2, int g, int col, const float4* post4,
+                                           float* Xs) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14;
+  const bool on_col = col < KS;
+  const bool self = W0 && g < 2;
+  float* xa = Xs + j2 * KS + col;                        // X[j2 + 16 i] at + 224 i
+  float* xb = Xs + (N - j2 - 16 * 15) * KS + col;        // X[N - j2 - 16 i] at + 224 (15 - i)
+  const float4* ps = post4 + j2;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    cf P;
+    P.x = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v[15 - i].x), 0x401f));   // lane ^ 16
+    P.y = __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v[15 - i].y), 0x401f));
+    if (W0) P = self ? ((j2 == 0) ? v[(16 - i) & 15] : v[15 - i]) : P;
+    const cf A = v[i];
+    const float4 ab = ps[16 * i];
+    const cf al = (cf){ab.x, ab.y}, be = (cf){ab.z, ab.w};
+    const cf s1 = add_conj(A, P), d1 = sub_conj(A, P);
+    const cf W = fma_iw(d1, be, fma_x(d1, be, fma_iw(s1, al, mul_x(s1, al))));
+    if (on_col) {
+      xa[224 * i] = W.x;
+      if (i > 4 || (i == 4 && j2 > 0)) xb[224 * (15 - i)] = -W.y;
+    }
+  }
+  if (W0 && j2 == 0 && on_col) {   // k = M (< Kh): A = B = Z[0]
+    const cf A = v[0];
+    const float4 ab = post4[M];
+    const cf s1 = add_conj(A, A), d1 = sub_conj(A, A);
+    const cf W = fma_iw(d1, (cf){ab.z, ab.w}, fma_x(d1, (cf){ab.z, ab.w}, cmul_pk(s1, (cf){ab.x, ab.y})));
+    Xs[M * KS + col] = W.x;
+  }
+}
+
+template <bool THR>
+__device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip, Cols7Lds& L, const float (&va)[16],
+                                              const float (&vb)[16], const float4* post4, const float2* tw_s,
+                                              const float* sbias, const float2 (&thr_r)[2][7], const EncParams& ep,
+                                              const TokenSinks& sk) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14, M16 = 16;
+  const int tid = opaque_tid();
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), g = (tid >> 4) & 3, col = tid & 15;
+  const bool on_col = col < KS;
+  cf* z = reinterpret_cast<cf*>(L.z);
+  (void)d;
+  // ---- pass 1 (Ns = 1): j1 = tid >> 4
+  {
+    const int j1 = tid >> 4;
+    cf v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = (cf){va[r], vb[r]};
+    DFTV<16>::run(v);
+    if (on_col) {
+      cf* zw = z + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) zw[z7addr(16 * j1 + r)] = v[r];
+    }
+  }
+  __syncthreads();
+  // ---- pass 2 (Ns = 16): z[j2 + 16 r] * W_M^{r j2} -> DFT16 -> Z[j2 + 16 r]
+  const int j2 = cols7_j2(w, g);
+  cf v[16];
+  {
+    const cf* zr = z + col;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = zr[z7addr(j2 + 16 * r)];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      const float2 tw = tw_s[r * j2];
+      v[r] = cmul_pk(v[r], (cf){tw.x, tw.y});
+    }
+    DFTV<16>::run(v);
+  }
+  // X aliases z: every wave's pass-2 reads of z must be done before any post writes X
+  __syncthreads();
+  // ---- Makhoul post: k = j2 + 16 i; A = Z[k], B = conj Z[M - k]
+  //      j2 >= 1: Z[M - k] = partner row's v[15 - i] (lane ^ 16, ds_swizzle);
+  //      j2 = 0: own v[(16 - i) & 15];  j2 = 8: own v[15 - i]  (wave 0, rows 0 and 1)
+  //      kept rows: Kh = 448 (H = 512): X[k] always, X[N - k] for k > 64
+  if (w == 0) cols7_post<true>(v, j2, g, col, post4, L.X);
+  else cols7_post<false>(v, j2, g, col, post4, L.X);
+  __syncthreads();
+  cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sbias, thr_r, ep, sk);
+}
+
 
 }  // namespace dctae
