@@ -78,6 +78,13 @@ struct dctae_ctx {
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
   int n_cu = 256;
+  // persistent XCD-local 512^2 encode (dctae_enc512.hip): T slots and the
+  // per-call sync words (grow-only); enc512 = 0 selects the two-kernel path
+  int enc512 = 1;
+  float* enc_slots = nullptr;
+  unsigned* enc_sync = nullptr;
+  size_t enc_sync_words = 0;
+  int enc_grid = 0;   // 0: occupancy x CUs
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
@@ -615,6 +622,10 @@ struct EncPlan {
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
   bool any_pad = true;   // some packed row shorter than max_seq_len
+  // every image 512 x 512 on the Makhoul plan with 32 x 32 tiles kept: the
+  // persistent encode (k_enc512) can run the rows + columns of the whole call
+  bool all512 = false;
+  int64_t tw512 = 0, post512 = 0;   // the N = 512 plan's tables
 };
 
 // ---------------------------------------------------------------------------
@@ -681,6 +692,8 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->fft_tab) hipFree(ctx->fft_tab);
   if (ctx->st_ws) hipFree(ctx->st_ws);
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
+  if (ctx->enc_slots) hipFree(ctx->enc_slots);
+  if (ctx->enc_sync) hipFree(ctx->enc_sync);
   delete ctx->enc_plan;
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
@@ -748,6 +761,8 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
+  else if (k == "enc512") ctx->enc512 = value != 0;
+  else if (k == "enc_grid" && value >= 0 && value <= (1 << 16)) ctx->enc_grid = (int)value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -823,6 +838,7 @@ int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
   if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
   if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
   if (h & 16) return fail(ctx, DCTAE_EINVAL, "VectorQuantize index out of range of the codebook");
+  if (h & 32) return fail(ctx, DCTAE_EHIP, "persistent encode (k_enc512): a hand-off wait timed out; outputs invalid");
   return 0;
 }
 
@@ -1106,6 +1122,16 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     j.pc_qw = pc_qw;
     j.pc_off = E.pb.add(pc.data(), pc.size());
   }
+  E.all512 = n > 0;
+  for (int i = 0; i < n && E.all512; ++i) {
+    const ImgDesc& d = D[i];
+    E.all512 = d.H == 512 && d.W == 512 && d.qh == 32 && d.qw == 32 && d.plan_w >= 0 && d.plan_h >= 0 &&
+               plans[d.plan_w].spec == 1 && plans[d.plan_h].spec == 1 && d.bs == 0;
+  }
+  if (E.all512) {
+    E.tw512 = plans[D[0].plan_w].tw_off;
+    E.post512 = plans[D[0].plan_w].post_off;
+  }
   E.plans_off = E.pb.add(plans.data(), plans.size());
   E.all_desc_off = E.pb.add(D.data(), D.size());
   if (full && pack->n_rows > 0) E.rowlen_off = E.pb.add(pack->row_len, pack->n_rows);
@@ -1309,9 +1335,31 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                              v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr, v == 1 ? j.n_pc : 0, j.pc_qw);
       }
   };
-  for (const ChunkJob& j : E.jobs) {
-    do_rows(j, s);
-    do_cols(j, s);
+  // the persistent XCD-local encode (dctae_enc512.hip): codes-only 512^2 calls
+  // with the exact LFQ thresholds (14 codebooks of 14 bits, the cols7 epilogue)
+  const bool thr_codes = epj.median && epj.thr && !skc.norm && !skc.raw && skc.codes && epj.maxph <= 32 &&
+                         epj.cb_dim == 14 && epj.ncb == 14;
+  if (E.all512 && ctx->enc512 && ctx->rows_kernel == 3 && thr_codes && !ctx->t_alias && !ctx->rows_ablate) {
+    const size_t words = enc512_sync_words(E.n_img);
+    if (!ctx->enc_slots) {
+      HIPCHK(ctx, hipMalloc((void**)&ctx->enc_slots, enc512_slot_bytes()));
+    }
+    if (words > ctx->enc_sync_words) {
+      if (ctx->enc_sync) HIPCHK(ctx, hipFree(ctx->enc_sync));
+      ctx->enc_sync = nullptr;
+      HIPCHK(ctx, hipMalloc((void**)&ctx->enc_sync, words * sizeof(unsigned)));
+      ctx->enc_sync_words = words;
+    }
+    const int grid = ctx->enc_grid > 0 ? ctx->enc_grid : enc512_grid(ctx->device);
+    Timer t(ctx, s, "enc512");
+    launch_enc512((const ImgDesc*)(pd + E.all_desc_off), E.n_img, imgs->rgb_dev, ctx->enc_slots,
+                  ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, epj, skc, ctx->enc_sync, grid,
+                  ctx->err_dev, s);
+  } else {
+    for (const ChunkJob& j : E.jobs) {
+      do_rows(j, s);
+      do_cols(j, s);
+    }
   }
   if (proj_w && E.n_tok > 0) {
     Timer t(ctx, s, "lfq_project_in");
@@ -1748,6 +1796,8 @@ static int vq_scratch(dctae_ctx* ctx, size_t need) {
   if (need <= ctx->vq_bytes) return 0;
   HIPCHK(ctx, hipDeviceSynchronize());
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
+  if (ctx->enc_slots) hipFree(ctx->enc_slots);
+  if (ctx->enc_sync) hipFree(ctx->enc_sync);
   ctx->vq_ws = nullptr;
   ctx->vq_bytes = 0;
   if (hipMalloc((void**)&ctx->vq_ws, need) != hipSuccess)

@@ -1,0 +1,234 @@
+// k_enc512: the 512^2 encode's row and column passes in ONE persistent launch
+// whose row -> column hand-off of the intermediate T stays inside one XCD,
+// so T (2.75 MB per image) is written to and read from that XCD's L2 (and
+// the Infinity Cache behind it) instead of making an HBM round trip between
+// two launches (SURVEY §7 hard part 2; reference util.py:333-334: dct_2d =
+// the row DCT, then the column DCT of its result).
+//
+// Work per image: 32 row items (16 rows each: rows512_item, dctae_rows512.h)
+// then 96 column items ((channel, tile column) x 448 kept rows: the cols7
+// transform + exact-threshold LFQ epilogue, dctae_spec512.h).  Every block
+// reads its XCD's id (HW_REG_XCC_ID) at run time and takes items from that
+// XCD's queue only, so producer and consumer of a T slot always share an L2;
+// nothing depends on how the dispatcher places blocks (an XCD without blocks
+// simply claims no images).
+//
+// Queue of XCD x (positions from its head counter):
+//   segment 0:        R(0) x 32
+//   segment k >= 1:   R(k) x 32, then C(k - 1) x 96
+// Segment k's image is claimed from the global image counter by the block
+// that takes R(k) item 0, after segment k - 1's claim is published (so
+// claims are monotone in k: once a segment gets no image, no later one does).
+// T slot of segment k: k % 3 (of 3 per XCD).  Waits (every one on an item at
+// a LOWER queue position, so the lowest unfinished item can always run: no
+// deadlock, whatever the residency; a block holds at most one taken-ahead
+// item, which is never lower than its current one):
+//   R(k)     waits for C(k - 3) done (its slot's previous reader);
+//   C(k - 1) waits for R(k - 1) done (all 32 row items of its image).
+// Hand-off (same XCD, one L2): producer plain T stores -> every wave
+// s_waitcnt vmcnt(0) -> barrier -> one agent-scope atomic add; consumer polls
+// the counter with relaxed agent-scope (sc1) loads and reads T with sc1 buffer
+// loads (L2-served, never a stale L1 line).  Every spin is bounded: on time
+// out the block sets error bit 32 and leaves (dctae_check_device_errors).
+#include "dctae_launch.h"
+#include "dctae_rows512.h"
+#include "dctae_spec512.h"
+
+namespace dctae {
+
+namespace {
+
+constexpr int kRowItems = 32;                    // 16-row items per image
+constexpr int kColItems = 96;                    // (channel, tile column) items per image
+constexpr int kSeg = kRowItems + kColItems;
+constexpr int kSlots = 3;                        // T slots per XCD
+constexpr int kKW = 448, kH = 512;
+constexpr int64_t kSlotFloats = 3ll * kH * kKW;  // one image's T
+constexpr unsigned kNone = 0x7fffffffu;          // published "no image" (claims start at 1)
+constexpr unsigned kSpinMax = 1u << 22;
+
+// sync block (unsigned words, zeroed per call): [0] image claim counter,
+// [32 (x + 1)] head of XCD x (own 128-byte lines), then
+// img[x][seg] (claimed image + 1, or kNone), rdone[n], cdone[n]
+constexpr int kHeadBase = 32;
+constexpr int kImgBase = 32 * 9;
+
+union EncU {
+  Rows512Xch rows;
+  Cols7Lds cols;
+};
+
+struct EncLds {
+  EncU u;
+  Rows512Tab rt;
+  float4 post4[257];
+  float2 tw_s[256];
+  float sbias[32];
+  int item[4];
+};
+
+__device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane: poll *p until pred holds (bounded; false on time out)
+template <class Pred>
+__device__ __forceinline__ bool spin_until(const unsigned* p, Pred pred, unsigned& v) {
+  for (unsigned it = 0; it < kSpinMax; ++it) {
+    v = ld_agent(p);
+    if (pred(v)) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ imgs, int n_img,
+                                               const float* __restrict__ rgb, float* __restrict__ tslots,
+                                               const float2* __restrict__ tw, const float2* __restrict__ post,
+                                               ColorMats cm, EncParams ep, TokenSinks sk, unsigned* __restrict__ sync,
+                                               int max_seg, int* __restrict__ err) {
+  __shared__ EncLds L;
+  const int tid = threadIdx.x;
+  rows512_tables(L.rt, tw, post);
+  {
+    const float4* p4 = reinterpret_cast<const float4*>(post);
+    for (int i = tid; i < 257; i += 256) L.post4[i] = p4[i];
+    L.tw_s[tid] = tw[tid];
+  }
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  const int x = (int)(xcc & 7);
+  unsigned* head = sync + kHeadBase * (x + 1);
+  unsigned* img_tab = sync + kImgBase + (size_t)x * max_seg;
+  unsigned* rdone = sync + kImgBase + (size_t)8 * max_seg;
+  unsigned* cdone = rdone + n_img;
+  float* tx = tslots + (int64_t)x * kSlots * kSlotFloats;
+
+  // item state in LDS: [0] current position, [1] the taken-ahead position,
+  // [2] image of the current item (or kNone), [3] abort flag
+  if (tid == 0) {
+    L.item[0] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    L.item[3] = 0;
+  }
+  for (;;) {
+    __syncthreads();   // tables (first pass); the previous item's LDS use is over
+    const int p = L.item[0];
+    // decode the position: R(k, i) or C(k, t)
+    bool is_row;
+    int k, i;
+    if (p < kRowItems) {
+      is_row = true, k = 0, i = p;
+    } else {
+      const int q = p - kRowItems, r = q % kSeg;
+      k = q / kSeg + 1;
+      is_row = r < kRowItems;
+      i = is_row ? r : r - kRowItems;
+      if (!is_row) k -= 1;
+    }
+    if (tid == 0) {
+      // take the next position now: the atomic's latency hides behind this item
+      L.item[1] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned img = kNone;
+      bool ok = true;
+      if (k >= max_seg) {
+        img = kNone;
+      } else if (is_row && i == 0) {
+        // claim segment k's image once segment k - 1's claim is published
+        unsigned prev = 1;
+        if (k > 0) ok = spin_until(img_tab + k - 1, [](unsigned v) { return v != 0u; }, prev);
+        if (ok) {
+          if (prev == kNone) {
+            img = kNone;
+          } else {
+            const unsigned n = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            img = n < (unsigned)n_img ? n + 1 : kNone;
+          }
+          __hip_atomic_store(img_tab + k, img, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        ok = spin_until(img_tab + k, [](unsigned v) { return v != 0u; }, img);
+      }
+      if (ok && img != kNone) {
+        const unsigned n = img - 1;
+        unsigned v;
+        if (is_row) {
+          // the slot's previous reader: segment k - 3's 96 column items
+          if (k >= kSlots) {
+            const unsigned pimg = ld_agent(img_tab + k - kSlots);   // published (earlier claim)
+            if (pimg != kNone) ok = spin_until(cdone + (pimg - 1), [](unsigned c) { return c >= (unsigned)kColItems; }, v);
+          }
+        } else {
+          ok = spin_until(rdone + n, [](unsigned c) { return c >= (unsigned)kRowItems; }, v);
+        }
+      }
+      if (!ok) {
+        atomicOr(err, 32);
+        L.item[3] = 1;
+      }
+      L.item[2] = (int)img;
+    }
+    __syncthreads();
+    if (L.item[3]) return;   // a hand-off timed out (error bit 32)
+    const unsigned img = (unsigned)L.item[2];
+    if (img == kNone) {
+      // a column item without an image: every later position is empty too
+      if (!is_row) return;
+    } else {
+      const int n = (int)img - 1;
+      const ImgDesc d = imgs[n];
+      float* T = tx + (int64_t)(k % kSlots) * kSlotFloats;
+      if (is_row) {
+        rows512_item<0>(L.u.rows, L.rt, rgb + d.rgb_off, kH, 16 * i, T, (uint32_t)(kH * kKW * 4), cm);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's T stores reached the L2
+        __syncthreads();
+        if (tid == 0) __hip_atomic_fetch_add(rdone + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        const int c = i >> 5, strip = i & 31;
+        float2 thr_r[2][7];
+        cols_thresholds<true>(d, c, strip, ep, thr_r, L.sbias);
+        float va[16], vb[16];
+        cols7_load<16>(d, c, strip, T, va, vb);
+        cols7_compute<true>(d, c, strip, L.u.cols, va, vb, L.post4, L.tw_s, L.sbias, thr_r, ep, sk);
+        __syncthreads();   // every wave's T loads have returned (their values were used)
+        if (tid == 0) __hip_atomic_fetch_add(cdone + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (tid == 0) L.item[0] = L.item[1];
+  }
+}
+
+size_t enc512_sync_words(int n_img) {
+  const int max_seg = n_img + 2;
+  return (size_t)kImgBase + (size_t)8 * max_seg + 2 * (size_t)n_img;
+}
+
+size_t enc512_slot_bytes() { return (size_t)8 * kSlots * kSlotFloats * sizeof(float); }
+
+int enc512_grid(int device) {
+  static int cached[64] = {0};
+  if (device >= 0 && device < 64 && cached[device]) return cached[device];
+  int per_cu = 0, n_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_enc512, 256, 0) != hipSuccess || per_cu < 1) per_cu = 2;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 1)
+    n_cu = 256;
+  hipGetLastError();
+  const int g = per_cu * n_cu;
+  if (device >= 0 && device < 64) cached[device] = g;
+  return g;
+}
+
+// imgs: n_img 512 x 512 images with qh = qw = 32 (Kw = Kh = 448) in one
+// staging (tok_off); sync: enc512_sync_words(n_img) words, zeroed here;
+// tslots: enc512_slot_bytes().  ep must carry the exact LFQ thresholds.
+void launch_enc512(const ImgDesc* imgs, int n_img, const float* rgb, float* tslots, const float2* tw,
+                   const float2* post, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, unsigned* sync,
+                   int grid, int* err, hipStream_t s) {
+  if (n_img <= 0) return;
+  hipMemsetAsync(sync, 0, enc512_sync_words(n_img) * sizeof(unsigned), s);
+  hipLaunchKernelGGL(k_enc512, dim3(grid), dim3(256), 0, s, imgs, n_img, rgb, tslots, tw, post, cm, ep, sk, sync,
+                     n_img + 2, err);
+}
+
+}  // namespace dctae

@@ -72,6 +72,14 @@ void launch_fft_cols(const ImgDesc* imgs, const FftPlan* plans, const int4* bloc
 void launch_norm_thresholds(const float* med, const float* b, int64_t n, float eps, float lo, float hi, float* thr,
                             int* bad, hipStream_t s);
 
+// dctae_enc512.hip: the persistent XCD-local encode of 512^2 images (rows + columns in one launch)
+size_t enc512_sync_words(int n_img);
+size_t enc512_slot_bytes();
+int enc512_grid(int device);
+void launch_enc512(const ImgDesc* imgs, int n_img, const float* rgb, float* tslots, const float2* tw,
+                   const float2* post, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, unsigned* sync,
+                   int grid, int* err, hipStream_t s);
+
 int fft_spec_id(int N, const int* radix, int npass, int P);
 int fft_spec_rows_per_block(int spec);
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,

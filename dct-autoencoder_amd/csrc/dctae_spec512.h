@@ -236,7 +236,7 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
                                               const float* sbias, const float2 (&thr_r)[2][7], const EncParams& ep,
                                               const TokenSinks& sk) {
 #pragma clang fp contract(fast)
-  constexpr int N = 512, M = 256, KS = 14, M16 = 16;
+  constexpr int KS = 14;
   const int tid = opaque_tid();
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), g = (tid >> 4) & 3, col = tid & 15;
   const bool on_col = col < KS;

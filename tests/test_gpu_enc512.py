@@ -1,0 +1,70 @@
+"""The persistent XCD-local 512^2 encode (k_enc512, dctae_enc512.hip: row and
+column passes in one launch, the intermediate T handed over inside one XCD's
+L2) against the two-kernel path (k_rows512 + k_fft_cols7) it replaces: every
+packed output bit-identical, for batch sizes below, at and above the XCD
+count, and for grids far smaller than the chip (1, 3, 24 blocks: the
+hand-off waits, slot reuse and claim chain then carry the whole batch; one
+block processes every image on a single XCD).  The two-kernel path itself is
+pinned against the oracle by test_gpu_parity.  Run on an MI355X.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def setup(pkg, ref_tables):
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    fe = pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, 32, 32, 3072)
+    pn = pkg.PatchNorm(32, 32, 14, 3).to(DEV)
+    pn.median.data.copy_(ref_tables.median)
+    pn.b.data.copy_(ref_tables.b)
+    pn.frozen = True
+    pn.eval()
+    lfq = pkg.LFQ(dim=196, codebook_size=2 ** 14, num_codebooks=14).to(DEV).eval()
+    return ops, fe_mod, fe, pn, lfq
+
+
+def _run(setup, B, enc512, grid=0, seed=1234, first=0):
+    ops, fe_mod, fe, pn, lfq = setup
+    dev = torch.device(DEV, torch.cuda.current_device())
+    x = ops.synth_images(B, 512, 512, seed=seed, first_index=first, device=dev)
+    ops.set_option("enc512", enc512, dev)
+    ops.set_option("enc_grid", grid, dev)
+    try:
+        enc = fe_mod.BatchEncoder(fe, B, 512, 512, pn, lfq, device=dev)
+        out = {k: v.clone() for k, v in enc(x).items()}
+        torch.cuda.synchronize()
+        ops.check_device_errors(dev)
+    finally:
+        ops.set_option("enc512", 1, dev)
+        ops.set_option("enc_grid", 0, dev)
+    return out
+
+
+def _same(a, b):
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("B", [1, 5, 8, 37, 256])
+def test_enc512_matches_two_kernel_path(setup, B):
+    ref = _run(setup, B, 0, seed=11)
+    _same(_run(setup, B, 1, seed=11), ref)
+
+
+@pytest.mark.parametrize("grid,B", [(1, 6), (3, 13), (24, 40)])
+def test_enc512_small_grids(setup, grid, B):
+    ref = _run(setup, B, 0, seed=12)
+    _same(_run(setup, B, 1, grid=grid, seed=12), ref)
+
+
+def test_enc512_full_batch_repeat(setup):
+    """the bench geometry, twice back to back (sync words re-zeroed per call)"""
+    ref = _run(setup, 1024, 0, seed=13)
+    _same(_run(setup, 1024, 1, seed=13), ref)
+    _same(_run(setup, 1024, 1, seed=13), ref)
