@@ -76,6 +76,8 @@ def kernel_models(h, w, p, maxp, ncb, s, images_per_row):
         "gemm_cols": ("mfma", 3 * 2.0 * kh * kw * h, "flop"),
         "fft_rows": ("hbm", 12 * h * w + inter, "B"),            # RGB in, T out
         "fft_cols": ("hbm", inter + stage, "B"),                  # T in, token staging out
+        # persistent rows + columns (k_enc512): RGB in, token staging out; T stays on chip
+        "enc512": ("hbm", 12 * h * w + stage, "B"),
         "tile_epilogue": ("hbm", 12 * kh * kw + stage, "B"),
         "sort_pack": ("hbm", stage + t * (8 * ncb + 32) + s / images_per_row, "B"),
         "pad_fill": ("hbm", s / images_per_row, "B"),
@@ -115,6 +117,29 @@ def cpu_baseline(size, seconds, pn_tables, threads):
             "sample": f"{n} images of {size}x{size} (torch.rand) through oracle/ref_cpu.encode: preprocess "
                       f"(FFT DCT, sort) + iter_batches (attn_mask built) + PatchNorm + LFQ, {el:.1f} s",
             "calibration": cpu_calibration()}
+
+
+def cpu_config1(threads, reps=10, size=224):
+    """BASELINE config 1: one 224x224 image through the reference's CPU round
+    trip (FE:154-310: preprocess -> iter_batches(None) -> postprocess, DCT then
+    IDCT) on the oracle port, median of ``reps`` runs."""
+    from oracle import ref_cpu
+    torch.set_num_threads(threads)
+    cfg = ref_cpu.FEConfig()
+    x = torch.rand(3, size, size, generator=torch.Generator().manual_seed(1))
+    times, err = [], 0.0
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        item = ref_cpu.preprocess(x, cfg)
+        (batch,) = list(ref_cpu.iter_batches(iter([{k: [v] for k, v in item.items()}]), cfg, None))
+        (y,) = ref_cpu.postprocess(batch, cfg)
+        times.append(time.perf_counter() - t0)
+        err = float((y - x).abs().max())
+    times = sorted(times[1:])   # the first run warms the allocator / thread pool
+    med = times[len(times) // 2]
+    return {"workload": f"config 1: one {size}x{size} image, preprocess -> iter_batches -> postprocess "
+                        "(DCT -> IDCT round trip) on the CPU port", "median_ms": round(med * 1e3, 3),
+            "reps": reps, "cores": threads, "kind": "port", "roundtrip_max_abs_err": err}
 
 
 def stats_fit_leg(pkg, fe, dev, rank, world, dist, steps, n_img=8, size=512):
@@ -538,6 +563,7 @@ def main():
         tables = ref_cpu.NormTables(torch.from_numpy(tabs["n"]), torch.from_numpy(tabs["median"]),
                                     torch.from_numpy(tabs["b"]))
         cpu = cpu_baseline(H, args.cpu_seconds, tables, threads)
+        cpu["config1"] = cpu_config1(threads)
 
     if rank == 0:
         line = {

@@ -45,7 +45,7 @@ constexpr int kSlots = 3;                        // T slots per XCD
 constexpr int kKW = 448, kH = 512;
 constexpr int64_t kSlotFloats = 3ll * kH * kKW;  // one image's T
 constexpr unsigned kNone = 0x7fffffffu;          // published "no image" (claims start at 1)
-constexpr unsigned kSpinMax = 1u << 22;
+constexpr uint64_t kSpinTicks = 50000000ull;    // bounded waits: 0.5 s of s_memrealtime (100 MHz)
 
 // sync block (unsigned words, zeroed per call): [0] image claim counter,
 // [32 (x + 1)] head of XCD x (own 128-byte lines), then
@@ -71,15 +71,31 @@ __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one lane: poll *p until pred holds (bounded; false on time out)
+// one lane: poll *p until pred holds (bounded in wall time; false on time out)
 template <class Pred>
 __device__ __forceinline__ bool spin_until(const unsigned* p, Pred pred, unsigned& v) {
-  for (unsigned it = 0; it < kSpinMax; ++it) {
+  v = ld_agent(p);
+  if (pred(v)) return true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    __builtin_amdgcn_s_sleep(2);
     v = ld_agent(p);
     if (pred(v)) return true;
-    __builtin_amdgcn_s_sleep(2);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) return false;
   }
-  return false;
+}
+
+// queue position -> (row item?, segment of its image k, item index i)
+__device__ __forceinline__ void decode_pos(int p, bool& is_row, int& k, int& i) {
+  if (p < kRowItems) {
+    is_row = true, k = 0, i = p;
+    return;
+  }
+  const int q = p - kRowItems, r = q % kSeg;
+  k = q / kSeg + 1;
+  is_row = r < kRowItems;
+  i = is_row ? r : r - kRowItems;
+  if (!is_row) k -= 1;   // C items of segment k serve image k - 1
 }
 
 }  // namespace
@@ -115,18 +131,9 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
   for (;;) {
     __syncthreads();   // tables (first pass); the previous item's LDS use is over
     const int p = L.item[0];
-    // decode the position: R(k, i) or C(k, t)
     bool is_row;
     int k, i;
-    if (p < kRowItems) {
-      is_row = true, k = 0, i = p;
-    } else {
-      const int q = p - kRowItems, r = q % kSeg;
-      k = q / kSeg + 1;
-      is_row = r < kRowItems;
-      i = is_row ? r : r - kRowItems;
-      if (!is_row) k -= 1;
-    }
+    decode_pos(p, is_row, k, i);
     if (tid == 0) {
       // take the next position now: the atomic's latency hides behind this item
       L.item[1] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -166,6 +173,10 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
       if (!ok) {
         atomicOr(err, 32);
         L.item[3] = 1;
+        printf("k_enc512 wait timed out: xcc %d block %d pos %d (%s k %d i %d) img %u rdone %u cdone %u claim %u\n",
+               x, (int)blockIdx.x, p, is_row ? "R" : "C", k, i, img,
+               img != kNone && img ? ld_agent(rdone + img - 1) : 0u, img != kNone && img ? ld_agent(cdone + img - 1) : 0u,
+               ld_agent(sync));
       }
       L.item[2] = (int)img;
     }
@@ -173,8 +184,19 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
     if (L.item[3]) return;   // a hand-off timed out (error bit 32)
     const unsigned img = (unsigned)L.item[2];
     if (img == kNone) {
-      // a column item without an image: every later position is empty too
-      if (!is_row) return;
+      // a column item without an image: every later position is empty too.
+      // The taken-ahead item is later; if it is a segment's claim (R(k', 0))
+      // others wait for its publication: publish "no image" (claims are
+      // monotone, so that is what the claim would give) before leaving.
+      if (!is_row) {
+        if (tid == 0) {
+          bool r2;
+          int k2, i2;
+          decode_pos(L.item[1], r2, k2, i2);
+          if (r2 && i2 == 0 && k2 < max_seg) __hip_atomic_store(img_tab + k2, kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
     } else {
       const int n = (int)img - 1;
       const ImgDesc d = imgs[n];
