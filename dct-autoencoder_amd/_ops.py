@@ -461,7 +461,8 @@ def dct2(x: torch.Tensor, inverse: bool, color: bool) -> torch.Tensor:
     ctx = _lib.context(dev)
     y = torch.empty_like(xb)
     B, _, H, W = xb.shape
-    rc = ctx.lib.dctae_dct2(ctx.h, ptr(xb), B, H, W, int(bool(inverse)), int(bool(color)), ptr(y),
+    color = int(color) if not isinstance(color, bool) else int(color)   # 0 / 1, or 2 / 3: fp16 / bf16 colour
+    rc = ctx.lib.dctae_dct2(ctx.h, ptr(xb), B, H, W, int(bool(inverse)), color, ptr(y),
                             _lib.stream_ptr(dev))
     ctx.check(rc, "dctae_dct2")
     return y[0] if one else y

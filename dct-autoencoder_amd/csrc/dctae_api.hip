@@ -1421,6 +1421,8 @@ int dctae_dct2(dctae_ctx* ctx, const float* x, int32_t n_img, int32_t H, int32_t
   if (!ctx) return DCTAE_EINVAL;
   hipSetDevice(ctx->device);
   if (n_img < 0 || H < 1 || W < 1 || (direction != 0 && direction != 1)) return fail(ctx, DCTAE_EINVAL, "bad dct2 shape");
+  if (color < 0 || color > 3 || (color > 1 && direction != 0))
+    return fail(ctx, DCTAE_EINVAL, "dct2 color: 0 none, 1 fp32, 2 / 3 fp16 / bf16 arithmetic (forward only)");
   if (n_img == 0) return 0;
   if (!x || !y || x == y) return fail(ctx, DCTAE_EINVAL, "dct2 needs distinct input / output buffers");
   hipStream_t s = (hipStream_t)stream;
@@ -1463,7 +1465,7 @@ int dctae_dct2(dctae_ctx* ctx, const float* x, int32_t n_img, int32_t H, int32_t
   uint8_t* pd = ctx->plan_dev;
   if (direction == 0 && color) {
     Timer t(ctx, s, "rgb_to_ipt");
-    launch_color(x, a, hw, n_img, 0, ctx->cm, s);
+    launch_color(x, a, hw, n_img, color >= 2 ? color : 0, ctx->cm, s);
   }
   {
     Timer t(ctx, s, "dct2_gemm");

@@ -13,18 +13,23 @@
 // nothing depends on how the dispatcher places blocks (an XCD without blocks
 // simply claims no images).
 //
-// Queue of XCD x (positions from its head counter):
-//   segment 0:        R(0) x 32
-//   segment k >= 1:   R(k) x 32, then C(k - 1) x 96
-// Segment k's image is claimed from the global image counter by the block
-// that takes R(k) item 0, after segment k - 1's claim is published (so
+// Queue of XCD x (positions from its head counter), L = kLag:
+//   segments 0 .. L - 1:   R(k) x 32
+//   segment k >= L:        R(k) x 32, then C(k - L) x 96
+// Segment k's image is claimed from the global image counter kAhead segments
+// early, by the block that takes R(k - kAhead) item 0 (R(0, 0) claims
+// segments 0 .. kAhead), each claim after segment k - 1's is published (so
 // claims are monotone in k: once a segment gets no image, no later one does).
-// T slot of segment k: k % 3 (of 3 per XCD).  Waits (every one on an item at
-// a LOWER queue position, so the lowest unfinished item can always run: no
-// deadlock, whatever the residency; a block holds at most one taken-ahead
-// item, which is never lower than its current one):
-//   R(k)     waits for C(k - 3) done (its slot's previous reader);
-//   C(k - 1) waits for R(k - 1) done (all 32 row items of its image).
+// Claiming at use instead stalled the segment's 31 other row items behind
+// the claimer's previous item.
+// L images are in flight per XCD: one image's rows alone take a block's item
+// time (~26 us), so column items of the image just finished would wait.
+// T slot of segment k: k % S (S = L + 2 per XCD).  Waits (every one on an
+// item at a LOWER queue position, so the lowest unfinished item can always
+// run: no deadlock, whatever the residency; a block holds at most one
+// taken-ahead item, which is never lower than its current one):
+//   R(k)     waits for C(k - S) done (its slot's previous reader);
+//   C(k)     waits for R(k) done (all 32 row items of its image).
 // Hand-off (same XCD, one L2): producer plain T stores -> every wave
 // s_waitcnt vmcnt(0) -> barrier -> one agent-scope atomic add; consumer polls
 // the counter with relaxed agent-scope (sc1) loads and reads T with sc1 buffer
@@ -41,7 +46,12 @@ namespace {
 constexpr int kRowItems = 32;                    // 16-row items per image
 constexpr int kColItems = 96;                    // (channel, tile column) items per image
 constexpr int kSeg = kRowItems + kColItems;
-constexpr int kSlots = 3;                        // T slots per XCD
+#ifndef DCTAE_ENC_LAG
+#define DCTAE_ENC_LAG 2
+#endif
+constexpr int kLag = DCTAE_ENC_LAG;              // column items of image k follow the row items of image k + kLag
+constexpr int kSlots = kLag + 2;                 // T slots per XCD
+constexpr int kAhead = 2;                        // R(k, 0) claims the image of segment k + kAhead
 constexpr int kKW = 448, kH = 512;
 constexpr int64_t kSlotFloats = 3ll * kH * kKW;  // one image's T
 constexpr unsigned kNone = 0x7fffffffu;          // published "no image" (claims start at 1)
@@ -87,16 +97,24 @@ __device__ __forceinline__ bool spin_until(const unsigned* p, Pred pred, unsigne
 
 // queue position -> (row item?, segment of its image k, item index i)
 __device__ __forceinline__ void decode_pos(int p, bool& is_row, int& k, int& i) {
-  if (p < kRowItems) {
-    is_row = true, k = 0, i = p;
+  if (p < kLag * kRowItems) {
+    is_row = true, k = p / kRowItems, i = p % kRowItems;
     return;
   }
-  const int q = p - kRowItems, r = q % kSeg;
-  k = q / kSeg + 1;
+  const int q = p - kLag * kRowItems, r = q % kSeg;
+  k = q / kSeg + kLag;
   is_row = r < kRowItems;
   i = is_row ? r : r - kRowItems;
-  if (!is_row) k -= 1;   // C items of segment k serve image k - 1
+  if (!is_row) k -= kLag;   // C items of segment k serve image k - kLag
 }
+
+#ifdef DCTAE_ENC_STATS
+// profiling builds (-DDCTAE_ENC_STATS): per-XCD item timing, printed by the
+// last block to leave: [0] blocks [1] row items [2] column items [3] wait
+// ticks [4] row ticks [5] column ticks [6] block lifetime ticks (100 MHz)
+__device__ unsigned long long g_enc_st[8][8];
+__device__ unsigned g_enc_st_left;
+#endif
 
 }  // namespace
 
@@ -128,8 +146,16 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
     L.item[0] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     L.item[3] = 0;
   }
+#ifdef DCTAE_ENC_STATS
+  unsigned long long st[8] = {1, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long t_born = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_a = 0, t_b = 0;
+#endif
   for (;;) {
     __syncthreads();   // tables (first pass); the previous item's LDS use is over
+#ifdef DCTAE_ENC_STATS
+    if (tid == 0) t_a = __builtin_amdgcn_s_memrealtime();
+#endif
     const int p = L.item[0];
     bool is_row;
     int k, i;
@@ -139,35 +165,40 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
       L.item[1] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       unsigned img = kNone;
       bool ok = true;
-      if (k >= max_seg) {
-        img = kNone;
-      } else if (is_row && i == 0) {
-        // claim segment k's image once segment k - 1's claim is published
-        unsigned prev = 1;
-        if (k > 0) ok = spin_until(img_tab + k - 1, [](unsigned v) { return v != 0u; }, prev);
-        if (ok) {
-          if (prev == kNone) {
-            img = kNone;
-          } else {
+      if (is_row && i == 0) {
+        // claims run kAhead segments ahead of their use (R(0, 0) claims
+        // segments 0 .. kAhead), each after the previous one is published
+        for (int kc = k == 0 ? 0 : k + kAhead; ok && kc <= k + kAhead && kc < max_seg; ++kc) {
+          unsigned prev = 1, got = kNone;
+          if (kc > 0) ok = spin_until(img_tab + kc - 1, [](unsigned v) { return v != 0u; }, prev);
+          if (ok && prev != kNone) {
             const unsigned n = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            img = n < (unsigned)n_img ? n + 1 : kNone;
+            got = n < (unsigned)n_img ? n + 1 : kNone;
           }
-          __hip_atomic_store(img_tab + k, img, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (ok) __hip_atomic_store(img_tab + kc, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-      } else {
-        ok = spin_until(img_tab + k, [](unsigned v) { return v != 0u; }, img);
+      }
+      if (ok) {
+        if (k >= max_seg) img = kNone;
+        else ok = spin_until(img_tab + k, [](unsigned v) { return v != 0u; }, img);
       }
       if (ok && img != kNone) {
         const unsigned n = img - 1;
         unsigned v;
+#ifdef DCTAE_ENC_NOWAIT
+        if (false) {   // profiling build: no dependency waits (wrong outputs)
+#else
         if (is_row) {
-          // the slot's previous reader: segment k - 3's 96 column items
+#endif
+          // the slot's previous reader: segment k - S's 96 column items
           if (k >= kSlots) {
             const unsigned pimg = ld_agent(img_tab + k - kSlots);   // published (earlier claim)
             if (pimg != kNone) ok = spin_until(cdone + (pimg - 1), [](unsigned c) { return c >= (unsigned)kColItems; }, v);
           }
         } else {
+#ifndef DCTAE_ENC_NOWAIT
           ok = spin_until(rdone + n, [](unsigned c) { return c >= (unsigned)kRowItems; }, v);
+#endif
         }
       }
       if (!ok) {
@@ -181,7 +212,13 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
       L.item[2] = (int)img;
     }
     __syncthreads();
-    if (L.item[3]) return;   // a hand-off timed out (error bit 32)
+#ifdef DCTAE_ENC_STATS
+    if (tid == 0) {
+      t_b = __builtin_amdgcn_s_memrealtime();
+      st[3] += t_b - t_a;
+    }
+#endif
+    if (L.item[3]) break;   // a hand-off timed out (error bit 32)
     const unsigned img = (unsigned)L.item[2];
     if (img == kNone) {
       // a column item without an image: every later position is empty too.
@@ -193,9 +230,10 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
           bool r2;
           int k2, i2;
           decode_pos(L.item[1], r2, k2, i2);
-          if (r2 && i2 == 0 && k2 < max_seg) __hip_atomic_store(img_tab + k2, kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (r2 && i2 == 0 && k2 + kAhead < max_seg)
+            __hip_atomic_store(img_tab + k2 + kAhead, kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        return;
+        break;
       }
     } else {
       const int n = (int)img - 1;
@@ -216,13 +254,39 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
         __syncthreads();   // every wave's T loads have returned (their values were used)
         if (tid == 0) __hip_atomic_fetch_add(cdone + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+#ifdef DCTAE_ENC_STATS
+      if (tid == 0) {
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_b;
+        st[is_row ? 1 : 2] += 1;
+        st[is_row ? 4 : 5] += dt;
+      }
+#endif
     }
     if (tid == 0) L.item[0] = L.item[1];
   }
+#ifdef DCTAE_ENC_STATS
+  if (tid == 0) {
+    st[6] = __builtin_amdgcn_s_memrealtime() - t_born;
+    for (int e = 0; e < 7; ++e) atomicAdd(&g_enc_st[x][e], st[e]);
+    __threadfence();
+    if (atomicAdd(&g_enc_st_left, 1u) == gridDim.x - 1) {
+      __threadfence();
+      for (int xx = 0; xx < 8; ++xx) {
+        unsigned long long v[7];
+        for (int e = 0; e < 7; ++e) v[e] = atomicExch(&g_enc_st[xx][e], 0ull);
+        const double b = v[0] ? (double)v[0] : 1.0;
+        printf("enc512 xcd %d: blocks %llu rows %llu (%.1f us) cols %llu (%.1f us) wait/item %.2f us life/block %.1f us\n",
+               xx, v[0], v[1], v[1] ? v[4] / 100.0 / v[1] : 0.0, v[2], v[2] ? v[5] / 100.0 / v[2] : 0.0,
+               (v[1] + v[2]) ? v[3] / 100.0 / (double)(v[1] + v[2]) : 0.0, v[6] / 100.0 / b);
+      }
+      atomicExch(&g_enc_st_left, 0u);
+    }
+  }
+#endif
 }
 
 size_t enc512_sync_words(int n_img) {
-  const int max_seg = n_img + 2;
+  const int max_seg = n_img + kLag + kAhead + 2;
   return (size_t)kImgBase + (size_t)8 * max_seg + 2 * (size_t)n_img;
 }
 
@@ -250,7 +314,7 @@ void launch_enc512(const ImgDesc* imgs, int n_img, const float* rgb, float* tslo
   if (n_img <= 0) return;
   hipMemsetAsync(sync, 0, enc512_sync_words(n_img) * sizeof(unsigned), s);
   hipLaunchKernelGGL(k_enc512, dim3(grid), dim3(256), 0, s, imgs, n_img, rgb, tslots, tw, post, cm, ep, sk, sync,
-                     n_img + 2, err);
+                     n_img + kLag + kAhead + 2, err);
 }
 
 }  // namespace dctae

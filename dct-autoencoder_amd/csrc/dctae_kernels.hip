@@ -10,6 +10,8 @@
 #include "dctae_internal.h"
 #include "dctae_launch.h"
 
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <rocprim/block/block_radix_sort.hpp>
 #include "dctae_device.h"
 
@@ -197,10 +199,59 @@ __global__ void k_color(const float* __restrict__ x, float* __restrict__ y, int6
   }
 }
 
+// rgb_to_ipt of an fp16 / bf16 image the way the reference runs it in the
+// input dtype (FE:135 calls util.rgb_to_ipt before x.float()): the matrices
+// rounded to the dtype (Trgb2lms.to(x.dtype), Mipt.to(x.dtype)), each einsum
+// accumulated in fp32 and rounded once (torch CPU einsum), the exponent 0.43
+// rounded to the dtype and |x|**g computed in fp32 then rounded (torch CPU
+// pow of a half / bfloat16 tensor), util.py:56-82.  x holds the dtype's values
+// exactly as fp32; y: the dtype-rounded IPT values as fp32.
+template <int LOWP>   // 2: fp16, 3: bf16
+__device__ __forceinline__ float round_lowp(float v) {
+  if (LOWP == 2) return __half2float(__float2half_rn(v));
+  return __bfloat162float(__float2bfloat16(v));
+}
+
+template <int LOWP>
+__global__ void k_color_lowp(const float* __restrict__ x, float* __restrict__ y, int64_t hw, int n_img, ColorMats cm) {
+  float m1[9], m2[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    m1[i] = round_lowp<LOWP>(cm.rgb2lms[i]);
+    m2[i] = round_lowp<LOWP>(cm.lms2ipt[i]);
+  }
+  const float g = round_lowp<LOWP>(0.430000007152557373046875f);
+  const int64_t n = hw * n_img;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / hw, p = e - i * hw;
+    const float* s = x + 3 * hw * i + p;
+    float* d = y + 3 * hw * i + p;
+    const float a = s[0], b = s[hw], c = s[2 * hw];
+    float l[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      // fp32 products of dtype values are exact; sum in j order, one rounding
+      const float v = round_lowp<LOWP>(__fadd_rn(__fadd_rn(__fmul_rn(m1[3 * r], a), __fmul_rn(m1[3 * r + 1], b)),
+                                                 __fmul_rn(m1[3 * r + 2], c)));
+      const float pw = round_lowp<LOWP>(powf(fabsf(v), g));
+      l[r] = v < 0.0f ? -pw : pw;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      d[r * hw] = round_lowp<LOWP>(__fadd_rn(__fadd_rn(__fmul_rn(m2[3 * r], l[0]), __fmul_rn(m2[3 * r + 1], l[1])),
+                                             __fmul_rn(m2[3 * r + 2], l[2])));
+  }
+}
+
 void launch_color(const float* x, float* y, int64_t hw, int n_img, int dir, const ColorMats& cm, hipStream_t s) {
   const int64_t n = hw * n_img;
   const int g = (int)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_color, dim3(std::max(g, 1)), dim3(256), 0, s, x, y, hw, n_img, dir, cm);
+  if (dir == 2)
+    hipLaunchKernelGGL(k_color_lowp<2>, dim3(std::max(g, 1)), dim3(256), 0, s, x, y, hw, n_img, cm);
+  else if (dir == 3)
+    hipLaunchKernelGGL(k_color_lowp<3>, dim3(std::max(g, 1)), dim3(256), 0, s, x, y, hw, n_img, cm);
+  else
+    hipLaunchKernelGGL(k_color, dim3(std::max(g, 1)), dim3(256), 0, s, x, y, hw, n_img, dir, cm);
 }
 
 // ---------------------------------------------------------------------------

@@ -106,8 +106,11 @@ class DCTAutoencoderFeatureExtractor:
     @torch.no_grad()
     def _transform_image_in(self, x: torch.Tensor) -> torch.Tensor:
         """FE:129-142: rgb_to_ipt, then the orthonormal dct2 of the whole
-        (c, h, w) image (dctae_dct2); result in x's dtype and on x's device."""
-        y = _ops.dct2(self._dev(x).float(), inverse=False, color=True)
+        (c, h, w) image (dctae_dct2); result in x's dtype and on x's device.
+        The reference runs rgb_to_ipt in the input's dtype before ``.float()``:
+        fp16 / bf16 inputs get that arithmetic (dctae_dct2 color 2 / 3)."""
+        color = {torch.float16: 2, torch.bfloat16: 3}.get(x.dtype, 1)
+        y = _ops.dct2(self._dev(x).float(), inverse=False, color=color)
         return y.to(x.dtype).to(x.device)
 
     def _transform_image_out(self, x: torch.Tensor) -> torch.Tensor:
@@ -140,6 +143,7 @@ class DCTAutoencoderFeatureExtractor:
         assert c == self.channels
         k = self._k(h, w)
         patches, pos, channels = _ops.patch_spectrum(self._dev(x), self.params(), k)
+        patches = patches.to(x.dtype)   # the reference's patches keep the spectrum's dtype
         s, z = patches.shape
         assert z == P ** 2, f"{z} != {P ** 2}"
         assert s <= self.max_seq_len
@@ -170,7 +174,9 @@ class DCTAutoencoderFeatureExtractor:
     @torch.no_grad()
     def preprocess_many(self, images: Sequence[torch.Tensor]) -> List[Dict[str, Any]]:
         """``preprocess`` for several images in one launch sequence."""
-        if self._staged_in():
+        if self._staged_in() or any(im.dtype != torch.float32 for im in images):
+            # fp16 / bf16 images: the reference's stage sequence, whose colour
+            # transform runs in the input dtype (FE:135-141)
             return [self._preprocess_staged(im) for im in images]
         images = [self._dev(im) for im in images]
         for im in images:

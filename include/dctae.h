@@ -141,7 +141,10 @@ int dctae_spectrum_tokens(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_i
 /* FE._transform_image_in / _transform_image_out (FE:129-152) on n_img
  * contiguous (3, H, W) fp32 images: direction 0 = dct2(rgb_to_ipt(x)),
  * direction 1 = ipt_to_rgb(idct2(x)); color = 0 skips the colour transform
- * (util.dct2 / util.idct2 alone, util.py:333-338).  Orthonormal DCT-II / III
+ * (util.dct2 / util.idct2 alone, util.py:333-338); forward only: color = 2 / 3
+ * runs rgb_to_ipt in fp16 / bf16 arithmetic, as the reference does for an
+ * input of that dtype (FE:135 transforms before x.float()), x then holding
+ * the dtype's values as fp32.  Orthonormal DCT-II / III
  * over the whole H x W (no crop).  x_dev and y_dev must not alias. */
 int dctae_dct2(dctae_ctx* ctx, const float* x_dev, int32_t n_img, int32_t H, int32_t W, int32_t direction,
                int32_t color, float* y_dev, void* stream);

@@ -241,8 +241,9 @@ def patch_image(x: torch.Tensor, cfg: FEConfig, rng=random, stable: bool = True)
 
 
 def transform_image_in(im: torch.Tensor) -> torch.Tensor:
-    """FE:129-142: rgb -> ipt -> dct2 (fp32, CPU)."""
-    return dct2(rgb_to_ipt(im.float()))
+    """FE:129-142: rgb -> ipt in the input's dtype (FE:135), then .float(),
+    dct2 (fp32, CPU) and back to the input's dtype (FE:139-141)."""
+    return dct2(rgb_to_ipt(im).float()).to(im.dtype)
 
 
 def transform_image_out(x: torch.Tensor) -> torch.Tensor:

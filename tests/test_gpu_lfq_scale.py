@@ -153,3 +153,20 @@ def test_model_lfq_scale(pkg, si):
     torch.cuda.synchronize()
     assert torch.equal(codes.cpu().view(1, m, 14), torch.from_numpy(G[f"n{si}_idx"])), s
     assert torch.equal(xq.cpu().view(1, m, 196), torch.from_numpy(G[f"n{si}_q"])), s
+
+
+@pytest.mark.parametrize("dim", [None, 24])
+def test_large_codebook_codes_are_float(pkg, dim):
+    """codebook_size > 2**16 (no materialised codebook buffer): indices_to_codes
+    keeps the float codebook dtype (lfq.py:101-124), so a non-integer scale
+    survives and project_out (dim 24 != 17) gets a float tensor."""
+    m = pkg.LFQ(dim=dim, codebook_size=2 ** 17, codebook_scale=0.5).to(DEV).eval()
+    assert not hasattr(m, "codebook") and m.dtype == torch.float32
+    idx = torch.tensor([[0, 1, 2 ** 17 - 1, 12345]], device=DEV)
+    codes = m.indices_to_codes(idx, project_out=False)
+    assert codes.dtype == torch.float32
+    bits = ((idx[..., None] & (2 ** torch.arange(16, -1, -1, device=DEV))) != 0).float()
+    assert torch.equal(codes, bits * 0.5 * 2 - 0.5)
+    if dim is not None:
+        out = m.indices_to_codes(idx)
+        assert out.dtype == torch.float32 and out.shape == (1, 4, dim)

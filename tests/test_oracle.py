@@ -240,3 +240,15 @@ def test_lfq_scale_rule_matches_reference(proj):
         assert torch.equal(idx, torch.from_numpy(g[f"{tag}{si}_idx"])), s
         torch.testing.assert_close(q, torch.from_numpy(g[f"{tag}{si}_q"]), rtol=0, atol=0, equal_nan=True)
         torch.testing.assert_close(codes, torch.from_numpy(g[f"{tag}{si}_codes"]), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("tag,dt", [("f16", torch.float16), ("bf16", torch.bfloat16)])
+def test_low_precision_colour_matches_reference(tag, dt):
+    """FE:135-141 on fp16 / bf16 inputs: rgb_to_ipt in the input dtype, then
+    .float() + dct2 + cast back.  The oracle's IPT stage is bit-exact with the
+    reference's; the spectrum equals it (same fp32 DCT restatement)."""
+    g = golden("color_dtype_ref.npz")
+    for i in range(2):
+        x = torch.from_numpy(g[f"{tag}_{i}_x"]).to(dt)
+        assert torch.equal(ref_cpu.rgb_to_ipt(x).float(), torch.from_numpy(g[f"{tag}_{i}_ipt"]))
+        assert torch.equal(ref_cpu.transform_image_in(x).float(), torch.from_numpy(g[f"{tag}_{i}_spec"]))
