@@ -79,8 +79,10 @@ struct dctae_ctx {
   int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
   int n_cu = 256;
   // persistent XCD-local 512^2 encode (dctae_enc512.hip): T slots and the
-  // per-call sync words (grow-only); enc512 = 0 selects the two-kernel path
-  int enc512 = 1;
+  // per-call sync words (grow-only).  Off by default: measured slower than
+  // the two-kernel path and a wrong-code race under 3
+  // workgroups per CU is not yet explained; enc512 = 1 selects it
+  int enc512 = 0;
   float* enc_slots = nullptr;
   unsigned* enc_sync = nullptr;
   size_t enc_sync_words = 0;

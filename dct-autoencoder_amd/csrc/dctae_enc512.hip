@@ -52,6 +52,15 @@ constexpr int kSeg = kRowItems + kColItems;
 constexpr int kLag = DCTAE_ENC_LAG;              // column items of image k follow the row items of image k + kLag
 constexpr int kSlots = kLag + 2;                 // T slots per XCD
 constexpr int kAhead = 2;                        // R(k, 0) claims the image of segment k + kAhead
+#ifndef DCTAE_ENC_PREL
+#define DCTAE_ENC_PREL 0                         // producer agent-scope release before the row-done add
+#endif
+#ifndef DCTAE_ENC_CACQ
+#define DCTAE_ENC_CACQ 0                         // consumer agent-scope acquire after the row-done poll
+#endif
+#ifndef DCTAE_ENC_RESERVE
+#define DCTAE_ENC_RESERVE 1                      // take the next position while the current item runs
+#endif
 constexpr int kKW = 448, kH = 512;
 constexpr int64_t kSlotFloats = 3ll * kH * kKW;  // one image's T
 constexpr unsigned kNone = 0x7fffffffu;          // published "no image" (claims start at 1)
@@ -78,7 +87,11 @@ struct EncLds {
 };
 
 __device__ __forceinline__ unsigned ld_agent(const unsigned* p) {
+#ifdef DCTAE_ENC_RMWPOLL
+  return __hip_atomic_fetch_add(const_cast<unsigned*>(p), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // one lane: poll *p until pred holds (bounded in wall time; false on time out)
@@ -108,13 +121,54 @@ __device__ __forceinline__ void decode_pos(int p, bool& is_row, int& k, int& i) 
   if (!is_row) k -= kLag;   // C items of segment k serve image k - kLag
 }
 
+#ifdef DCTAE_ENC_CHECK
+// debug builds: protocol invariants (claims per image, slot owners)
+__device__ unsigned g_chk_claims[1 << 16];
+__device__ unsigned g_chk_owner[8][8];
+__device__ unsigned g_chk_bad[4];
+#endif
+
 #ifdef DCTAE_ENC_STATS
 // profiling builds (-DDCTAE_ENC_STATS): per-XCD item timing, printed by the
 // last block to leave: [0] blocks [1] row items [2] column items [3] wait
-// ticks [4] row ticks [5] column ticks [6] block lifetime ticks (100 MHz)
+// ticks [4] row ticks [5] column ticks [6] block lifetime ticks [7] row-item wait
+// ticks (100 MHz)
 __device__ unsigned long long g_enc_st[8][8];
 __device__ unsigned g_enc_st_left;
 #endif
+
+// take the next queue position of XCD x (one lane).  A position that is a
+// segment's first row item R(k, 0) claims the image of segment k + kAhead
+// right here (R(0, 0): segments 0 .. kAhead), after segment k + kAhead - 1's
+// claim is published -- by whoever took R(k - 1, 0), also at its take, so the
+// claim chain advances at dequeue speed and never waits on item processing.
+// false: a wait timed out.
+__device__ __forceinline__ bool take_pos(unsigned* head, unsigned* sync, unsigned* img_tab, int n_img, int max_seg,
+                                         int& p) {
+  p = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool is_row;
+  int k, i;
+  decode_pos(p, is_row, k, i);
+  if (!is_row || i != 0) return true;
+  for (int kc = k == 0 ? 0 : k + kAhead; kc <= k + kAhead && kc < max_seg; ++kc) {
+    unsigned prev = 1, got = kNone;
+    if (kc > 0 && !spin_until(img_tab + kc - 1, [](unsigned v) { return v != 0u; }, prev)) return false;
+    if (prev != kNone) {
+      const unsigned n = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      got = n < (unsigned)n_img ? n + 1 : kNone;
+#ifdef DCTAE_ENC_CHECK
+      if (got != kNone) printf("CLAIM %u %u %d %u\n", n, (unsigned)(head - sync) / kHeadBase - 1, kc,
+                               __builtin_amdgcn_s_getreg((3 << 11) | 20));
+      if (got != kNone && atomicAdd(&g_chk_claims[n], 1u) != 0) {
+        atomicAdd(&g_chk_bad[0], 1u);
+        printf("CHK double claim image %u seg %d\n", n, kc);
+      }
+#endif
+    }
+    __hip_atomic_store(img_tab + kc, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
 
 }  // namespace
 
@@ -133,7 +187,11 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
   }
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+#ifdef DCTAE_ENC_ONEQ
+  const int x = 0 * (int)(xcc & 7);   // debug: one queue for the whole chip (needs the agent fences)
+#else
   const int x = (int)(xcc & 7);
+#endif
   unsigned* head = sync + kHeadBase * (x + 1);
   unsigned* img_tab = sync + kImgBase + (size_t)x * max_seg;
   unsigned* rdone = sync + kImgBase + (size_t)8 * max_seg;
@@ -143,8 +201,9 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
   // item state in LDS: [0] current position, [1] the taken-ahead position,
   // [2] image of the current item (or kNone), [3] abort flag
   if (tid == 0) {
-    L.item[0] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    L.item[3] = 0;
+    int p0;
+    L.item[3] = take_pos(head, sync, img_tab, n_img, max_seg, p0) ? 0 : 1;
+    L.item[0] = p0;
   }
 #ifdef DCTAE_ENC_STATS
   unsigned long long st[8] = {1, 0, 0, 0, 0, 0, 0, 0};
@@ -160,24 +219,17 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
     bool is_row;
     int k, i;
     decode_pos(p, is_row, k, i);
-    if (tid == 0) {
-      // take the next position now: the atomic's latency hides behind this item
-      L.item[1] = (int)__hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && !L.item[3]) {
       unsigned img = kNone;
       bool ok = true;
-      if (is_row && i == 0) {
-        // claims run kAhead segments ahead of their use (R(0, 0) claims
-        // segments 0 .. kAhead), each after the previous one is published
-        for (int kc = k == 0 ? 0 : k + kAhead; ok && kc <= k + kAhead && kc < max_seg; ++kc) {
-          unsigned prev = 1, got = kNone;
-          if (kc > 0) ok = spin_until(img_tab + kc - 1, [](unsigned v) { return v != 0u; }, prev);
-          if (ok && prev != kNone) {
-            const unsigned n = __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            got = n < (unsigned)n_img ? n + 1 : kNone;
-          }
-          if (ok) __hip_atomic_store(img_tab + kc, got, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+#if DCTAE_ENC_RESERVE
+      // take the next position now: the atomic's latency hides behind this item
+      {
+        int pn;
+        ok = take_pos(head, sync, img_tab, n_img, max_seg, pn);
+        L.item[1] = pn;
       }
+#endif
       if (ok) {
         if (k >= max_seg) img = kNone;
         else ok = spin_until(img_tab + k, [](unsigned v) { return v != 0u; }, img);
@@ -204,46 +256,70 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
       if (!ok) {
         atomicOr(err, 32);
         L.item[3] = 1;
+#ifdef DCTAE_ENC_DEBUG
         printf("k_enc512 wait timed out: xcc %d block %d pos %d (%s k %d i %d) img %u rdone %u cdone %u claim %u\n",
                x, (int)blockIdx.x, p, is_row ? "R" : "C", k, i, img,
                img != kNone && img ? ld_agent(rdone + img - 1) : 0u, img != kNone && img ? ld_agent(cdone + img - 1) : 0u,
                ld_agent(sync));
+#endif
       }
       L.item[2] = (int)img;
+#if DCTAE_ENC_CACQ
+      if (!is_row && ok && img != kNone) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+#endif
     }
     __syncthreads();
 #ifdef DCTAE_ENC_STATS
     if (tid == 0) {
       t_b = __builtin_amdgcn_s_memrealtime();
       st[3] += t_b - t_a;
+      if (is_row) st[7] += t_b - t_a;
     }
 #endif
     if (L.item[3]) break;   // a hand-off timed out (error bit 32)
     const unsigned img = (unsigned)L.item[2];
     if (img == kNone) {
-      // a column item without an image: every later position is empty too.
-      // The taken-ahead item is later; if it is a segment's claim (R(k', 0))
-      // others wait for its publication: publish "no image" (claims are
-      // monotone, so that is what the claim would give) before leaving.
-      if (!is_row) {
-        if (tid == 0) {
-          bool r2;
-          int k2, i2;
-          decode_pos(L.item[1], r2, k2, i2);
-          if (r2 && i2 == 0 && k2 + kAhead < max_seg)
-            __hip_atomic_store(img_tab + k2 + kAhead, kNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        break;
-      }
+      // a column item without an image: every later position is empty too
+      // (claims are monotone; a taken-ahead position made its claim at take)
+      if (!is_row) break;
     } else {
       const int n = (int)img - 1;
       const ImgDesc d = imgs[n];
       float* T = tx + (int64_t)(k % kSlots) * kSlotFloats;
+#ifdef DCTAE_ENC_CHECK
+      if (tid == 0) {
+        const int sl = k % kSlots;
+        if (is_row) {
+          const unsigned prev = atomicExch(&g_chk_owner[x][sl], img);
+          if (prev != 0 && prev != img && ld_agent(cdone + prev - 1) != (unsigned)kColItems) {
+            atomicAdd(&g_chk_bad[1], 1u);
+            printf("CHK slot reuse: xcd %d seg %d slot %d img %u prev %u prev-cdone %u\n", x, k, sl, img, prev,
+                   ld_agent(cdone + prev - 1));
+          }
+        } else {
+          const unsigned own = __hip_atomic_load(&g_chk_owner[x][sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned rd = ld_agent(rdone + n);
+          if (own != img || rd != (unsigned)kRowItems) {
+            atomicAdd(&g_chk_bad[2], 1u);
+            printf("CHK col item: xcd %d seg %d slot %d img %u owner %u rdone %u\n", x, k, sl, img, own, rd);
+          }
+        }
+      }
+#endif
       if (is_row) {
         rows512_item<0>(L.u.rows, L.rt, rgb + d.rgb_off, kH, 16 * i, T, (uint32_t)(kH * kKW * 4), cm);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's T stores reached the L2
         __syncthreads();
-        if (tid == 0) __hip_atomic_fetch_add(rdone + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) {
+#if DCTAE_ENC_PREL
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+          __hip_atomic_fetch_add(rdone + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       } else {
         const int c = i >> 5, strip = i & 31;
         float2 thr_r[2][7];
@@ -262,22 +338,33 @@ __global__ __launch_bounds__(256, 3) void k_enc512(const ImgDesc* __restrict__ i
       }
 #endif
     }
-    if (tid == 0) L.item[0] = L.item[1];
+    if (tid == 0) {
+#if DCTAE_ENC_RESERVE
+      L.item[0] = L.item[1];
+#else
+      int pn;
+      if (!take_pos(head, sync, img_tab, n_img, max_seg, pn)) {
+        atomicOr(err, 32);
+        L.item[3] = 1;
+      }
+      L.item[0] = pn;
+#endif
+    }
   }
 #ifdef DCTAE_ENC_STATS
   if (tid == 0) {
     st[6] = __builtin_amdgcn_s_memrealtime() - t_born;
-    for (int e = 0; e < 7; ++e) atomicAdd(&g_enc_st[x][e], st[e]);
+    for (int e = 0; e < 8; ++e) atomicAdd(&g_enc_st[x][e], st[e]);
     __threadfence();
     if (atomicAdd(&g_enc_st_left, 1u) == gridDim.x - 1) {
       __threadfence();
       for (int xx = 0; xx < 8; ++xx) {
-        unsigned long long v[7];
-        for (int e = 0; e < 7; ++e) v[e] = atomicExch(&g_enc_st[xx][e], 0ull);
+        unsigned long long v[8];
+        for (int e = 0; e < 8; ++e) v[e] = atomicExch(&g_enc_st[xx][e], 0ull);
         const double b = v[0] ? (double)v[0] : 1.0;
-        printf("enc512 xcd %d: blocks %llu rows %llu (%.1f us) cols %llu (%.1f us) wait/item %.2f us life/block %.1f us\n",
-               xx, v[0], v[1], v[1] ? v[4] / 100.0 / v[1] : 0.0, v[2], v[2] ? v[5] / 100.0 / v[2] : 0.0,
-               (v[1] + v[2]) ? v[3] / 100.0 / (double)(v[1] + v[2]) : 0.0, v[6] / 100.0 / b);
+        printf("enc512 xcd %d: blocks %llu rows %llu (%.1f us, wait %.2f) cols %llu (%.1f us, wait %.2f) life/block %.1f us\n",
+               xx, v[0], v[1], v[1] ? v[4] / 100.0 / v[1] : 0.0, v[1] ? v[7] / 100.0 / v[1] : 0.0, v[2],
+               v[2] ? v[5] / 100.0 / v[2] : 0.0, v[2] ? (v[3] - v[7]) / 100.0 / v[2] : 0.0, v[6] / 100.0 / b);
       }
       atomicExch(&g_enc_st_left, 0u);
     }
