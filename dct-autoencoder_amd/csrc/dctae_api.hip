@@ -1800,8 +1800,6 @@ static int vq_scratch(dctae_ctx* ctx, size_t need) {
   if (need <= ctx->vq_bytes) return 0;
   HIPCHK(ctx, hipDeviceSynchronize());
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
-  if (ctx->enc_slots) hipFree(ctx->enc_slots);
-  if (ctx->enc_sync) hipFree(ctx->enc_sync);
   ctx->vq_ws = nullptr;
   ctx->vq_bytes = 0;
   if (hipMalloc((void**)&ctx->vq_ws, need) != hipSuccess)
