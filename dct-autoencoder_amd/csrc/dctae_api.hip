@@ -83,6 +83,10 @@ struct dctae_ctx {
   // the two-kernel path and a wrong-code race under 3
   // workgroups per CU is not yet explained; enc512 = 1 selects it
   int enc512 = 0;
+  // DCT GEMMs (lengths without a Makhoul plan, dctae_dct2, decode): 1 = the
+  // split-bf16 MFMA kernel k_gemm_x3 (fp32 accuracy, 0.375 of the MFMA time),
+  // 0 = the fp32 MFMA kernel k_gemm_f32
+  int gemm_x3 = 1;
   float* enc_slots = nullptr;
   unsigned* enc_sync = nullptr;
   size_t enc_sync_words = 0;
@@ -102,6 +106,16 @@ struct dctae_ctx {
   std::vector<hipEvent_t> evt_pool;
   std::vector<TimingEntry> totals;
 };
+
+namespace {
+void ctx_gemm(const dctae_ctx* ctx, int nc, const dctae::GemmProblem* probs, const dctae::TileRef* tiles, int n_tiles,
+              hipStream_t s, int share = 0) {
+  if (ctx->gemm_x3)
+    dctae::launch_gemm_x3(nc, probs, tiles, n_tiles, s, share);
+  else
+    dctae::launch_gemm(nc, probs, tiles, n_tiles, s, share);
+}
+}  // namespace
 
 namespace {
 
@@ -764,6 +778,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "enc512") ctx->enc512 = value != 0;
+  else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "enc_grid" && value >= 0 && value <= (1 << 16)) ctx->enc_grid = (int)value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
@@ -1279,7 +1294,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         launch_rgb_to_ipt(dd, (const int2*)(pd + j.ipt_off), j.n_ipt, imgs->rgb_dev, ctx->ws, ctx->cm, st);
       }
       Timer t(ctx, st, "gemm_rows");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st, 1);
+      ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st, 1);
     }
     for (int l = 0; l < 4; ++l)
       if (j.n_br[l]) {
@@ -1312,7 +1327,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
         launch_fold_t(dd, (const int32_t*)(pd + j.fold_off), j.n_fold, j.fold_max_hw, ctx->ws, st);
       }
       Timer t(ctx, st, "gemm_cols");
-      launch_gemm(3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st, 2);
+      ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st, 2);
     }
     for (int l = 0; l < 4; ++l)
       if (j.n_bc[l]) {
@@ -1471,9 +1486,9 @@ int dctae_dct2(dctae_ctx* ctx, const float* x, int32_t n_img, int32_t H, int32_t
   }
   {
     Timer t(ctx, s, "dct2_gemm");
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s,
+    ctx_gemm(ctx, 3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s,
                 gemm_share(probs[0]));
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s,
+    ctx_gemm(ctx, 3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s,
                 gemm_share(probs[1]));
   }
   if (direction == 1 && color) {
@@ -1820,7 +1835,7 @@ static int vq_linear(dctae_ctx* ctx, const float* A, int64_t n, int K, const flo
   int rc;
   if ((rc = upload_plan(ctx, pb, s))) return rc;
   Timer tm(ctx, s, name);
-  launch_gemm(1, (const GemmProblem*)(ctx->plan_dev + g_off), (const TileRef*)(ctx->plan_dev + t_off), (int)t.size(), s);
+  ctx_gemm(ctx, 1, (const GemmProblem*)(ctx->plan_dev + g_off), (const TileRef*)(ctx->plan_dev + t_off), (int)t.size(), s);
   launch_vq_bias(O, bias, n, N, mask, orig, s);
   return 0;
 }
@@ -2122,11 +2137,11 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   }
   {
     Timer t(ctx, s, "idct_cols");
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s, 2);
+    ctx_gemm(ctx, 3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t1_off), (int)t1.size(), s, 2);
   }
   {
     Timer t(ctx, s, "idct_rows");
-    launch_gemm(3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s, 1);
+    ctx_gemm(ctx, 3, (const GemmProblem*)(pd + g_off), (const TileRef*)(pd + t2_off), (int)t2.size(), s, 1);
   }
   {
     Timer t(ctx, s, "ipt_to_rgb");

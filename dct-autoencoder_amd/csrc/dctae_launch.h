@@ -19,6 +19,8 @@ void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t
 // tiles reference (gemm_share of one of them)
 int gemm_share(const GemmProblem& g);
 void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share = 0);
+// the same GEMM on the bf16 MFMA with three-piece operand splits (fp32 accuracy, k_gemm_x3)
+void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share = 0);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
