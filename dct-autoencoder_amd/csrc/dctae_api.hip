@@ -35,6 +35,12 @@ struct dctae_ctx {
   std::string err;
   // DCT-II matrices C_N[rows][N] (fp32, from float64), keyed by (N, rows)
   std::map<std::pair<int, int>, float*> dct;
+  // the same matrices pre-split for k_gemm_x3 (GemmProblem::Xs), by fp32 pointer
+  struct X3Mat {
+    uint16_t* d;
+    int R, K, Rp, Kp;
+  };
+  std::map<const float*, X3Mat> dct_x3;
   // workspace (floats) and token staging (bytes), grow-only
   float* ws = nullptr;
   size_t ws_bytes = 0;
@@ -307,8 +313,40 @@ int dct_matrix(dctae_ctx* ctx, int N, int rows, const float** out, int parity = 
   HIPCHK(ctx, hipMalloc((void**)&d, h.size() * sizeof(float)));
   HIPCHK(ctx, hipMemcpy(d, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice));
   ctx->dct[key] = d;
+  {
+    std::vector<uint16_t> x;
+    dctae_ctx::X3Mat xm{nullptr, R, Nc, 0, 0};
+    split_matrix_x3(h.data(), R, Nc, x, &xm.Rp, &xm.Kp);
+    HIPCHK(ctx, hipMalloc((void**)&xm.d, x.size() * sizeof(uint16_t)));
+    HIPCHK(ctx, hipMemcpy(xm.d, x.data(), x.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    ctx->dct_x3[d] = xm;
+  }
   *out = d;
   return 0;
+}
+
+// point a GEMM's shared DCT-matrix operand at its pre-split planes (used by
+// k_gemm_x3 only): the operand must be a whole cached matrix read row-major
+// with k contiguous
+void attach_x3(const dctae_ctx* ctx, GemmProblem& g) {
+  const int sh = gemm_share(g);
+  if (ctx->gemm_x3) {
+    // k_gemm_x3's tiles: 128 wide along the shared operand (launch_gemm_x3)
+    if (sh == 1) g.tile_n = 128;
+    if (sh == 2) g.tile_m = 128;
+    g.tiles_n = (g.N + g.tile_n - 1) / g.tile_n;
+  }
+  const float* m = sh == 1 ? g.B : sh == 2 ? g.A : nullptr;
+  if (!m) return;
+  auto it = ctx->dct_x3.find(m);
+  if (it == ctx->dct_x3.end()) return;
+  const auto& x = it->second;
+  const int64_t sr = sh == 1 ? g.sBn : g.sAm, sk = sh == 1 ? g.sBk : g.sAk;
+  const int rows = sh == 1 ? g.N : g.M;
+  if (sk != 1 || sr != x.K || g.K > x.K || rows > x.R) return;
+  g.Xs = x.d;
+  g.xs_ld = x.Kp;
+  g.xs_plane = (int64_t)x.Rp * x.Kp;
 }
 
 int check_cfg(dctae_ctx* ctx, const dctae_fe_cfg* cfg) {
@@ -360,12 +398,52 @@ GemmProblem gemm(const float* A, int64_t sAc, int64_t sAm, int64_t sAk, const fl
   g.sBc = sBc, g.sBn = sBn, g.sBk = sBk;
   g.sOc = sOc, g.sOm = sOm, g.sOn = sOn;
   g.M = M, g.N = N, g.K = K, g.C = C;
+  g.tile_m = g.tile_n = 64;
   g.tiles_n = (N + 63) / 64;
   return g;
 }
 
+// XCD-aware order of a GEMM tile list (speed only; any order is correct).
+// Workgroup b runs on XCD b % 8, so the tiles that read the same per-channel
+// operand panel -- (problem, tile row) when B is the shared matrix (share 1),
+// (problem, tile column) when A is (share 2) -- are dealt to one XCD as
+// consecutive b / 8: the panel is then fetched into that XCD's L2 once instead
+// of once per XCD.  Groups go to the least-loaded XCD; the lanes are padded to
+// equal length with empty tiles (problem -1, the kernels return at once) so
+// the b % 8 affinity holds to the end of the launch.
+void xcd_deal_tiles(std::vector<TileRef>& t, const GemmProblem* probs, int share) {
+  if (t.size() < 16 || share == 0) return;
+  std::vector<std::vector<TileRef>> groups;
+  std::map<std::pair<int, int>, size_t> gi;
+  for (const TileRef& r : t) {
+    const int tn = probs[r.problem].tiles_n;
+    const std::pair<int, int> key{r.problem, share == 1 ? r.tile / tn : r.tile % tn};
+    auto it = gi.find(key);
+    if (it == gi.end()) {
+      gi[key] = groups.size();
+      groups.push_back({r});
+    } else {
+      groups[it->second].push_back(r);
+    }
+  }
+  std::vector<std::vector<TileRef>> lanes(8);
+  for (auto& g : groups) {
+    size_t best = 0;
+    for (size_t x = 1; x < 8; ++x)
+      if (lanes[x].size() < lanes[best].size()) best = x;
+    lanes[best].insert(lanes[best].end(), g.begin(), g.end());
+  }
+  size_t maxlen = 0;
+  for (auto& l : lanes) maxlen = std::max(maxlen, l.size());
+  std::vector<TileRef> out;
+  out.reserve(8 * maxlen);
+  for (size_t q = 0; q < maxlen; ++q)
+    for (int x = 0; x < 8; ++x) out.push_back(q < lanes[x].size() ? lanes[x][q] : TileRef{-1, 0});
+  t.swap(out);
+}
+
 void add_tiles(std::vector<TileRef>& t, int prob, const GemmProblem& g) {
-  int tm = (g.M + 63) / 64;
+  int tm = (g.M + g.tile_m - 1) / g.tile_m;
   for (int i = 0; i < tm * g.tiles_n; ++i) t.push_back({prob, i});
 }
 
@@ -700,6 +778,7 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipDeviceSynchronize();
   for (auto& kv : ctx->dct) hipFree(kv.second);
+  for (auto& kv : ctx->dct_x3) hipFree(kv.second.d);
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->stage) hipFree(ctx->stage);
   if (ctx->plan_host) hipHostFree(ctx->plan_host);
@@ -1015,6 +1094,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           // dimension; with the roles swapped they strided by Kw floats)
           GemmProblem g = gemm(ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1, CW, 0, K, 1,
                                ws + d.ws_t + par, (int64_t)d.Kw * d.H, d.Kw, 2, d.H, M, K, 3);
+          attach_x3(ctx, g);
           add_tiles(rt, (int)(probs.size() - p0), g);
           probs.push_back(g);
         }
@@ -1050,6 +1130,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
                                (int64_t)d.Kw * d.H, 1, par ? -(int64_t)d.Kw : d.Kw,
                                ws + d.ws_y + (int64_t)par * d.Kw, (int64_t)d.Kh * d.Kw, 2 * (int64_t)d.Kw, 1, M,
                                d.Kw, K, 3);
+          attach_x3(ctx, g);
           add_tiles(ct, (int)(probs.size() - p0), g);
           probs.push_back(g);
         }
@@ -1085,6 +1166,10 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       }
     }
     j.gp_off = E.pb.add(probs.data() + p0, probs.size() - p0);
+    if (ctx->xcd_order) {
+      xcd_deal_tiles(rt, probs.data() + p0, 1);
+      xcd_deal_tiles(ct, probs.data() + p0, 2);
+    }
     j.rows_t_off = E.pb.add(rt.data(), rt.size());
     j.cols_t_off = E.pb.add(ct.data(), ct.size());
     // XCD-aware order of the column blocks (speed only; any order is correct):
@@ -1200,7 +1285,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
-                             64 * ctx->t_alias + 1024 * ctx->xcd_order,
+                             64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1467,6 +1552,8 @@ int dctae_dct2(dctae_ctx* ctx, const float* x, int32_t n_img, int32_t H, int32_t
       g1 = gemm(CH, 0, 1, H, x + o, hw, 1, W, u + o, hw, W, 1, H, W, H, 3);
       g2 = gemm(u + o, hw, W, 1, CW, 0, 1, W, dst, hw, W, 1, H, W, W, 3);
     }
+    attach_x3(ctx, g1);
+    attach_x3(ctx, g2);
     const int pr = (int)probs.size();
     probs.push_back(g1);
     probs.push_back(g2);
@@ -2091,6 +2178,8 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
     // X[c][y][x] = sum_kx U[c][y][kx] * CW[kx][x]
     GemmProblem g2 = gemm(ws + d.ws_t, (int64_t)d.H * d.Kw, d.Kw, 1, CW, 0, 1, d.W, ws + d.ws_p,
                           (int64_t)d.H * d.W, d.W, 1, d.H, d.W, d.Kw, 3);
+    attach_x3(ctx, g1);
+    attach_x3(ctx, g2);
     int pr = (int)probs.size();
     probs.push_back(g1);
     probs.push_back(g2);

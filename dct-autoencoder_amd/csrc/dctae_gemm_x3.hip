@@ -1,0 +1,372 @@
+// k_gemm_x3: the batched strided DCT GEMM of dctae_kernels.hip (k_gemm_f32,
+//   O[c][m][n] = sum_k A[c][m][k] B[c][n][k])
+// on the bf16 MFMA at fp32 accuracy.  Every operand element is split into
+// three bf16 pieces a = a0 + a1 + a2 (a0 = bf16(a), a1 = bf16(a - a0),
+// a2 = bf16(a - a0 - a1): 24 significant bits, as fp32) and the product keeps
+// the six terms whose piece orders sum to <= 2,
+//   a0 b0 + a0 b1 + a1 b0 + a1 b1 + a0 b2 + a2 b0,
+// accumulated in fp32 by v_mfma_f32_32x32x16_bf16 (the dropped terms are
+// ~2^-24 of |a b|).  Six bf16 MFMAs per 16-deep k step cost 6 x 32 cycles
+// against 8 x 64 for the same step on v_mfma_f32_32x32x2_f32.  Measured
+// against float64 on the orthonormal DCT: ~5e-8 of max |Y| (fp32 GEMM ~6e-7).
+//
+// Tiles as k_gemm_f32: 64 x 64 per workgroup, 4 waves of 32 x 32, K chunks of
+// 32 (two k steps), the next chunk's global loads in flight during the MFMAs.
+// Staging, per operand and channel:
+//   * the shared DCT matrix comes pre-split (GemmProblem::Xs, three zero-padded
+//     bf16 planes built once with the matrix): three 16-byte loads and LDS
+//     writes per thread, no arithmetic;
+//   * an fp32 operand whose k is contiguous: thread (row tid / 4, k 8 (tid % 4))
+//     reads 8 floats as two 16-byte buffer loads;
+//   * otherwise (row-contiguous, e.g. T of the column GEMM, stride +-Kw along
+//     k): thread (row tid % 64, k 8 (tid / 64)), 8 four-byte loads that
+//     coalesce across the wave's 64 rows;
+//   then v_cvt_pk_bf16_f32 splits (the plain vector casts compile to it) and
+//   three 16-byte LDS writes.  Buffer resources span exactly the operand's
+//   element range, so rows past M / N and k past the range read 0; k past K
+//   inside the range is zeroed in the last chunk only.
+// LDS rows are 40 bf16 (80 bytes): the 32 lanes of a ds_read_b128 fragment
+// group hit distinct banks, as do the 16-byte staging writes.
+#include "dctae_launch.h"
+#include "dctae_device.h"
+
+namespace dctae {
+
+namespace {
+
+constexpr int XK = 32;        // k chunk
+constexpr int kOob = 0x7ffffff0;
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// LDS image of one operand tile: three bf16 pieces of ROWS x 32 k, rows of
+// 64 bytes, the 16-byte k group kq of row r at slot kq ^ swz(r).  With this
+// swizzle the 16-lane groups of a ds_read_b128 fragment read, the 8-lane
+// groups of the staging ds_write_b128 (two rows x four k groups, or eight rows
+// x one k group) all hit distinct banks (exhaustive check over the lane
+// groups of MI355X_MICROARCH.md §LDS).
+__device__ __forceinline__ int swz(int r) { return ((r >> 1) ^ (r >> 2)) & 3; }
+__device__ __forceinline__ int lds_off(int r, int kq) { return r * XK + 8 * (kq ^ swz(r)); }
+
+template <int ROWS>
+struct Pieces {
+  uint16_t p[3][ROWS * XK];
+};
+
+// one fp32 operand (64 rows x depth k) of one channel, as this thread stages it
+struct Src {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff;    // byte offset of this thread's (row, first k) from the range start; kOob for a row past the edge
+  int kstep;   // bytes per k
+  bool kc;     // k contiguous
+  int kq;      // this thread's k group (8 kq)
+  int row;     // this thread's row in the 64-row block
+};
+
+// rows [r0, r0 + 64) of X[r][k] = base[r * sr + k * sk], r < R, k < K
+__device__ __forceinline__ Src make_src(const float* base, int64_t sr, int64_t sk, int r0, int R, int K) {
+  Src s;
+  s.kc = (sk == 1);
+  const int tid = threadIdx.x;
+  s.row = s.kc ? (tid >> 2) : (tid & 63);
+  s.kq = s.kc ? (tid & 3) : (tid >> 6);
+  // element range of the whole operand: [lo, hi]
+  const int64_t lo = (sr < 0 ? (int64_t)(R - 1) * sr : 0) + (sk < 0 ? (int64_t)(K - 1) * sk : 0);
+  const int64_t hi = (sr > 0 ? (int64_t)(R - 1) * sr : 0) + (sk > 0 ? (int64_t)(K - 1) * sk : 0);
+  s.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + lo), 0, (int)((hi - lo + 1) * 4), 0x00020000);
+  s.kstep = (int)(sk * 4);
+  const int r = r0 + s.row;
+  s.voff = r < R ? (int)(((int64_t)r * sr + (int64_t)(8 * s.kq) * sk - lo) * 4) : kOob;
+  return s;
+}
+
+__device__ __forceinline__ f32x8 load_src(const Src& s, int k0, int K) {
+  f32x8 v;
+  if (s.kc) {
+    const int o = s.voff + k0 * 4;
+    const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, o, 0, 0));
+    const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, o + 16, 0, 0));
+    v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(s.rsrc, s.voff + (k0 + e) * s.kstep, 0, 0));
+  }
+  if (k0 + XK > K) {   // last chunk: k past K inside the range
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (k0 + 8 * s.kq + e >= K) v[e] = 0.0f;
+  }
+  return v;
+}
+
+template <int ROWS>
+__device__ __forceinline__ void split_store(Pieces<ROWS>& L, const Src& s, int rbase, f32x8 v) {
+  const bfv8 h0 = __builtin_convertvector(v, bfv8);
+  const f32x8 r1 = v - __builtin_convertvector(h0, f32x8);
+  const bfv8 h1 = __builtin_convertvector(r1, bfv8);
+  const f32x8 r2 = r1 - __builtin_convertvector(h1, f32x8);
+  const bfv8 h2 = __builtin_convertvector(r2, bfv8);
+  const int o = lds_off(rbase + s.row, s.kq);
+  *reinterpret_cast<bfv8*>(&L.p[0][o]) = h0;
+  *reinterpret_cast<bfv8*>(&L.p[1][o]) = h1;
+  *reinterpret_cast<bfv8*>(&L.p[2][o]) = h2;
+}
+
+// pre-split planes, ROWS rows: thread slot i = tid + 256 j -> (row i / 4, k group i % 4)
+template <int ROWS>
+struct PreSplit {
+  u32x4 v[ROWS / 64][3];
+};
+
+template <int ROWS>
+__device__ __forceinline__ void load_pre(PreSplit<ROWS>& q, const GemmProblem& p, int r0, int k0) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < ROWS / 64; ++j) {
+    const uint16_t* x = p.Xs + (int64_t)(r0 + 64 * j + (tid >> 2)) * p.xs_ld + k0 + 8 * (tid & 3);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) q.v[j][i] = *reinterpret_cast<const u32x4*>(x + i * p.xs_plane);
+  }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void store_pre(Pieces<ROWS>& L, const PreSplit<ROWS>& q) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < ROWS / 64; ++j) {
+    const int o = lds_off(64 * j + (tid >> 2), tid & 3);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) *reinterpret_cast<u32x4*>(&L.p[i][o]) = q.v[j][i];
+  }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void read_frag(bf16x8 (&f)[3], const Pieces<ROWS>& L, int r, int kq) {
+  const int o = lds_off(r, kq);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8*>(&L.p[q][o]);
+}
+
+// six split products, small terms first
+__device__ __forceinline__ void mfma6(floatx16& acc, const bf16x8 (&a)[3], const bf16x8 (&b)[3]) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+}
+
+}  // namespace
+
+// SH: 0 none shared (NC operands each, 64 x 64 tiles), 1 B shared (64 x 128
+// tiles), 2 A shared (128 x 64 tiles): the tile is 128 wide along the shared
+// operand, so the per-channel operand's split (the VALU part of the staging)
+// serves twice the MFMAs.  PRE: the shared operand is read pre-split (p.Xs);
+// the two forms are separate bodies so that only one form's staging registers
+// are live.  4 waves in 2 x 2, each (TM / 2) x (TN / 2) of every channel.
+template <int NC, int SH>
+struct X3Shape {
+  static constexpr int NA = SH == 2 ? 1 : NC, NB = SH == 1 ? 1 : NC;
+  static constexpr int TM = SH == 2 ? 128 : 64, TN = SH == 1 ? 128 : 64;
+};
+
+template <int NC, int SH, bool PRE>
+__device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int tn,
+                                             Pieces<X3Shape<NC, SH>::TM> (&As)[X3Shape<NC, SH>::NA],
+                                             Pieces<X3Shape<NC, SH>::TN> (&Bs)[X3Shape<NC, SH>::NB]) {
+  using S = X3Shape<NC, SH>;
+  constexpr int NA = S::NA, NB = S::NB, TM = S::TM, TN = S::TN;
+  constexpr int BM = TM / 64, BN = TN / 64;   // 32 x 32 MFMA blocks per wave, per dimension
+  constexpr bool preA = PRE && SH == 2, preB = PRE && SH == 1;
+  constexpr int SAM = preA ? 0 : BM, SBN = preB ? 0 : BN;   // fp32 sources per channel
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  Src sa[NA][SAM > 0 ? SAM : 1], sb[NB][SBN > 0 ? SBN : 1];
+#pragma unroll
+  for (int c = 0; c < NA; ++c)
+#pragma unroll
+    for (int j = 0; j < SAM; ++j) sa[c][j] = make_src(p.A + (int64_t)c * p.sAc, p.sAm, p.sAk, m0 + 64 * j, p.M, p.K);
+#pragma unroll
+  for (int c = 0; c < NB; ++c)
+#pragma unroll
+    for (int j = 0; j < SBN; ++j) sb[c][j] = make_src(p.B + (int64_t)c * p.sBc, p.sBn, p.sBk, n0 + 64 * j, p.N, p.K);
+
+  floatx16 acc[NC][BM][BN];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < BM; ++i)
+#pragma unroll
+      for (int j = 0; j < BN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][i][j][r] = 0.0f;
+
+  f32x8 va[NA][SAM > 0 ? SAM : 1], vb[NB][SBN > 0 ? SBN : 1];
+  PreSplit<TM> qa;
+  PreSplit<TN> qb;
+  auto load = [&](int k0) {
+    if constexpr (preA) load_pre(qa, p, m0, k0);
+#pragma unroll
+    for (int c = 0; c < NA; ++c)
+#pragma unroll
+      for (int j = 0; j < SAM; ++j) va[c][j] = load_src(sa[c][j], k0, p.K);
+    if constexpr (preB) load_pre(qb, p, n0, k0);
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+#pragma unroll
+      for (int j = 0; j < SBN; ++j) vb[c][j] = load_src(sb[c][j], k0, p.K);
+  };
+  auto store = [&]() {
+    if constexpr (preA) store_pre(As[0], qa);
+#pragma unroll
+    for (int c = 0; c < NA; ++c)
+#pragma unroll
+      for (int j = 0; j < SAM; ++j) split_store(As[c], sa[c][j], 64 * j, va[c][j]);
+    if constexpr (preB) store_pre(Bs[0], qb);
+#pragma unroll
+    for (int c = 0; c < NB; ++c)
+#pragma unroll
+      for (int j = 0; j < SBN; ++j) split_store(Bs[c], sb[c][j], 64 * j, vb[c][j]);
+  };
+  load(0);
+  store();
+  __syncthreads();
+  for (int k0 = 0; k0 < p.K; k0 += XK) {
+    const bool more = k0 + XK < p.K;
+    if (more) load(k0 + XK);
+#pragma unroll
+    for (int s = 0; s < XK / 16; ++s) {
+      // lane (l32, half): A[row l32][k = 16 s + 8 half + j], B[k][col l32]: k group 2 s + half
+      const int kq = 2 * s + half;
+      if constexpr (NB == 1) {
+        bf16x8 b[BN][3];
+#pragma unroll
+        for (int j = 0; j < BN; ++j) read_frag(b[j], Bs[0], wn * (TN / 2) + 32 * j + l32, kq);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int i = 0; i < BM; ++i) {
+            bf16x8 a[3];
+            read_frag(a, As[c], wm * (TM / 2) + 32 * i + l32, kq);
+#pragma unroll
+            for (int j = 0; j < BN; ++j) mfma6(acc[c][i][j], a, b[j]);
+          }
+      } else if constexpr (NA == 1) {
+        bf16x8 a[BM][3];
+#pragma unroll
+        for (int i = 0; i < BM; ++i) read_frag(a[i], As[0], wm * (TM / 2) + 32 * i + l32, kq);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int j = 0; j < BN; ++j) {
+            bf16x8 b[3];
+            read_frag(b, Bs[c], wn * (TN / 2) + 32 * j + l32, kq);
+#pragma unroll
+            for (int i = 0; i < BM; ++i) mfma6(acc[c][i][j], a[i], b);
+          }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          bf16x8 a[3], b[3];
+          read_frag(a, As[c], wm * 32 + l32, kq);
+          read_frag(b, Bs[c], wn * 32 + l32, kq);
+          mfma6(acc[c][0][0], a, b);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  // C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float* O = p.O + (int64_t)c * p.sOc;
+#pragma unroll
+    for (int i = 0; i < BM; ++i)
+#pragma unroll
+      for (int j = 0; j < BN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * half;
+          const int gm = m0 + wm * (TM / 2) + 32 * i + row, gn = n0 + wn * (TN / 2) + 32 * j + l32;
+          if (gm < p.M && gn < p.N) O[(int64_t)gm * p.sOm + (int64_t)gn * p.sOn] = acc[c][i][j][r];
+        }
+  }
+}
+
+template <int NC, int SH>
+__global__ __launch_bounds__(256, (SH == 0 && NC == 3) ? 1 : 2) void k_gemm_x3(const GemmProblem* __restrict__ probs,
+                                                                             const TileRef* __restrict__ tiles) {
+  using S = X3Shape<NC, SH>;
+  __shared__ Pieces<S::TM> As[S::NA];
+  __shared__ Pieces<S::TN> Bs[S::NB];
+  const TileRef tr = tiles[blockIdx.x];
+  if (tr.problem < 0) return;   // padding of an XCD-dealt list
+  const GemmProblem p = probs[tr.problem];
+  const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
+  if (SH != 0 && p.Xs != nullptr)
+    gemm_x3_body<NC, SH, true>(p, tm, tn, As, Bs);
+  else
+    gemm_x3_body<NC, SH, false>(p, tm, tn, As, Bs);
+}
+
+void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
+  if (n_tiles <= 0) return;
+  if (nc == 3 && share == 1)
+    hipLaunchKernelGGL((k_gemm_x3<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else if (nc == 3 && share == 2)
+    hipLaunchKernelGGL((k_gemm_x3<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else if (nc == 3)
+    hipLaunchKernelGGL((k_gemm_x3<3, 0>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else
+    hipLaunchKernelGGL((k_gemm_x3<1, 0>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+}
+
+// host: three bf16 planes [3][Rp][Kp] of a row-major fp32 matrix (R x K),
+// zero padded to Rp = ceil128(R), Kp = ceil32(K); the same round-to-nearest-
+// even split the kernel applies to fp32 operands
+static uint16_t host_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static float host_f32(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp) {
+  *Rp = (R + 127) / 128 * 128;
+  *Kp = (K + XK - 1) / XK * XK;
+  const size_t plane = (size_t)*Rp * *Kp;
+  out.assign(3 * plane, 0);
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < K; ++k) {
+      const float v = m[(size_t)r * K + k];
+      const uint16_t h0 = host_bf16(v);
+      const float r1 = v - host_f32(h0);
+      const uint16_t h1 = host_bf16(r1);
+      const float r2 = r1 - host_f32(h1);
+      const size_t o = (size_t)r * *Kp + k;
+      out[o] = h0;
+      out[plane + o] = h1;
+      out[2 * plane + o] = host_bf16(r2);
+    }
+}
+
+}  // namespace dctae

@@ -44,8 +44,15 @@ struct GemmProblem {
   int64_t sBc, sBn, sBk;
   int64_t sOc, sOm, sOn;
   int32_t M, N, K, C;
-  int32_t tiles_n;   // ceil(N / 64)
-  int32_t pad;
+  int32_t tiles_n;   // ceil(N / tile_n)
+  int32_t tile_m, tile_n;   // 64 x 64 (k_gemm_f32); k_gemm_x3: 128 along the shared operand
+  // k_gemm_x3 only: the shared operand (B when only B is shared, else A)
+  // pre-split into three bf16 planes [3][Rp][xs_ld] (Rp = rows rounded up to
+  // 128, xs_ld = K rounded up to 32, zero padded); null = split in the kernel
+  int32_t xs_ld;
+  int32_t pad2;
+  const uint16_t* Xs;
+  int64_t xs_plane;  // Rp * xs_ld
 };
 
 // FFT-DCT plan for one length N (M = N/2 point complex FFT), dctae_fft.hip

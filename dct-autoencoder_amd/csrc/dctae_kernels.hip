@@ -278,6 +278,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
   __shared__ __attribute__((aligned(16))) float As[NA][GT * GLD];
   __shared__ __attribute__((aligned(16))) float Bs[NB][GT * GLD];
   const TileRef tr = tiles[blockIdx.x];
+  if (tr.problem < 0) return;   // padding of an XCD-dealt list
   const GemmProblem p = probs[tr.problem];
   const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
   const int m0 = tm * GT, n0 = tn * GT;
@@ -395,166 +396,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
       if (gm < p.M && gn < p.N) O[(int64_t)gm * p.sOm + (int64_t)gn * p.sOn] = acc[c][r];
     }
   }
-}
-
-// ---------------------------------------------------------------------------
-// The same batched strided GEMM on the bf16 MFMA at fp32 accuracy: every
-// operand element is split into three bf16 pieces a = a0 + a1 + a2 (a0 =
-// bf16(a), a1 = bf16(a - a0), a2 = bf16(a - a0 - a1): 24 significant bits, as
-// fp32) and the product takes the six terms whose piece orders sum to <= 2,
-//   a0 b0 + (a0 b1 + a1 b0) + (a1 b1 + a0 b2 + a2 b0),
-// accumulated in fp32 by v_mfma_f32_32x32x16_bf16 (the dropped terms are
-// ~2^-24 of |a b|).  Six bf16 MFMAs per 16-deep k step take 0.375 of the time
-// of the eight f32 MFMAs (v_mfma_f32_32x32x2_f32) of the same step.  Measured
-// against float64 on a 1000-point DCT matrix: error 5e-8 of max |Y| (fp32
-// GEMM: 6e-7).  Tiles as k_gemm_f32: 64 x 64 per workgroup, 4 waves of
-// 32 x 32, K chunks of 32 (two k steps).
-// Staging: each thread owns 8 consecutive k of one row (m or n) of a tile;
-// rows are picked along the operand's contiguous dimension so global loads
-// coalesce; the split pieces go to LDS as three 16-byte writes.
-// ---------------------------------------------------------------------------
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int XLD = GK + 8;   // LDS row stride in bf16 (80 bytes): b128 fragment reads spread over the banks
-
-__device__ __forceinline__ unsigned short f32_to_bf16_rne(float f) {
-  // round to nearest even (finite inputs; NaN stays NaN through the plain cast)
-  return __builtin_bit_cast(unsigned short, (__bf16)f);
-}
-__device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
-
-template <int NC, int SH>
-__global__ __launch_bounds__(256, 2) void k_gemm_x3(const GemmProblem* __restrict__ probs,
-                                                 const TileRef* __restrict__ tiles) {
-  constexpr int NA = SH == 2 ? 1 : NC, NB = SH == 1 ? 1 : NC;
-  // [operand tile][piece][row][k]
-  __shared__ __attribute__((aligned(16))) unsigned short As[NA][3][GT * XLD];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[NB][3][GT * XLD];
-  const TileRef tr = tiles[blockIdx.x];
-  const GemmProblem p = probs[tr.problem];
-  const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
-  const int m0 = tm * GT, n0 = tn * GT;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int half = lane >> 5, l32 = lane & 31;
-
-  floatx16 acc[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[c][r] = 0.0f;
-
-  // staging coordinates: k-contiguous operand -> (row tid >> 2, k 8 (tid & 3));
-  // row-contiguous operand -> (row tid & 63, k 8 (tid >> 6))
-  const bool akf = (p.sAk == 1), bkf = (p.sBk == 1);
-  const int ar = akf ? (tid >> 2) : (tid & 63), ak = akf ? 8 * (tid & 3) : 8 * (tid >> 6);
-  const int br = bkf ? (tid >> 2) : (tid & 63), bk = bkf ? 8 * (tid & 3) : 8 * (tid >> 6);
-  const int sAm = (int)p.sAm, sAk = (int)p.sAk, sBn = (int)p.sBn, sBk = (int)p.sBk;
-  float ra[NA][8], rb[NB][8];
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int c = 0; c < NA; ++c) {
-      const float* A = p.A + (int64_t)c * p.sAc;
-      const int gm = m0 + ar;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int gk = k0 + ak + e;
-        const bool ok = gm < p.M && gk < p.K;
-        ra[c][e] = ok ? A[ok ? gm * sAm + gk * sAk : 0] : 0.0f;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < NB; ++c) {
-      const float* B = p.B + (int64_t)c * p.sBc;
-      const int gn = n0 + br;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int gk = k0 + bk + e;
-        const bool ok = gn < p.N && gk < p.K;
-        rb[c][e] = ok ? B[ok ? gn * sBn + gk * sBk : 0] : 0.0f;
-      }
-    }
-  };
-  auto split_store = [&](unsigned short (*dst)[GT * XLD], const float (&v)[8], int row, int k) {
-    bf16x8 p0, p1, p2;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const unsigned short h0 = f32_to_bf16_rne(v[e]);
-      const float r1 = v[e] - bf16_to_f32(h0);
-      const unsigned short h1 = f32_to_bf16_rne(r1);
-      const float r2 = r1 - bf16_to_f32(h1);
-      p0[e] = (short)h0;
-      p1[e] = (short)h1;
-      p2[e] = (short)f32_to_bf16_rne(r2);
-    }
-    *reinterpret_cast<bf16x8*>(&dst[0][row * XLD + k]) = p0;
-    *reinterpret_cast<bf16x8*>(&dst[1][row * XLD + k]) = p1;
-    *reinterpret_cast<bf16x8*>(&dst[2][row * XLD + k]) = p2;
-  };
-  auto store = [&]() {
-#pragma unroll
-    for (int c = 0; c < NA; ++c) split_store(As[c], ra[c], ar, ak);
-#pragma unroll
-    for (int c = 0; c < NB; ++c) split_store(Bs[c], rb[c], br, bk);
-  };
-  load(0);
-  store();
-  __syncthreads();
-  for (int k0 = 0; k0 < p.K; k0 += GK) {
-    const bool more = k0 + GK < p.K;
-    if (more) load(k0 + GK);
-#pragma unroll
-    for (int s = 0; s < GK / 16; ++s) {
-      // lane (l32, half): A[row l32][k = 16 s + 8 half + j], B[k][col l32]
-      const int ko = 16 * s + 8 * half;
-      bf16x8 b[NB][3];
-#pragma unroll
-      for (int c = 0; c < NB; ++c)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) b[c][q] = *reinterpret_cast<const bf16x8*>(&Bs[c][q][(wn * 32 + l32) * XLD + ko]);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int ca = NA == 1 ? 0 : c, cb = NB == 1 ? 0 : c;
-        bf16x8 a[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8*>(&As[ca][q][(wm * 32 + l32) * XLD + ko]);
-        // small terms first
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[cb][0], acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[cb][2], acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[cb][1], acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[cb][0], acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[cb][1], acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[cb][0], acc[c], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-    if (more) {
-      store();
-      __syncthreads();
-    }
-  }
-  // ---- store: C/D map col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    float* O = p.O + (int64_t)c * p.sOc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      int row = (r & 3) + 8 * (r >> 2) + 4 * half;
-      int gm = m0 + wm * 32 + row, gn = n0 + wn * 32 + l32;
-      if (gm < p.M && gn < p.N) O[(int64_t)gm * p.sOm + (int64_t)gn * p.sOn] = acc[c][r];
-    }
-  }
-}
-
-void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
-  if (n_tiles <= 0) return;
-  if (nc == 3 && share == 1)
-    hipLaunchKernelGGL((k_gemm_x3<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
-  else if (nc == 3 && share == 2)
-    hipLaunchKernelGGL((k_gemm_x3<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
-  else if (nc == 3)
-    hipLaunchKernelGGL((k_gemm_x3<3, 0>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
-  else
-    hipLaunchKernelGGL((k_gemm_x3<1, 0>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
 }
 
 int gemm_share(const GemmProblem& g) {

@@ -1,6 +1,8 @@
 // Host-side launch wrappers of the kernels in dctae_kernels.hip / dctae_fft.hip.
 #pragma once
 #include <algorithm>
+#include <cstring>
+#include <vector>
 
 #include "dctae_internal.h"
 
@@ -21,6 +23,8 @@ int gemm_share(const GemmProblem& g);
 void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share = 0);
 // the same GEMM on the bf16 MFMA with three-piece operand splits (fp32 accuracy, k_gemm_x3)
 void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share = 0);
+// three bf16 planes [3][Rp][Kp] of a row-major fp32 matrix (GemmProblem::Xs)
+void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,

@@ -9,6 +9,8 @@ rm -rf $OUT; mkdir -p $OUT
 # DECODE=1: the config-3 decode leg runs too (its kernels land in the same passes)
 DEC="--no-decode"; [ -n "${DECODE:-}" ] && DEC=""
 BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-stats --no-model --no-configs $DEC ${BENCH_ARGS:-}"
+# CMD=...: profile another program instead (e.g. CMD="python3 tools/cfg4_run.py 1")
+BENCH=${CMD:-$BENCH}
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
@@ -21,4 +23,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 $OUT/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_enc_summary.py $OUT > /dev/null
+python3 tools/pmc_enc_summary.py $OUT ${SUMMARY_ARGS:-} > $OUT/summary.txt; cat $OUT/summary.txt
