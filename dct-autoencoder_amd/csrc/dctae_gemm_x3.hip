@@ -123,14 +123,19 @@ struct PreSplit {
   u32x4 v[ROWS / 64][3];
 };
 
+// buffer loads (a plain load through the pointer read from the problem struct
+// compiles to flat_load, which also counts in lgkmcnt: the first LDS wait of
+// the chunk's MFMAs then waited for these global loads too)
 template <int ROWS>
 __device__ __forceinline__ void load_pre(PreSplit<ROWS>& q, const GemmProblem& p, int r0, int k0) {
   const int tid = threadIdx.x;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.Xs), 0, (int)(3 * p.xs_plane * 2), 0x00020000);
 #pragma unroll
   for (int j = 0; j < ROWS / 64; ++j) {
-    const uint16_t* x = p.Xs + (int64_t)(r0 + 64 * j + (tid >> 2)) * p.xs_ld + k0 + 8 * (tid & 3);
+    const int o = ((r0 + 64 * j + (tid >> 2)) * p.xs_ld + k0 + 8 * (tid & 3)) * 2;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) q.v[j][i] = *reinterpret_cast<const u32x4*>(x + i * p.xs_plane);
+    for (int i = 0; i < 3; ++i)
+      q.v[j][i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + (int)(i * p.xs_plane * 2), 0, 0));
   }
 }
 
@@ -289,7 +294,31 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
       __syncthreads();
     }
   }
-  // C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  // C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+  // Row-major outputs (a row's extent within the row stride): buffer stores
+  // on the channel's output range, one 32-bit lane offset per (i, j) plus a
+  // uniform row step; rows past M land past the range and columns past N get
+  // an out-of-range offset, so no per-store predicate or 64-bit address math
+  const int64_t ext = (int64_t)(p.M - 1) * p.sOm + (int64_t)(p.N - 1) * p.sOn + 1;
+  if (p.sOm > 0 && p.sOn > 0 && p.sOm >= (int64_t)(p.N - 1) * p.sOn + 1 && (ext + 160 * p.sOm) * 4 < kOob) {
+    const int sOm4 = (int)(p.sOm * 4);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.O + (int64_t)c * p.sOc, 0, (int)(ext * 4), 0x00020000);
+#pragma unroll
+      for (int i = 0; i < BM; ++i)
+#pragma unroll
+        for (int j = 0; j < BN; ++j) {
+          const int gm = m0 + wm * (TM / 2) + 32 * i + 4 * half, gn = n0 + wn * (TN / 2) + 32 * j + l32;
+          const int vo = gn < p.N ? gm * sOm4 + (int)(gn * p.sOn * 4) : kOob;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c][i][j][r]), rsrc,
+                                                  vo + ((r & 3) + 8 * (r >> 2)) * sOm4, 0, 0);
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     float* O = p.O + (int64_t)c * p.sOc;
