@@ -102,6 +102,9 @@ struct dctae_ctx {
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
   uint8_t* vq_ws = nullptr;
   size_t vq_bytes = 0;
+  // LFQ projection scratch (the pre-split weight planes), grow-only
+  uint16_t* proj_ws = nullptr;
+  size_t proj_bytes = 0;
   size_t st_bytes = 0;
   // cached encode plan
   std::vector<int64_t> enc_key;
@@ -322,6 +325,20 @@ int dct_matrix(dctae_ctx* ctx, int N, int rows, const float** out, int parity = 
     ctx->dct_x3[d] = xm;
   }
   *out = d;
+  return 0;
+}
+
+// grow-only scratch for the LFQ projections' pre-split weight (N x K)
+int proj_scratch(dctae_ctx* ctx, int N, int K) {
+  const size_t need = lfq_proj_scratch_bytes(N, K);
+  if (need <= ctx->proj_bytes) return 0;
+  HIPCHK(ctx, hipDeviceSynchronize());
+  if (ctx->proj_ws) hipFree(ctx->proj_ws);
+  ctx->proj_ws = nullptr;
+  ctx->proj_bytes = 0;
+  if (hipMalloc((void**)&ctx->proj_ws, need) != hipSuccess)
+    return fail(ctx, DCTAE_ENOMEM, "LFQ projection scratch allocation failed");
+  ctx->proj_bytes = need;
   return 0;
 }
 
@@ -787,6 +804,7 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->fft_tab) hipFree(ctx->fft_tab);
   if (ctx->st_ws) hipFree(ctx->st_ws);
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
+  if (ctx->proj_ws) hipFree(ctx->proj_ws);
   if (ctx->enc_slots) hipFree(ctx->enc_slots);
   if (ctx->enc_sync) hipFree(ctx->enc_sync);
   delete ctx->enc_plan;
@@ -1465,7 +1483,9 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   }
   if (proj_w && E.n_tok > 0) {
     Timer t(ctx, s, "lfq_project_in");
-    launch_lfq_project_in16(sk.norm, E.n_tok, PP, proj_w, proj_b, lfq->codebook_dim, lfq->num_codebooks, sk.codes, s);
+    if ((rc = proj_scratch(ctx, lfq->codebook_dim * lfq->num_codebooks, PP))) return rc;
+    launch_lfq_project_in16(sk.norm, E.n_tok, PP, proj_w, proj_b, lfq->codebook_dim, lfq->num_codebooks, sk.codes,
+                            ctx->proj_ws, s);
   }
   if (full && E.n_img > 0) {
     Timer t(ctx, s, "sort_pack");
@@ -1844,8 +1864,10 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, i
   if (int rc = lfq_proj_check(ctx, lfq, n, dim, x, w, idx, 64)) return rc;
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (int rc = proj_scratch(ctx, lfq->codebook_dim * lfq->num_codebooks, dim)) return rc;
   Timer t(ctx, s, "lfq_project_in");
-  launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, idx, s);
+  launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, idx,
+                        ctx->proj_ws, s);
   HIPCHK(ctx, hipGetLastError());
   return 0;
 }
@@ -1856,8 +1878,10 @@ int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* i
   if (int rc = lfq_proj_check(ctx, lfq, n, dim, idx, w, out, 32)) return rc;
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (int rc = proj_scratch(ctx, dim, lfq->codebook_dim * lfq->num_codebooks)) return rc;
   Timer t(ctx, s, "lfq_project_out");
-  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out, s);
+  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
+                         ctx->proj_ws, s);
   HIPCHK(ctx, hipGetLastError());
   return 0;
 }
@@ -1877,9 +1901,10 @@ int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, con
     return fail(ctx, DCTAE_EINVAL, "fused inverse PatchNorm needs 16-byte aligned median / b / out");
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
+  if (int rc = proj_scratch(ctx, dim, lfq->codebook_dim * lfq->num_codebooks)) return rc;
   Timer t(ctx, s, "lfq_project_out");
-  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out, s,
-                         channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h, max_patch_w,
+  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
+                         ctx->proj_ws, s, channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h, max_patch_w,
                          ctx->err_dev);
   HIPCHK(ctx, hipGetLastError());
   return 0;

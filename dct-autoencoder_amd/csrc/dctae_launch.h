@@ -38,12 +38,14 @@ void launch_lfq_forward(const float* x, int64_t n, int cb_dim, int ncb, float sc
                         hipStream_t s);
 void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float scale, float* out, hipStream_t s);
 // dctae_lfq_proj.hip: LFQ with projections, fused project_in + sign + pack / codes + project_out
+// wsp: scratch of lfq_proj_scratch_bytes(out features, in features) for the pre-split weight
+size_t lfq_proj_scratch_bytes(int N, int K);
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                           float scale, int64_t* idx, hipStream_t s);
+                           float scale, int64_t* idx, uint16_t* wsp, hipStream_t s);
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                             uint16_t* idx, hipStream_t s);
+                             uint16_t* idx, uint16_t* wsp, hipStream_t s);
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                            float scale, float* out, hipStream_t s, const int64_t* ch = nullptr,
+                            float scale, float* out, uint16_t* wsp, hipStream_t s, const int64_t* ch = nullptr,
                             const int64_t* pos = nullptr, const float* med = nullptr, const float* nb = nullptr,
                             float eps = 0.f, int maxph = 0, int maxpw = 0, int* err = nullptr);
 // VectorQuantize inference (dctae_vq.hip)

@@ -41,22 +41,56 @@ struct InvNorm {
 };
 
 constexpr int kTokW = 16;    // tokens per wave and M tile
-constexpr int kKc = 16;      // k chunk
-constexpr int kLd = kKc + 4; // LDS row stride (floats)
+constexpr int kKc = 32;      // k chunk (one v_mfma_f32_16x16x32_bf16 step)
 
-template <int NT, int MODE, int WB>
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// LDS image of a 32-k chunk: bf16 pieces of R rows, 64-byte rows, 16-byte k
+// group kq of row r at slot kq ^ swz(r) (conflict-free for the fragment reads
+// and the staging writes, as k_gemm_x3)
+__device__ __forceinline__ int pswz(int r) { return ((r >> 1) ^ (r >> 2)) & 3; }
+__device__ __forceinline__ int poff(int r, int kq) { return r * kKc + 8 * (kq ^ pswz(r)); }
+
+// split 8 floats into NPC bf16 pieces (v = p0 + p1 + p2 to fp32 precision)
+// and write them to the piece planes at offset o
+template <int NPC>
+__device__ __forceinline__ void split8(uint16_t* planes, int plane, int o, f32x8 v) {
+  const bfv8 h0 = __builtin_convertvector(v, bfv8);
+  *reinterpret_cast<bfv8*>(planes + o) = h0;
+  if constexpr (NPC > 1) {
+    const f32x8 r1 = v - __builtin_convertvector(h0, f32x8);
+    const bfv8 h1 = __builtin_convertvector(r1, bfv8);
+    const f32x8 r2 = r1 - __builtin_convertvector(h1, f32x8);
+    *reinterpret_cast<bfv8*>(planes + plane + o) = h1;
+    *reinterpret_cast<bfv8*>(planes + 2 * plane + o) = __builtin_convertvector(r2, bfv8);
+  }
+}
+
+// Split-precision GEMM on the bf16 MFMA: A (tokens or +-scale codes) and W are
+// split into three bf16 pieces each and the product keeps the six terms of
+// piece order <= 2 (a0 b0 + a0 b1 + a1 b0 + a1 b1 + a0 b2 + a2 b0, fp32
+// accumulation; the dropped terms are ~2^-24 |a b|: fp32-level accuracy, as
+// k_gemm_x3).  A1: A is exact in bf16 (mode 1 with a bf16-exact scale: +-scale
+// codes), one piece, three products.
+template <int NT, int MODE, int WB, bool A1>
 __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ w,
                                                  const float* __restrict__ bias, int cd, int ncb, float scale,
                                                  int64_t* __restrict__ idx_out, float* __restrict__ out,
-                                                 uint16_t* __restrict__ idx16, InvNorm inv) {
-  constexpr int MT = 1;                            // 16-token M tiles per wave (2 measured slower, see launch_mode)
+                                                 uint16_t* __restrict__ idx16, InvNorm inv,
+                                                 const uint16_t* __restrict__ wsp, int Kp) {
+  constexpr int MT = 1;                            // 16-token M tiles per wave
   constexpr int kThr = 64 * WB;                    // WB waves per block
   constexpr int kTok = kTokW * WB * MT;            // tokens per block
   constexpr int NP = NT * 16;                      // padded output features
-  constexpr int WV = (NP * 4 + kThr - 1) / kThr;   // W float4 per thread and chunk
-  __shared__ __attribute__((aligned(16))) float Ws[2][NP * kLd];   // double-buffered K chunks
-  __shared__ __attribute__((aligned(16))) float As[2][kTok * kLd];
+  constexpr int NPA = A1 ? 1 : 3;                  // A pieces
+  constexpr int kPA = kTok * kKc, kPW = NP * kKc;  // plane sizes (bf16)
+  static_assert(kThr == 4 * kTok, "A staging: one 8-k group per thread");
+  __shared__ __attribute__((aligned(16))) uint16_t As[NPA * kPA];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[3 * kPW];
   __shared__ int64_t Tb[MODE == 1 ? 32 : 1];   // mode 1 + inverse: table rows of a round's 32 tokens
   __shared__ int32_t Ix[MODE == 1 ? kTok * 32 : 1];   // mode 1: the block's indices (ncb <= 32)
   __shared__ uint32_t Msk[MODE == 0 ? WB * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
@@ -80,75 +114,81 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[m][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // A staging: thread tid owns float4 tid & 3 of tokens (tid >> 2) + 64 m
+  // A staging: thread tid owns k group tid & 3 (8 k) of token tid >> 2
   const int at = tid >> 2, aq = tid & 3;
-  float4 ra[MT], rw[WV];
+  // W: the three pre-split bf16 planes [3][NP][Kp] (k_split_w), 16-byte pieces
+  constexpr int WG = (NP * 4 + kThr - 1) / kThr;   // W 8-k groups per thread and chunk
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wsp), 0, 3 * NP * Kp * 2, 0x00020000);
+  f32x8 ra;
+  u32x4 rw[WG][3];
   auto load = [&](int k0) {
-    const int k = k0 + 4 * aq;
+    const int k = k0 + 8 * aq;
+    if (MODE == 0) {
+      const bool ok = at < nt;
+      const float* xr = x + (tok0 + (ok ? at : 0)) * K + k;
+      const float4 lo = ok && k < K ? *reinterpret_cast<const float4*>(xr) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 hi = ok && k + 4 < K ? *reinterpret_cast<const float4*>(xr + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ra = (f32x8){lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    } else {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int tk = at + kTokW * WB * m;
-      if (MODE == 0) {
-        ra[m] = (tk < nt && k < K) ? *reinterpret_cast<const float4*>(x + (tok0 + tk) * K + k)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int kk = k + e;
-          const int c = kk / cd, b = kk - c * cd;
-          const bool bit = kk < K && ((Ix[tk * ncb + (kk < K ? c : 0)] >> (cd - 1 - b)) & 1);
-          v[e] = kk < K ? (bit ? scale : -scale) : 0.f;
-        }
-        ra[m] = make_float4(v[0], v[1], v[2], v[3]);
+      for (int e = 0; e < 8; ++e) {
+        const int kk = k + e;
+        const int c = kk / cd, b = kk - c * cd;
+        const bool bit = kk < K && ((Ix[at * ncb + (kk < K ? c : 0)] >> (cd - 1 - b)) & 1);
+        ra[e] = kk < K ? (bit ? scale : -scale) : 0.f;
       }
     }
 #pragma unroll
-    for (int i = 0; i < WV; ++i) {
-      const int e = tid + kThr * i;
-      const int row = e >> 2, kk = k0 + 4 * (e & 3);
-      rw[i] = (row < N && kk < K) ? *reinterpret_cast<const float4*>(w + (int64_t)row * K + kk)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < WG; ++i) {
+      const int g = tid + kThr * i;
+      const int o = g < NP * 4 ? ((g >> 2) * Kp + k0 + 8 * (g & 3)) * 2 : 0x7ffffff0;
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        rw[i][pc] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, o + pc * NP * Kp * 2, 0, 0));
     }
   };
-  auto store = [&](int bf) {
+  auto store = [&]() {
+    split8<NPA>(As, kPA, poff(at, aq), ra);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) *reinterpret_cast<float4*>(&As[bf][(at + kTokW * WB * m) * kLd + 4 * aq]) = ra[m];
+    for (int i = 0; i < WG; ++i) {
+      const int g = tid + kThr * i;
+      if (g < NP * 4) {
 #pragma unroll
-    for (int i = 0; i < WV; ++i) {
-      const int e = tid + kThr * i;
-      if (e < NP * 4) *reinterpret_cast<float4*>(&Ws[bf][(e >> 2) * kLd + 4 * (e & 3)]) = rw[i];
+        for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(&Ws[pc * kPW + poff(g >> 2, g & 3)]) = rw[i][pc];
+      }
     }
   };
 
-  // wave w owns tokens [16 (w + 4 m), + 16) of the block for m < MT
-  // one barrier per chunk: chunk c is read from buffer c & 1 while chunk c + 1
-  // is written to the other one (whose last readers, chunk c - 1, all passed
-  // the previous barrier)
+  // wave w owns tokens [16 w, + 16) of the block; one 32-k MFMA step per chunk
   load(0);
-  store(0);
+  store();
   __syncthreads();
-  int bf = 0;
-  for (int k0 = 0; k0 < K; k0 += kKc, bf ^= 1) {
+  for (int k0 = 0; k0 < K; k0 += kKc) {
     const bool more = k0 + kKc < K;
     if (more) load(k0 + kKc);
-    float4 a4[MT];
+    bf16x8 a[NPA];
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-      a4[m] = *reinterpret_cast<const float4*>(&As[bf][((wave + WB * m) * kTokW + r) * kLd + 4 * q]);
+    for (int pc = 0; pc < NPA; ++pc) a[pc] = *reinterpret_cast<const bf16x8*>(&As[pc * kPA + poff(wave * kTokW + r, q)]);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const float4 b4 = *reinterpret_cast<const float4*>(&Ws[bf][(t * 16 + r) * kLd + 4 * q]);
+      bf16x8 b[3];
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].x, b4.x, acc[m][t], 0, 0, 0);
-        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].y, b4.y, acc[m][t], 0, 0, 0);
-        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].z, b4.z, acc[m][t], 0, 0, 0);
-        acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[m].w, b4.w, acc[m][t], 0, 0, 0);
+      for (int pc = 0; pc < 3; ++pc) b[pc] = *reinterpret_cast<const bf16x8*>(&Ws[pc * kPW + poff(16 * t + r, q)]);
+      floatx4& c = acc[0][t];
+      if constexpr (!A1) {
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
       }
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
     }
-    if (more) store(bf ^ 1);
     __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
   }
 
   // C/D map: lane l, register v -> token 4 (l >> 4) + v of the M tile, feature 16 t + (l & 15)
@@ -195,7 +235,7 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
         // pieces along each token's 196 contiguous floats (same fp32 ops as
         // dctae_norm_inverse on the stored projection: bit-equal)
         constexpr int WPR = 2;
-        float* stg = &Ws[0][0];   // 2 NP kLd floats >= WPR x 16 x N
+        float* stg = reinterpret_cast<float*>(Ws);   // 6 NP kKc bytes >= WPR x 16 x N floats
         const int N4 = N >> 2;
         for (int rd = 0; rd < WB / WPR; ++rd) {
           __syncthreads();   // the previous round's (or the K loop's) LDS reads are done
@@ -258,12 +298,29 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
   }
 }
 
-template <int MODE, int WB>
+// W (N x K fp32, row-major) -> three bf16 planes [3][NP][Kp], zero padded
+// (rows N .. NP, k K .. Kp): the same round-to-nearest-even split as split8
+__global__ void k_split_w(const float* __restrict__ w, int N, int K, int NP, int Kp, uint16_t* __restrict__ ws) {
+  const int64_t plane = (int64_t)NP * Kp;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < plane; e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / Kp), k = (int)(e - (int64_t)row * Kp);
+    const float v = row < N && k < K ? w[(int64_t)row * K + k] : 0.f;
+    const __bf16 h0 = (__bf16)v;
+    const float r1 = v - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    const float r2 = r1 - (float)h1;
+    ws[e] = __builtin_bit_cast(uint16_t, h0);
+    ws[plane + e] = __builtin_bit_cast(uint16_t, h1);
+    ws[2 * plane + e] = __builtin_bit_cast(uint16_t, (__bf16)r2);
+  }
+}
+
+template <int MODE, int WB, bool A1>
 void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-               uint16_t* idx16, InvNorm inv) {
+               uint16_t* idx16, InvNorm inv, const uint16_t* wsp, int Kp) {
 #define DCTAE_LFQP(T) \
-  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv); break;
+  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB, A1>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp); break;
   switch (nt) {
     DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
     DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
@@ -275,39 +332,56 @@ void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx
 
 }  // namespace
 
+size_t lfq_proj_scratch_bytes(int N, int K) {
+  const size_t NP = (size_t)(N + 15) / 16 * 16, Kp = (size_t)(K + 31) / 32 * 32;
+  return 3 * NP * Kp * sizeof(uint16_t);
+}
+
 template <int MODE>
 static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                         const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-                        uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}) {
-  // 8 waves x 16 tokens per block (the W chunk in LDS shared by 128 tokens; 2
-  // blocks / CU by LDS, 4 waves / SIMD).  Measured on 3,145,728 tokens (196 ->
-  // 208): project_in 2.45 ms / project_out 2.80 ms; 4 waves per block 2.73 /
-  // 3.05; 16 waves 2.51 / 3.23; MT = 2 (32 tokens per wave, half the W LDS
-  // reads per MFMA) at 4 waves: 1 wave / SIMD, 3.91 / 5.37
-  launch_nt<MODE, 8>(nt, dim3((unsigned)((n + 127) / 128)), s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out,
-                     idx16, inv);
+                        uint16_t* wsp, uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}) {
+  // W pre-split once per call (a few microseconds: N x K <= 256 x 256)
+  const int NP = nt * 16, Kp = (K + 31) / 32 * 32;
+  hipLaunchKernelGGL(k_split_w, dim3((NP * Kp + 255) / 256), dim3(256), 0, s, w, N, K, NP, Kp, wsp);
+  // 8 waves x 16 tokens per block (the W chunk in LDS shared by 128 tokens).
+  // Measured with the fp32 MFMA (v_mfma_f32_16x16x4_f32) on 3,145,728 tokens
+  // (196 -> 208): project_in 2.45 ms / project_out 2.80 ms; 4 waves per block
+  // 2.73 / 3.05; 16 waves 2.51 / 3.23; 32 tokens per wave 3.91 / 5.37.  Now on
+  // the split bf16 MFMA.
+  // Mode 1's A (+-scale) is exact in bf16 when scale is: one A piece
+  uint32_t sb;
+  memcpy(&sb, &scale, 4);
+  const dim3 g((unsigned)((n + 127) / 128));
+  if constexpr (MODE == 1) {
+    if ((sb & 0xffffu) == 0) {
+      launch_nt<MODE, 8, true>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp);
+      return;
+    }
+  }
+  launch_nt<MODE, 8, false>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp);
 }
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                           float scale, int64_t* idx, hipStream_t s) {
+                           float scale, int64_t* idx, uint16_t* wsp, hipStream_t s) {
   if (n <= 0) return;
-  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, scale, idx, nullptr);
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, scale, idx, nullptr, wsp);
 }
 
 // the same into the encode's u16 token staging (cd <= 16)
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                             uint16_t* idx, hipStream_t s) {
+                             uint16_t* idx, uint16_t* wsp, hipStream_t s) {
   if (n <= 0) return;
-  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, nullptr, nullptr, idx);
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, nullptr, nullptr, wsp, idx);
 }
 
 // indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                            float scale, float* out, hipStream_t s, const int64_t* ch, const int64_t* pos,
+                            float scale, float* out, uint16_t* wsp, hipStream_t s, const int64_t* ch, const int64_t* pos,
                             const float* med, const float* nb, float eps, int maxph, int maxpw, int* err) {
   if (n <= 0) return;
-  launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out, nullptr,
+  launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out, wsp, nullptr,
                  InvNorm{ch, pos, med, nb, eps, maxph, maxpw, err});
 }
 
