@@ -336,8 +336,13 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * measured slower at these sizes), "chunk_bytes", "workspace_limit" (bytes),
  * "rows_kernel" (3: k_rows512, 2: k_fft_rows2 for 512-wide rows),
  * "sort_kernel" (2: rocPRIM radix, 1: bitonic), "fft_decode" (0/1),
- * "xcd_order" (0/1); profiling only (outputs invalid): "rows_ablate",
- * "t_alias". */
+ * "xcd_order" (0/1), "dec_rows_kernel" (3 / 2), "gemm_x3" (1, default:
+ * the DCT GEMMs on the split-bf16 MFMA kernel k_gemm_x3, fp32-level
+ * accuracy; 0: the fp32 MFMA kernel), "enc512" (0, default / 1: the
+ * persistent XCD-local 512^2 encode, measured slower),
+ * "enc_grid" (its block count, 0 = auto); profiling builds only
+ * (make PROFILING=1; the shipped library returns DCTAE_EUNSUP):
+ * "rows_ablate", "bs_ablate", "t_alias". */
 int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
 
 /* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an
