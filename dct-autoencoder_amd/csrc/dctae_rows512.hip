@@ -17,7 +17,10 @@ struct Rows512Lds {
 // blocks[i] = (image, first row); ablate (profiling builds only, else 0):
 // bit 0 drops every T store, bit 1 replaces the RGB loads
 template <int KW>
-__global__ __launch_bounds__(256) void k_rows512(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+#ifndef DCTAE_ROWS_MINB
+#define DCTAE_ROWS_MINB 1
+#endif
+__global__ __launch_bounds__(256, DCTAE_ROWS_MINB) void k_rows512(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                 const float* __restrict__ rgb, float* __restrict__ ws,
                                                 const float2* __restrict__ tw, const float2* __restrict__ post,
                                                 ColorMats cm, int ablate) {
