@@ -76,7 +76,8 @@ struct dctae_ctx {
   int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
   int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)
   int bs_ablate = 0;                  // profiling only: Bluestein kernels skip 1 loads, 2 FFTs, 4 post (wrong output)
-  int rows_kernel = 3;                // 512-wide rows: 3 = k_rows512 (registers + one LDS transpose), 2 = k_fft_rows2
+  int rows_kernel = 3;                // 512-wide rows: 3 = k_rows512 (registers + one LDS transpose), 4 = its packed-f32
+                                      // form k_rows512pk, 2 = k_fft_rows2
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
@@ -97,6 +98,11 @@ struct dctae_ctx {
   unsigned* enc_sync = nullptr;
   size_t enc_sync_words = 0;
   int enc_grid = 0;   // 0: occupancy x CUs
+  // pipelined 512^2 encode (dctae_encpipe.hip): images per chunk, 0 = off;
+  // launch L = rows of chunk L + columns of chunk L - 1, T in a two-chunk ring
+  int enc_pipe = 0;
+  float* pipe_ring = nullptr;
+  size_t pipe_ring_bytes = 0;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
@@ -806,6 +812,7 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
   if (ctx->proj_ws) hipFree(ctx->proj_ws);
   if (ctx->enc_slots) hipFree(ctx->enc_slots);
+  if (ctx->pipe_ring) hipFree(ctx->pipe_ring);
   if (ctx->enc_sync) hipFree(ctx->enc_sync);
   delete ctx->enc_plan;
   for (auto& p : ctx->pending) {
@@ -870,13 +877,14 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "t_alias" || k == "rows_ablate" || k == "bs_ablate")
     return fail(ctx, DCTAE_EUNSUP, "option " + k + " exists only in a profiling build (make PROFILING=1)");
 #endif
-  else if (k == "rows_kernel" && (value == 2 || value == 3)) ctx->rows_kernel = (int)value;
+  else if (k == "rows_kernel" && value >= 2 && value <= 4) ctx->rows_kernel = (int)value;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "enc512") ctx->enc512 = value != 0;
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "enc_grid" && value >= 0 && value <= (1 << 16)) ctx->enc_grid = (int)value;
+  else if (k == "enc_pipe" && value >= 0 && value <= 4096) ctx->enc_pipe = (int)value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1413,9 +1421,10 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fr[v]) {
         Timer t(ctx, st, "fft_rows");
-        if (v == 1 && ctx->rows_kernel == 3 && cfg->max_patch_w >= 32)
+        if (v == 1 && ctx->rows_kernel >= 3 && cfg->max_patch_w >= 32)
           launch_rows512(dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
-                         ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st, ctx->rows_ablate);
+                         ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st, ctx->rows_ablate,
+                         ctx->rows_kernel == 4);
         else
           launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
                                ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st);
@@ -1475,6 +1484,20 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     launch_enc512((const ImgDesc*)(pd + E.all_desc_off), E.n_img, imgs->rgb_dev, ctx->enc_slots,
                   ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, epj, skc, ctx->enc_sync, grid,
                   ctx->err_dev, s);
+  } else if (E.all512 && ctx->enc_pipe > 0 && ctx->rows_kernel >= 3 && thr_codes && !ctx->t_alias &&
+             !ctx->rows_ablate) {
+    const int C = std::min(ctx->enc_pipe, E.n_img);
+    const size_t need = enc_pipe_ring_bytes(C);
+    if (need > ctx->pipe_ring_bytes) {
+      if (ctx->pipe_ring) HIPCHK(ctx, hipFree(ctx->pipe_ring));
+      ctx->pipe_ring = nullptr;
+      ctx->pipe_ring_bytes = 0;
+      HIPCHK(ctx, hipMalloc((void**)&ctx->pipe_ring, need));
+      ctx->pipe_ring_bytes = need;
+    }
+    Timer t(ctx, s, "enc_pipe");
+    launch_enc_pipe((const ImgDesc*)(pd + E.all_desc_off), E.n_img, C, imgs->rgb_dev, ctx->pipe_ring,
+                    ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, epj, skc, ctx->rows_kernel == 4, s);
   } else {
     for (const ChunkJob& j : E.jobs) {
       do_rows(j, s);

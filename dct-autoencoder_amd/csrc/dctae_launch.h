@@ -106,9 +106,14 @@ void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, in
 void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
                          const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate = 0);
+                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate = 0,
+                    bool packed = false);
 
 int cols7_grid(int n_list, int qw, int ipb);
+size_t enc_pipe_ring_bytes(int C);
+void launch_enc_pipe(const ImgDesc* imgs, int n_img, int C, const float* rgb, float* tring, const float2* tw,
+                     const float2* post, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, bool packed,
+                     hipStream_t s);
 
 // Bluestein DCT for lengths without a Makhoul plan (dctae_bluestein.hip)
 int bs_rows_per_block(int L);

@@ -222,4 +222,160 @@ __device__ __forceinline__ void rows512_item(Rows512Xch& X, const Rows512Tab& L,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Packed-f32 variant (rows_kernel 4).  The same transform as rows512_item with
+// the VALU work issued as v_pk_{mul,fma,add}_f32 (two fp32 lanes per
+// instruction, the 157 TF vector peak; the scalar item is ~2,850 VALU per wave
+// and VALU-bound once T stays on chip):
+//  * IPT: the channel mixes run on pixel pairs (0, 1) / (2, 3) of each float4
+//    (adjacent registers) and write the pairs (0, 2) / (3, 1) -- exactly the
+//    Makhoul (re, im) of z[j + 16 b] and the mirror lane's z[(15 - j) + 16 (15 - b)];
+//    log / exp / copysign stay scalar (no packed form);
+//  * pass 1 / pass 2: DFTV<16> on complex pairs, the transpose as ds_write_b64
+//    (element (k1, lane r) at 16 k1 + (r ^ (k1 & 14))) / ds_read_b128 (lane of
+//    row s reads chunk q at q ^ (s >> 1): 16 distinct 4-bank groups);
+//  * pass 2 lane l runs butterfly s = sigma(l) (l < 8: l; 8 <= l < 15: l + 1;
+//    15: 8) so the Makhoul partner 16 - s sits on the mirror lane 15 - l: one
+//    DPP row_mirror per value (lanes 0 / 15, s = 0 / 8, pair with themselves);
+//  * post: (X[k], X[N - k]) as one pair, four packed FMAs.
+// Same rounding as rows512_item for the IPT (identical fma order per pixel);
+// the FFT differs in operation order only (tolerance-tested).
+// ---------------------------------------------------------------------------
+constexpr int kXchStridePk = 272;   // complex slots per row group: 2 KB + 128 B (row groups 0/1 on opposite bank halves)
+
+struct Rows512XchPk {
+  cf xch[4][4][kXchStridePk];
+};
+
+__device__ __forceinline__ cf splat_mix(const float* m, int i, cf a, cf b, cf c) {
+  // packed mat3_row: fma(m2, c, fma(m1, b, m0 * a)) per half (same rounding)
+  const cf m0 = (cf){m[3 * i], m[3 * i]}, m1 = (cf){m[3 * i + 1], m[3 * i + 1]}, m2 = (cf){m[3 * i + 2], m[3 * i + 2]};
+  return __builtin_elementwise_fma(m2, c, __builtin_elementwise_fma(m1, b, m0 * a));
+}
+
+// (X[k], X[N - k]) = (c1 A.x + c2 P.x - c3 A.y + c4 P.y, -c1 A.y + c2 P.y - c3 A.x - c4 P.x)
+// (the swaps / signs as VOP3P op_sel / neg modifiers; plain vector code
+// materialises them with v_mov / v_xor)
+__device__ __forceinline__ cf makhoul_pair(cf A, cf P, cf c12, cf c34) {
+  cf t;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0] neg_hi:[1,0]" : "=v"(t) : "v"(A), "v"(c12));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(t) : "v"(P), "v"(c12), "v"(t));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+      : "=v"(t) : "v"(A), "v"(c34), "v"(t));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+      : "=v"(t) : "v"(P), "v"(c34), "v"(t));
+  return t;
+}
+
+__device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Tab& L, const float* __restrict__ img,
+                                                int H, int y0, float* T, uint32_t plane_bytes, const ColorMats& cm) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KW = 448;
+  const int tid = threadIdx.x;
+  const int wv = tid >> 6, g = (tid >> 4) & 3, j = tid & 15;
+  const int y = y0 + 4 * wv + g;
+  const int yl = min(y, H - 1);
+  const int64_t hw = (int64_t)H * N;
+  const float* src = img + (int64_t)yl * N + 4 * j;
+
+  float4 I[3][8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    I[0][b] = *reinterpret_cast<const float4*>(src + 64 * b);
+    I[1][b] = *reinterpret_cast<const float4*>(src + hw + 64 * b);
+    I[2][b] = *reinterpret_cast<const float4*>(src + 2 * hw + 64 * b);
+  }
+  // ---- IPT (util.py:70-82): A[c][b] = (ipt_c(x0), ipt_c(x2)), B[c][b] = (ipt_c(x3), ipt_c(x1))
+  cf A[3][8], B[3][8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const cf r01 = (cf){I[0][b].x, I[0][b].y}, r23 = (cf){I[0][b].z, I[0][b].w};
+    const cf g01 = (cf){I[1][b].x, I[1][b].y}, g23 = (cf){I[1][b].z, I[1][b].w};
+    const cf b01 = (cf){I[2][b].x, I[2][b].y}, b23 = (cf){I[2][b].z, I[2][b].w};
+    cf p02[3], p31[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const cf l01 = splat_mix(cm.rgb2lms, i, r01, g01, b01);
+      const cf l23 = splat_mix(cm.rgb2lms, i, r23, g23, b23);
+      // sign(x) |x|^0.43 (util.py:76-78): log scalar, the 0.43 scale packed, exp / copysign scalar
+      const cf lg01 = (cf){__builtin_amdgcn_logf(fabsf(l01.x)), __builtin_amdgcn_logf(fabsf(l01.y))};
+      const cf lg23 = (cf){__builtin_amdgcn_logf(fabsf(l23.x)), __builtin_amdgcn_logf(fabsf(l23.y))};
+      const cf k = (cf){0.430000007152557373046875f, 0.430000007152557373046875f};
+      const cf e01 = k * lg01, e23 = k * lg23;
+      p02[i] = (cf){__builtin_copysignf(__builtin_amdgcn_exp2f(e01.x), l01.x),
+                    __builtin_copysignf(__builtin_amdgcn_exp2f(e23.x), l23.x)};
+      p31[i] = (cf){__builtin_copysignf(__builtin_amdgcn_exp2f(e23.y), l23.y),
+                    __builtin_copysignf(__builtin_amdgcn_exp2f(e01.y), l01.y)};
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      A[c][b] = splat_mix(cm.lms2ipt, c, p02[0], p02[1], p02[2]);
+      B[c][b] = splat_mix(cm.lms2ipt, c, p31[0], p31[1], p31[2]);
+    }
+  }
+
+  cf* xr = X.xch[wv][g];
+  const int s = j < 8 ? j : (j < 15 ? j + 1 : 8);   // sigma(j)
+  const bool self0 = (j == 0), self8 = (j == 15);
+  // T stores of butterfly s: X[s + 16 i] at + 64 i, X[N - s - 16 i] at + 64 (15 - i)
+  const int rowo = (y * KW + s) * 4;
+  const int rown = (y * KW + (N - 15 * 16) - s) * 4;
+  const int rown4 = s >= 1 ? rown : 0x7ffffff0;   // i = 4: k = 64 + s, X[N - k] kept iff s >= 1
+
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    // ---- pass 1: lane j's z[j + 16 r]
+    cf v[16];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      v[b] = A[c][b];
+      v[15 - b] = (cf){mirror16(B[c][b].x), mirror16(B[c][b].y)};
+    }
+    DFTV<16>::run(v);
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) xr[16 * k1 + (j ^ (k1 & 14))] = v[k1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- pass 2: butterfly s reads z1[s + 16 r] = lane r's output s
+    {
+      const float4* rr = reinterpret_cast<const float4*>(xr + 16 * s);
+      const int sw = s >> 1;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 a = rr[q ^ sw];
+        v[2 * q] = (cf){a.x, a.y};
+        v[2 * q + 1] = (cf){a.z, a.w};
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();   // reads done before the next channel's writes
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      const float2 w = L.tw2[r][s];
+      v[r] = cmul_pk(v[r], (cf){w.x, w.y});
+    }
+    DFTV<16>::run(v);
+    // ---- Makhoul post: k = s + 16 i, A = Z[k] = v[i], P = Z[M - k]
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(T + (int64_t)c * H * KW, 0, plane_bytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const cf m = (cf){mirror16(v[15 - i].x), mirror16(v[15 - i].y)};
+      const cf own = self0 ? v[(16 - i) & 15] : v[15 - i];
+      const cf P = (self0 || self8) ? own : m;
+      const float4 cc = L.pc[s + 16 * i];
+      const cf xx = makhoul_pair(v[i], P, (cf){cc.x, cc.y}, (cf){cc.z, cc.w});
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xx.x), rsrc, rowo, 64 * i, 0);
+      if (i >= 5) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xx.y), rsrc, rown, 64 * (15 - i), 0);
+      if (i == 4) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xx.y), rsrc, rown4, 64 * 11, 0);
+    }
+    // k = M (s = 0, lane 0): A = P = Z[0]: X[M] = (c1 + c2) Z0.x + (c4 - c3) Z0.y
+    {
+      const float4 cc = L.pc[M];
+      const float xm = (cc.x + cc.y) * v[0].x + (cc.w - cc.z) * v[0].y;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xm), rsrc, self0 ? (y * KW + M) * 4 : 0x7ffffff0, 0, 0);
+    }
+  }
+}
+
 }  // namespace dctae

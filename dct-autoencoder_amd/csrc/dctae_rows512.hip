@@ -40,10 +40,27 @@ __global__ __launch_bounds__(256, DCTAE_ROWS_MINB) void k_rows512(const ImgDesc*
   rows512_item<0>(L.x, L.t, rgb + d.rgb_off, d.H, jb.y, ws + d.ws_t, plane_bytes, cm);
 }
 
+// rows_kernel 4: the packed-f32 item (dctae_rows512.h rows512_item_pk)
+__global__ __launch_bounds__(256) void k_rows512pk(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                                                   const float* __restrict__ rgb, float* __restrict__ ws,
+                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                   ColorMats cm) {
+  __shared__ Rows512XchPk x;
+  __shared__ Rows512Tab t;
+  rows512_tables(t, tw, post);
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  __syncthreads();   // tables
+  rows512_item_pk(x, t, rgb + d.rgb_off, d.H, jb.y, ws + d.ws_t, (uint32_t)(d.H * 448 * 4), cm);
+}
+
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate) {
+                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate, bool packed) {
   if (n_blocks <= 0) return;
-  hipLaunchKernelGGL(k_rows512<448>, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm, ablate);
+  if (packed && !ablate)
+    hipLaunchKernelGGL(k_rows512pk, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+  else
+    hipLaunchKernelGGL(k_rows512<448>, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm, ablate);
 }
 
 }  // namespace dctae

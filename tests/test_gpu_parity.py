@@ -571,6 +571,7 @@ DEFAULTS = {"rows_kernel": 3, "sort_kernel": 2, "chunk_bytes": 1 << 40}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "rows_lds": {"rows_kernel": 2},
+    "rows_pk": {"rows_kernel": 4},
     "sort_bitonic": {"sort_kernel": 1},
     "chunks": {"chunk_bytes": 4 << 20},
 }
