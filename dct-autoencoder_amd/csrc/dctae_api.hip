@@ -76,8 +76,8 @@ struct dctae_ctx {
   int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
   int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)
   int bs_ablate = 0;                  // profiling only: Bluestein kernels skip 1 loads, 2 FFTs, 4 post (wrong output)
-  int rows_kernel = 3;                // 512-wide rows: 3 = k_rows512 (registers + one LDS transpose), 4 = its packed-f32
-                                      // form k_rows512pk, 2 = k_fft_rows2
+  int rows_kernel = 4;                // 512-wide rows: 4 = k_rows512pk (packed-f32 VALU; 1.13 vs 1.155 ms per 1024 images),
+                                      // 3 = k_rows512 (scalar), 2 = k_fft_rows2
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
@@ -1468,7 +1468,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   // with the exact LFQ thresholds (14 codebooks of 14 bits, the cols7 epilogue)
   const bool thr_codes = epj.median && epj.thr && !skc.norm && !skc.raw && skc.codes && epj.maxph <= 32 &&
                          epj.cb_dim == 14 && epj.ncb == 14;
-  if (E.all512 && ctx->enc512 && ctx->rows_kernel == 3 && thr_codes && !ctx->t_alias && !ctx->rows_ablate) {
+  if (E.all512 && ctx->enc512 && ctx->rows_kernel >= 3 && thr_codes && !ctx->t_alias && !ctx->rows_ablate) {
     const size_t words = enc512_sync_words(E.n_img);
     if (!ctx->enc_slots) {
       HIPCHK(ctx, hipMalloc((void**)&ctx->enc_slots, enc512_slot_bytes()));

@@ -162,11 +162,12 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
     for (int e = tid; e < (N - KS * 32) * KS; e += 256) L.x[KS * 32 * KS + e] = 0.0f;
   }
   __syncthreads();
-  const int jj = tid & 15, col = tid >> 4;
-  const bool on_col = col < KS;
+  // lanes of columns 14 / 15 (tid >= 224) redo column 13: same reads, same
+  // values, same stores (no divergent branches)
+  const int jj = tid & 15, col = min(tid >> 4, KS - 1);
   // ---- 2. conj Z_k, k = jj + 16 i
   cf zk[16];
-  if (on_col) {
+  {
     const float* xc = L.x + col;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -181,10 +182,10 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
   // ---- 3. forward FFT of conj Z (radix 16 x 16, Stockham).  Pass 1's item
   // jj reads z[jj + 16 r] = this lane's zk[r]: it runs on the registers
   // (no LDS round trip); its outputs go to z[16 jj + r] for pass 2.
-  if (on_col) DFTV<16>::run(zk);
+  DFTV<16>::run(zk);
   __syncthreads();   // every wave's X reads (step 2) before z (aliased on X) is written
   const cf* zr = reinterpret_cast<const cf*>(L.z) + 15 * jj + col;   // z[jj + 16 r]
-  if (on_col) {
+  {
     cf* zw = reinterpret_cast<cf*>(L.z) + S16 * jj + col;
 #pragma unroll
     for (int r = 0; r < 16; ++r) zw[15 * r] = zk[r];
@@ -192,7 +193,7 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
   __syncthreads();
   {
     cf v[16];
-    if (on_col) {
+    {
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = zr[S16 * r];
 #pragma unroll
@@ -204,7 +205,7 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
     }
     __syncthreads();
     // ---- 4. w[jj + 16 r] -> x rows (natural), z = conj w
-    if (on_col) {
+    {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = jj + 16 * r;

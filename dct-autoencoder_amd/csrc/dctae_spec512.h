@@ -77,12 +77,16 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
         for (int p = 0; p < KS / 2; ++p) {
           const f2v v2 = row[p];
           am = max(am, max(__float_as_uint(v2.x) & 0x7fffffffu, __float_as_uint(v2.y) & 0x7fffffffu));
-          code |= (v2.x >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
-          code |= (v2.y >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
+          // MSB-first (lfq.py:187): code = 2 code + bit (v_cmp + v_addc with the compare's carry)
+          code = 2 * code + (v2.x >= thr_r[r][p].x ? 1u : 0u);
+          code = 2 * code + (v2.y >= thr_r[r][p].y ? 1u : 0u);
         }
         am = jl < KS ? am : 0u;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
+        // max over the 16-lane row: DPP row rotations by 8, 4, 2, 1 (no LDS permutes)
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x128, 0xf, 0xf, false));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x124, 0xf, 0xf, false));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x122, 0xf, 0xf, false));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x121, 0xf, 0xf, false));
         const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
         if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
         if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
@@ -189,7 +193,7 @@ __device__ __forceinline__ float partner_row(float x, bool even_row) {
 // X aliases z (one more barrier, 37 KB instead of 62 KB: 4 workgroups per CU)
 union Cols7Lds {
   float2 z[256 * 16];
-  float X[448 * 14];
+  float X[449 * 14];   // 448 kept rows + a spare row (the post's unconditional X[448] store)
 };
 
 // Makhoul post of cols7 for one lane: v = Z[j2 + 16 i]; writes X[k], X[N - k]
@@ -200,10 +204,12 @@ __device__ __forceinline__ void cols7_post(const cf (&v)[16], int j2, int g, int
                                            float* Xs) {
 #pragma clang fp contract(fast)
   constexpr int N = 512, M = 256, KS = 14;
-  const bool on_col = col < KS;
+  // lanes 14 / 15 loaded column 13 (cols7_load clamps) and hold its values:
+  // they store the same values to the same slots (no divergent branches)
+  const int colc = col < KS ? col : KS - 1;
   const bool self = W0 && g < 2;
-  float* xa = Xs + j2 * KS + col;                        // X[j2 + 16 i] at + 224 i
-  float* xb = Xs + (N - j2 - 16 * 15) * KS + col;        // X[N - j2 - 16 i] at + 224 (15 - i)
+  float* xa = Xs + j2 * KS + colc;                       // X[j2 + 16 i] at + 224 i
+  float* xb = Xs + (N - j2 - 16 * 15) * KS + colc;       // X[N - j2 - 16 i] at + 224 (15 - i)
   const float4* ps = post4 + j2;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -216,17 +222,16 @@ __device__ __forceinline__ void cols7_post(const cf (&v)[16], int j2, int g, int
     const cf al = (cf){ab.x, ab.y}, be = (cf){ab.z, ab.w};
     const cf s1 = add_conj(A, P), d1 = sub_conj(A, P);
     const cf W = fma_iw(d1, be, fma_x(d1, be, fma_iw(s1, al, mul_x(s1, al))));
-    if (on_col) {
-      xa[224 * i] = W.x;
-      if (i > 4 || (i == 4 && j2 > 0)) xb[224 * (15 - i)] = -W.y;
-    }
+    xa[224 * i] = W.x;
+    // i = 4, j2 = 0: k = 64, X[N - k] = X[448] is past Kh: the spare row
+    if (i >= 4) xb[224 * (15 - i)] = -W.y;
   }
-  if (W0 && j2 == 0 && on_col) {   // k = M (< Kh): A = B = Z[0]
+  if (W0 && j2 == 0) {   // k = M (< Kh): A = B = Z[0]
     const cf A = v[0];
     const float4 ab = post4[M];
     const cf s1 = add_conj(A, A), d1 = sub_conj(A, A);
     const cf W = fma_iw(d1, (cf){ab.z, ab.w}, fma_x(d1, (cf){ab.z, ab.w}, cmul_pk(s1, (cf){ab.x, ab.y})));
-    Xs[M * KS + col] = W.x;
+    Xs[M * KS + colc] = W.x;
   }
 }
 
@@ -239,7 +244,6 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
   constexpr int KS = 14;
   const int tid = opaque_tid();
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), g = (tid >> 4) & 3, col = tid & 15;
-  const bool on_col = col < KS;
   cf* z = reinterpret_cast<cf*>(L.z);
   (void)d;
   // ---- pass 1 (Ns = 1): j1 = tid >> 4
@@ -249,11 +253,10 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = (cf){va[r], vb[r]};
     DFTV<16>::run(v);
-    if (on_col) {
-      cf* zw = z + col;
+    // lanes 14 / 15 (duplicates of column 13) fill z's own columns 14 / 15
+    cf* zw = z + col;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) zw[z7addr(16 * j1 + r)] = v[r];
-    }
+    for (int r = 0; r < 16; ++r) zw[z7addr(16 * j1 + r)] = v[r];
   }
   __syncthreads();
   // ---- pass 2 (Ns = 16): z[j2 + 16 r] * W_M^{r j2} -> DFT16 -> Z[j2 + 16 r]
@@ -276,9 +279,24 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
   //      j2 >= 1: Z[M - k] = partner row's v[15 - i] (lane ^ 16, ds_swizzle);
   //      j2 = 0: own v[(16 - i) & 15];  j2 = 8: own v[15 - i]  (wave 0, rows 0 and 1)
   //      kept rows: Kh = 448 (H = 512): X[k] always, X[N - k] for k > 64
+#if defined(DCTAE_PROFILING) && defined(DCTAE_C7_ABL)
+  // profiling ablations (wrong outputs): bit 0 no token epilogue, bit 1 no
+  // Makhoul post either (pass-2 results summed into one LDS word per lane)
+  if (DCTAE_C7_ABL & 2) {
+    cf acc = v[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) acc += v[i];
+    L.X[tid] = acc.x + acc.y;
+    __syncthreads();
+    return;
+  }
+#endif
   if (w == 0) cols7_post<true>(v, j2, g, col, post4, L.X);
   else cols7_post<false>(v, j2, g, col, post4, L.X);
   __syncthreads();
+#if defined(DCTAE_PROFILING) && defined(DCTAE_C7_ABL)
+  if (DCTAE_C7_ABL & 1) return;
+#endif
   cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sbias, thr_r, ep, sk);
 }
 

@@ -39,6 +39,7 @@ def _run(setup, B, enc512, grid=0, seed=1234, first=0):
     x = ops.synth_images(B, 512, 512, seed=seed, first_index=first, device=dev)
     ops.set_option("enc512", enc512, dev)
     ops.set_option("enc_grid", grid, dev)
+    ops.set_option("rows_kernel", 3, dev)   # k_enc512 runs the scalar row item (rows512_item)
     try:
         enc = fe_mod.BatchEncoder(fe, B, 512, 512, pn, lfq, device=dev)
         out = {k: v.clone() for k, v in enc(x).items()}
@@ -47,6 +48,7 @@ def _run(setup, B, enc512, grid=0, seed=1234, first=0):
     finally:
         ops.set_option("enc512", 0, dev)
         ops.set_option("enc_grid", 0, dev)
+        ops.set_option("rows_kernel", 4, dev)
     return out
 
 

@@ -33,7 +33,7 @@ def _run(setup, B, opts, seed):
     ops, fe_mod, fe, pn, lfq = setup
     dev = torch.device(DEV, torch.cuda.current_device())
     x = ops.synth_images(B, 512, 512, seed=seed, device=dev)
-    saved = {"enc_pipe": 0, "rows_kernel": 3}
+    saved = {"enc_pipe": 0, "rows_kernel": 4}
     for k, v in opts.items():
         ops.set_option(k, v, dev)
     try:
