@@ -112,6 +112,11 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
   constexpr int N = 512, M = 256, KS = 14, S16 = 257, PP = KS * KS;
   const int tid = itid();
   // ---- 1. tokens -> X rows 14 h + jl (tile h = g16 + 16 r)
+#if defined(DCTAE_PROFILING) && defined(DCTAE_IC_ABL)
+  if (DCTAE_IC_ABL & 1) {   // profiling ablation: no token loads / expansion (wrong output)
+    for (int e = tid; e < N * KS; e += 256) L.x[e] = 0.001f * (e & 63);
+  } else
+#endif
   {
     const int g16 = tid >> 4, jl = tid & 15;
     int32_t sl[2];
@@ -218,6 +223,12 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
     __syncthreads();
   }
   // ---- 5. U[c][y][14 strip + 2p, +1] for rows y = y0 + 32 k
+#if defined(DCTAE_PROFILING) && defined(DCTAE_IC_ABL)
+  if (DCTAE_IC_ABL & 2) {   // profiling ablation: no U stores (wrong output)
+    __syncthreads();
+    return;
+  }
+#endif
   if (tid < 32 * (KS / 2)) {
     const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
     f2v* dst = reinterpret_cast<f2v*>(ws + d.ws_t + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;

@@ -29,6 +29,16 @@ __device__ __forceinline__ void cols_thresholds(const ImgDesc& d, int c, int str
   constexpr int KS = 14, EPR = 2;
   const int tid = opaque_tid();
   const int g16 = tid >> 4, jl = tid & 15;
+#if defined(DCTAE_PROFILING) && defined(DCTAE_C7_ABL)
+  if (DCTAE_C7_ABL & 4) {   // profiling ablation: constant thresholds, no table loads (wrong codes)
+#pragma unroll
+    for (int r = 0; r < EPR; ++r)
+#pragma unroll
+      for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = make_float2(0.001f * (p + r), -0.002f * (p + jl));
+    if (tid < 32) sbias[tid] = 0.0f;
+    return;
+  }
+#endif
   if (THR) {
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
