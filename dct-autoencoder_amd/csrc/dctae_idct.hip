@@ -177,10 +177,14 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int k = jj + 16 * i;
-      float yk = xc[xrow(k) * KS];
-      const float ynk = k == 0 ? 0.0f : xc[xrow(N - k) * KS];
+      // xrow(M + y) = M + xrow(y) for y < M: rows k / M + k and M - k / N - k
+      // are M * KS floats apart -> one ds_read2st64_b32 per pair
+      const float* pk = xc + xrow(k) * KS;
+      const float* pm = xc + xrow(M - k) * KS;   // k = 0: row M (its N - k partner is not read)
+      float yk = pk[0];
+      const float ymk = pk[M * KS], ymk2 = pm[0];
+      const float ynk = k == 0 ? 0.0f : pm[M * KS];
       if (k == 0) yk *= 1.41421356237309515f;
-      const float ymk = xc[xrow(M + k) * KS], ymk2 = xc[xrow(M - k) * KS];
       zk[i] = pre_z(yk, ynk, ymk, ymk2, pre_s[k]);
     }
   }
