@@ -101,6 +101,7 @@ struct dctae_ctx {
   // pipelined 512^2 encode (dctae_encpipe.hip): images per chunk, 0 = off;
   // launch L = rows of chunk L + columns of chunk L - 1, T in a two-chunk ring
   int enc_pipe = 0;
+  int sort_grid = 0;                  // k_sort_pack2 blocks (grid-stride over images); 0 = one per image
   float* pipe_ring = nullptr;
   size_t pipe_ring_bytes = 0;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
@@ -885,6 +886,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "enc_grid" && value >= 0 && value <= (1 << 16)) ctx->enc_grid = (int)value;
   else if (k == "enc_pipe" && value >= 0 && value <= 4096) ctx->enc_pipe = (int)value;
+  else if (k == "sort_grid" && value >= 0 && value <= (1 << 20)) ctx->sort_grid = (int)value;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1522,7 +1524,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       eps.code_neg = (uint32_t)neg;
     }
     launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), eps, sk, ps, s,
-                     ctx->sort_kernel, E.max_T);
+                     ctx->sort_kernel, E.max_T, ctx->sort_grid);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);

@@ -28,7 +28,7 @@ void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, i
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
-                      const PackSinks& out, hipStream_t s, int kernel = 1, int max_T = 1 << 30);
+                      const PackSinks& out, hipStream_t s, int kernel = 1, int max_T = 1 << 30, int grid = 0);
 void launch_pad_fill(const int32_t* row_len, int n_rows, const EncParams& ep, uint8_t* key_pad,
                      const PackSinks& out, hipStream_t s);
 void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t n, int PP, int maxph, int maxpw,

@@ -77,3 +77,18 @@ def test_packed_rows_close_to_scalar_rows(setup):
             assert torch.equal(a[k], b[k]), k
     diff = (a["codes"] != b["codes"]).sum().item()
     assert diff <= 8, diff
+
+
+@pytest.mark.parametrize("grid", [1, 7, 256])
+def test_sort_grid_stride_matches(setup, grid):
+    """k_sort_pack2 with fewer blocks than images (grid-stride loop, option
+    sort_grid) writes the same packed rows as one block per image"""
+    ops = setup[0]
+    dev = torch.device(DEV, torch.cuda.current_device())
+    ref = _run(setup, 40, {}, seed=24)
+    ops.set_option("sort_grid", grid, dev)
+    try:
+        got = _run(setup, 40, {}, seed=24)
+    finally:
+        ops.set_option("sort_grid", 0, dev)
+    _same(got, ref)
