@@ -102,6 +102,9 @@ struct dctae_ctx {
   // launch L = rows of chunk L + columns of chunk L - 1, T in a two-chunk ring
   int enc_pipe = 0;
   int sort_grid = 0;                  // k_sort_pack2 blocks (grid-stride over images); 0 = one per image
+  // 512^2 batches: the column FFT's first pass in the row kernel (k_rows512p1
+  // + k_fft_cols7p2); 0 = k_rows512pk + k_fft_cols7
+  int rows_p1 = 0;
   float* pipe_ring = nullptr;
   size_t pipe_ring_bytes = 0;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
@@ -887,6 +890,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "enc_grid" && value >= 0 && value <= (1 << 16)) ctx->enc_grid = (int)value;
   else if (k == "enc_pipe" && value >= 0 && value <= 4096) ctx->enc_pipe = (int)value;
   else if (k == "sort_grid" && value >= 0 && value <= (1 << 20)) ctx->sort_grid = (int)value;
+  else if (k == "rows_p1") ctx->rows_p1 = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1502,6 +1506,18 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                     ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, epj, skc, ctx->rows_kernel == 4, s);
   } else {
     for (const ChunkJob& j : E.jobs) {
+      const int nj = j.i1 - j.i0;
+      if (E.all512 && ctx->rows_p1 && j.n_pc == nj && !ctx->t_alias && !ctx->rows_ablate) {
+        const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
+        {
+          Timer t(ctx, s, "fft_rows");
+          launch_rows512p1(dd, nj, imgs->rgb_dev, ctx->ws, ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, s);
+        }
+        Timer t(ctx, s, "fft_cols");
+        launch_fft_cols7p2(dd, (const int*)(pd + j.pc_off), j.n_pc, j.pc_qw, ctx->ws, ctx->fft_tab + E.tw512,
+                           ctx->fft_tab + E.post512, epj, skc, s);
+        continue;
+      }
       do_rows(j, s);
       do_cols(j, s);
     }

@@ -111,6 +111,10 @@ void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const
 
 int cols7_grid(int n_list, int qw, int ipb);
 size_t enc_pipe_ring_bytes(int C);
+void launch_rows512p1(const ImgDesc* imgs, int n_img, const float* rgb, float* ws, const float2* tw,
+                      const float2* post, const ColorMats& cm, hipStream_t s);
+void launch_fft_cols7p2(const ImgDesc* imgs, const int* list, int n_list, int qw, const float* ws, const float2* tw,
+                        const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
 void launch_enc_pipe(const ImgDesc* imgs, int n_img, int C, const float* rgb, float* tring, const float2* tw,
                      const float2* post, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, bool packed,
                      hipStream_t s);

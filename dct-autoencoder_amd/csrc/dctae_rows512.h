@@ -379,3 +379,160 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
 }
 
 }  // namespace dctae
+
+namespace dctae {
+
+// ---------------------------------------------------------------------------
+// Row pass + the column FFT's first pass (option rows_p1, k_rows512p1): one
+// 512-thread block = the 32 rows of column butterfly j1 of one image,
+//   q = 2 r + sub (r < 16, sub < 2), m = j1 + 16 r:
+//   r < 8: row 4 m + 2 sub;  r >= 8: row 1023 - 4 m - 2 sub
+// (exactly the rows the column kernel's pass-1 butterfly j1 reads: z[m] =
+// (T[row(q = 2r)], T[row(q = 2r + 1)]) column by column).  Per channel: the
+// row transform of rows512_item_pk, its 448 kept coefficients into the row
+// group's own LDS region (aliasing its transpose buffer), a block barrier,
+// then thread kx < 448 runs the column DFT16 over r and stores the 16
+// outputs Y_j1[k1] as P1[c][j1][k1][kx] (float2; 448 contiguous per (c, j1,
+// k1): coalesced).  P1 has T's size and takes T's workspace slot; the column
+// kernel (k_fft_cols7p2) starts at pass 2.  Same arithmetic as
+// k_rows512pk + k_fft_cols7, so the outputs are bit-identical.
+// ---------------------------------------------------------------------------
+struct Rows512P1Lds {
+  cf xch[8][4][kXchStridePk];   // [wave][row group]: row transposes, then the row's 448 coefficients
+  Rows512Tab t;
+};
+
+__device__ __forceinline__ void rows512_p1_tables(Rows512Tab& L, const float2* __restrict__ tw,
+                                                  const float2* __restrict__ post) {
+  const int tid = threadIdx.x;
+  if (tid < 256) L.tw2[tid >> 4][tid & 15] = tw[(tid >> 4) * (tid & 15)];
+  const float4* p4 = reinterpret_cast<const float4*>(post);
+  for (int i = tid; i < 257; i += 512) {
+    const float4 ab = p4[i];
+    L.pc[i] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
+  }
+}
+
+__device__ __forceinline__ void rows512_p1_item(Rows512P1Lds& X, const float* __restrict__ img, int j1,
+                                                float2* __restrict__ P1, const ColorMats& cm) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KW = 448;
+  const int tid = threadIdx.x;
+  const int wv = tid >> 6, g = (tid >> 4) & 3, j = tid & 15;
+  const int q = 4 * wv + g, r = q >> 1, sub = q & 1;
+  const int m = j1 + 16 * r;
+  const int y = r < 8 ? 4 * m + 2 * sub : 1023 - 4 * m - 2 * sub;
+  const int64_t hw = (int64_t)N * N;
+  const float* src = img + (int64_t)y * N + 4 * j;
+
+  float4 I[3][8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    I[0][b] = *reinterpret_cast<const float4*>(src + 64 * b);
+    I[1][b] = *reinterpret_cast<const float4*>(src + hw + 64 * b);
+    I[2][b] = *reinterpret_cast<const float4*>(src + 2 * hw + 64 * b);
+  }
+  cf A[3][8], B[3][8];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const cf r01 = (cf){I[0][b].x, I[0][b].y}, r23 = (cf){I[0][b].z, I[0][b].w};
+    const cf g01 = (cf){I[1][b].x, I[1][b].y}, g23 = (cf){I[1][b].z, I[1][b].w};
+    const cf b01 = (cf){I[2][b].x, I[2][b].y}, b23 = (cf){I[2][b].z, I[2][b].w};
+    cf p02[3], p31[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const cf l01 = splat_mix(cm.rgb2lms, i, r01, g01, b01);
+      const cf l23 = splat_mix(cm.rgb2lms, i, r23, g23, b23);
+      const cf lg01 = (cf){__builtin_amdgcn_logf(fabsf(l01.x)), __builtin_amdgcn_logf(fabsf(l01.y))};
+      const cf lg23 = (cf){__builtin_amdgcn_logf(fabsf(l23.x)), __builtin_amdgcn_logf(fabsf(l23.y))};
+      const cf k = (cf){0.430000007152557373046875f, 0.430000007152557373046875f};
+      const cf e01 = k * lg01, e23 = k * lg23;
+      p02[i] = (cf){__builtin_copysignf(__builtin_amdgcn_exp2f(e01.x), l01.x),
+                    __builtin_copysignf(__builtin_amdgcn_exp2f(e23.x), l23.x)};
+      p31[i] = (cf){__builtin_copysignf(__builtin_amdgcn_exp2f(e23.y), l23.y),
+                    __builtin_copysignf(__builtin_amdgcn_exp2f(e01.y), l01.y)};
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      A[c][b] = splat_mix(cm.lms2ipt, c, p02[0], p02[1], p02[2]);
+      B[c][b] = splat_mix(cm.lms2ipt, c, p31[0], p31[1], p31[2]);
+    }
+  }
+
+  cf* xr = X.xch[wv][g];
+  float* xl = reinterpret_cast<float*>(xr);   // the row's kept coefficients (after pass 2's reads)
+  const int s = j < 8 ? j : (j < 15 ? j + 1 : 8);
+  const bool self0 = (j == 0), self8 = (j == 15);
+  // this thread's column in the column pass
+  const int kx = tid;
+  const bool colt = kx < KW;
+
+#pragma unroll 1
+  for (int c = 0; c < 3; ++c) {
+    cf v[16];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      v[b] = A[c][b];
+      v[15 - b] = (cf){mirror16(B[c][b].x), mirror16(B[c][b].y)};
+    }
+    DFTV<16>::run(v);
+    if (c > 0) __syncthreads();   // the previous channel's column-pass reads of every row region
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) xr[16 * k1 + (j ^ (k1 & 14))] = v[k1];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+      const float4* rr = reinterpret_cast<const float4*>(xr + 16 * s);
+      const int sw = s >> 1;
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) {
+        const float4 a = rr[qq ^ sw];
+        v[2 * qq] = (cf){a.x, a.y};
+        v[2 * qq + 1] = (cf){a.z, a.w};
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();   // pass-2 reads done before the coefficients overwrite the region
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int rr2 = 1; rr2 < 16; ++rr2) {
+      const float2 w = X.t.tw2[rr2][s];
+      v[rr2] = cmul_pk(v[rr2], (cf){w.x, w.y});
+    }
+    DFTV<16>::run(v);
+    // ---- Makhoul post -> the row's kept coefficients in LDS
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const cf mm = (cf){mirror16(v[15 - i].x), mirror16(v[15 - i].y)};
+      const cf own = self0 ? v[(16 - i) & 15] : v[15 - i];
+      const cf P = (self0 || self8) ? own : mm;
+      const float4 cc = X.t.pc[s + 16 * i];
+      const cf xx = makhoul_pair(v[i], P, (cf){cc.x, cc.y}, (cf){cc.z, cc.w});
+      xl[s + 16 * i] = xx.x;
+      // X[N - k] kept for k > 64; i = 4, s = 0 (k = 64) lands on slot 448, past the kept row
+      if (i >= 4) xl[N - s - 16 * i] = xx.y;
+    }
+    if (self0) {
+      const float4 cc = X.t.pc[M];
+      xl[M] = (cc.x + cc.y) * v[0].x + (cc.w - cc.z) * v[0].y;
+    }
+    __syncthreads();   // every row's coefficients of channel c
+    // ---- column pass 1: z[r'] = (row q = 2 r', row 2 r' + 1) of column kx, DFT16 over r'
+    if (colt) {
+      cf z[16];
+#pragma unroll
+      for (int r2 = 0; r2 < 16; ++r2) {
+        const float* a = reinterpret_cast<const float*>(X.xch[r2 >> 1][(2 * r2) & 3]);
+        const float* b2 = reinterpret_cast<const float*>(X.xch[r2 >> 1][(2 * r2 + 1) & 3]);
+        z[r2] = (cf){a[kx], b2[kx]};
+      }
+      DFTV<16>::run(z);
+      float2* dst = P1 + ((int64_t)(c * 16 + j1) * 16) * KW + kx;
+#pragma unroll
+      for (int k1 = 0; k1 < 16; ++k1) dst[k1 * KW] = make_float2(z[k1].x, z[k1].y);
+    }
+  }
+}
+
+}  // namespace dctae

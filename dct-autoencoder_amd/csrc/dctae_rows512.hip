@@ -54,6 +54,27 @@ __global__ __launch_bounds__(256) void k_rows512pk(const ImgDesc* __restrict__ i
   rows512_item_pk(x, t, rgb + d.rgb_off, d.H, jb.y, ws + d.ws_t, (uint32_t)(d.H * 448 * 4), cm);
 }
 
+// rows_p1: the row pass + the column FFT's pass 1 (dctae_rows512.h
+// rows512_p1_item); blocks[i] = (image, j1), 512 threads
+__global__ __launch_bounds__(512) void k_rows512p1(const ImgDesc* __restrict__ imgs, int n_img,
+                                                   const float* __restrict__ rgb, float* __restrict__ ws,
+                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                   ColorMats cm) {
+  __shared__ Rows512P1Lds L;
+  rows512_p1_tables(L.t, tw, post);
+  const int i = blockIdx.x >> 4, j1 = blockIdx.x & 15;
+  if (i >= n_img) return;   // never: grid = 16 x n_img
+  const ImgDesc d = imgs[i];
+  __syncthreads();   // tables
+  rows512_p1_item(L, rgb + d.rgb_off, j1, reinterpret_cast<float2*>(ws + d.ws_t), cm);
+}
+
+void launch_rows512p1(const ImgDesc* imgs, int n_img, const float* rgb, float* ws, const float2* tw,
+                      const float2* post, const ColorMats& cm, hipStream_t s) {
+  if (n_img <= 0) return;
+  hipLaunchKernelGGL(k_rows512p1, dim3(16 * n_img), dim3(512), 0, s, imgs, n_img, rgb, ws, tw, post, cm);
+}
+
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                     const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate, bool packed) {
   if (n_blocks <= 0) return;

@@ -33,7 +33,7 @@ def _run(setup, B, opts, seed):
     ops, fe_mod, fe, pn, lfq = setup
     dev = torch.device(DEV, torch.cuda.current_device())
     x = ops.synth_images(B, 512, 512, seed=seed, device=dev)
-    saved = {"enc_pipe": 0, "rows_kernel": 4}
+    saved = {"enc_pipe": 0, "rows_kernel": 4, "rows_p1": 0}
     for k, v in opts.items():
         ops.set_option(k, v, dev)
     try:
@@ -92,3 +92,12 @@ def test_sort_grid_stride_matches(setup, grid):
     finally:
         ops.set_option("sort_grid", 0, dev)
     _same(got, ref)
+
+
+@pytest.mark.parametrize("B", [1, 7, 64, 1024])
+def test_rows_p1_matches_two_kernel_path(setup, B):
+    """k_rows512p1 (row pass + the column FFT's pass 1) + k_fft_cols7p2 (pass
+    2 onwards): the same arithmetic as k_rows512pk + k_fft_cols7, so every
+    packed output is bit-identical"""
+    ref = _run(setup, B, {}, seed=25)
+    _same(_run(setup, B, {"rows_p1": 1}, seed=25), ref)
