@@ -469,11 +469,20 @@ __device__ __forceinline__ void rows512_p1_item(Rows512P1Lds& X, const float* __
 
 #pragma unroll 1
   for (int c = 0; c < 3; ++c) {
+    // channel c's IPT values are in A[0] / B[0] (rotated below: no dynamic
+    // register indexing in the rolled channel loop, which would go to scratch)
     cf v[16];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-      v[b] = A[c][b];
-      v[15 - b] = (cf){mirror16(B[c][b].x), mirror16(B[c][b].y)};
+      v[b] = A[0][b];
+      v[15 - b] = (cf){mirror16(B[0][b].x), mirror16(B[0][b].y)};
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      A[0][b] = A[1][b];
+      A[1][b] = A[2][b];
+      B[0][b] = B[1][b];
+      B[1][b] = B[2][b];
     }
     DFTV<16>::run(v);
     if (c > 0) __syncthreads();   // the previous channel's column-pass reads of every row region
