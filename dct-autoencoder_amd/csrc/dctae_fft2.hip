@@ -37,7 +37,10 @@ __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const 
   constexpr int B1 = M / R1, B2 = M / R2;
   constexpr int PX = (N + 63) / 64;        // pixels per lane and row
   constexpr int KI = (M + 63) / 64;        // k = lane + 64 i, i < KI, covers k < M (k = M by lane 0)
-  constexpr int RPW = 4;                   // rows per wave (block = 16 rows)
+#ifndef DCTAE_RPW224
+#define DCTAE_RPW224 1   // 224-wide rows: one row per wave (0.074 vs 0.081 ms at 4 rows per wave, config 2)
+#endif
+  constexpr int RPW = N == 224 ? DCTAE_RPW224 : 4;   // rows per wave (block = 4 RPW rows)
   static_assert(R1 * R2 == M, "two-pass plan");
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
@@ -354,12 +357,15 @@ __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, c
         for (int p = 0; p < KS / 2; ++p) {
           const float v0 = row[2 * p], v1 = row[2 * p + 1];
           am = max(am, max(__float_as_uint(v0) & 0x7fffffffu, __float_as_uint(v1) & 0x7fffffffu));
-          code |= (v0 >= thr_r[r][p].x ? 1u : 0u) << (KS - 1 - 2 * p);   // MSB-first (lfq.py:187)
-          code |= (v1 >= thr_r[r][p].y ? 1u : 0u) << (KS - 2 - 2 * p);
+          code = 2 * code + (v0 >= thr_r[r][p].x ? 1u : 0u);   // MSB-first (lfq.py:187)
+          code = 2 * code + (v1 >= thr_r[r][p].y ? 1u : 0u);
         }
         am = jl < KS ? am : 0u;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) am = max(am, (uint32_t)__shfl_xor((int)am, o, 64));
+        // 16-lane row max by DPP row rotations (as cols_epilogue, dctae_spec512.h)
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x128, 0xf, 0xf, false));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x124, 0xf, 0xf, false));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x122, 0xf, 0xf, false));
+        am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x121, 0xf, 0xf, false));
         const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
         if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
         if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
@@ -533,7 +539,7 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
   return 0;
 }
 
-int fft_spec_rows_per_block(int spec) { return spec ? 16 : 0; }
+int fft_spec_rows_per_block(int spec) { return spec == 2 ? 4 * DCTAE_RPW224 : (spec ? 16 : 0); }
 
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                           const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s) {
