@@ -92,7 +92,11 @@ void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int
 // the bank rule of MI355X_MICROARCH.md, SQ_LDS_BANK_CONFLICT 91.5 M per launch
 // before; the kernel time did not move: it is latency-bound).  Rows
 // 448 .. 511 map onto themselves (the zero fill is unchanged).
+#ifdef DCTAE_NO_XROW
+__device__ __forceinline__ int xrow(int y) { return y; }
+#else
 __device__ __forceinline__ int xrow(int y) { return y ^ ((y >> 4) & 3); }
+#endif
 
 struct IColsLds {
   union {
