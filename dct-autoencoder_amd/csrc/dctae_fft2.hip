@@ -561,10 +561,13 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
   const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
   if (spec == 1 && list && n_list > 0) {
     const int n_items = 3 * qw;
-    const int grid = cols7_grid(n_list, qw, 2);
+#ifndef DCTAE_C7_IPB
+#define DCTAE_C7_IPB 2
+#endif
+    const int grid = cols7_grid(n_list, qw, thr ? DCTAE_C7_IPB : 2);
     if (thr)
-      hipLaunchKernelGGL((k_fft_cols7<true, 2, true>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, n_items, qw, ws,
-                         tw, post, ep, sk);
+      hipLaunchKernelGGL((k_fft_cols7<true, DCTAE_C7_IPB, true>), dim3(grid), dim3(256), 0, s, imgs, list, n_list,
+                         n_items, qw, ws, tw, post, ep, sk);
     else
       hipLaunchKernelGGL((k_fft_cols7<false, 2, true>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, n_items, qw,
                          ws, tw, post, ep, sk);
