@@ -241,7 +241,10 @@ __device__ __forceinline__ void rows512_item(Rows512Xch& X, const Rows512Tab& L,
 // Same rounding as rows512_item for the IPT (identical fma order per pixel);
 // the FFT differs in operation order only (tolerance-tested).
 // ---------------------------------------------------------------------------
-constexpr int kXchStridePk = 272;   // complex slots per row group: 2 KB + 128 B (row groups 0/1 on opposite bank halves)
+#ifndef DCTAE_XCH_PK
+#define DCTAE_XCH_PK 272
+#endif
+constexpr int kXchStridePk = DCTAE_XCH_PK;   // complex slots per row group: 2 KB + 128 B (row groups 0/1 on opposite bank halves)
 
 struct Rows512XchPk {
   cf xch[4][4][kXchStridePk];
