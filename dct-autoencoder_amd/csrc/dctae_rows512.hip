@@ -41,10 +41,12 @@ __global__ __launch_bounds__(256, DCTAE_ROWS_MINB) void k_rows512(const ImgDesc*
 }
 
 // rows_kernel 4: the packed-f32 item (dctae_rows512.h rows512_item_pk)
-#ifndef DCTAE_PK_WPE
-#define DCTAE_PK_WPE 3
+#ifdef DCTAE_PK_WPE   // experiment switch (waves per SIMD); default: the compiler's choice (3)
+#define DCTAE_PK_ATTR __attribute__((amdgpu_waves_per_eu(DCTAE_PK_WPE)))
+#else
+#define DCTAE_PK_ATTR
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DCTAE_PK_WPE))) void k_rows512pk(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+__global__ __launch_bounds__(256) DCTAE_PK_ATTR void k_rows512pk(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                    const float* __restrict__ rgb, float* __restrict__ ws,
                                                    const float2* __restrict__ tw, const float2* __restrict__ post,
                                                    ColorMats cm) {
