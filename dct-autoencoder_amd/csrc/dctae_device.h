@@ -31,6 +31,15 @@ __device__ __forceinline__ float nanmax(float a, float b) {
   return (a != a || a > b) ? a : ((b != b) ? b : (a > b ? a : b));
 }
 
+// nanmax over each 16-lane row of the wave, every lane gets its row's value:
+// DPP row rotations by 8, 4, 2, 1 (VALU only; __shfl_xor is an LDS permute)
+__device__ __forceinline__ float row16_nanmax(float a) {
+  a = nanmax(a, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x128, 0xf, 0xf, false)));
+  a = nanmax(a, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x124, 0xf, 0xf, false)));
+  a = nanmax(a, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x122, 0xf, 0xf, false)));
+  return nanmax(a, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a), 0x121, 0xf, 0xf, false)));
+}
+
 // order-preserving float -> uint32 key; every NaN sorts above +inf
 // (torch.sort(descending=True) puts NaN first).
 __device__ __forceinline__ uint32_t float_key(float f) {
@@ -87,8 +96,7 @@ __device__ inline void token_epilogue(const EncParams& ep, int c, int h, int w, 
     }
   }
   // group max over the 16 lanes (xor shuffles stay inside the group)
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
+  amax = row16_nanmax(amax);
   if (j == 0) {
     // score = amax*mw + (-(h+w))/ci[c]      (FE:409-416, fp32 ops)
     float s = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
@@ -133,9 +141,22 @@ __device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int
     }
     if (ep.median) {
       if (sk.norm || ny || !ep.thr) {
+        float med[P], bb[P];
+        if ((P & 1) == 0) {   // tab is even: 8-byte table loads
+          const float2* m2 = reinterpret_cast<const float2*>(ep.median + tab);
+          const float2* b2 = reinterpret_cast<const float2*>(ep.b + tab);
+#pragma unroll
+          for (int p = 0; p < P / 2; ++p) {
+            const float2 mv = m2[p], bv = b2[p];
+            med[2 * p] = mv.x, med[2 * p + 1] = mv.y, bb[2 * p] = bv.x, bb[2 * p + 1] = bv.y;
+          }
+        } else {
+#pragma unroll
+          for (int p2 = 0; p2 < P; ++p2) med[p2] = ep.median[tab + p2], bb[p2] = ep.b[tab + p2];
+        }
 #pragma unroll
         for (int p2 = 0; p2 < P; ++p2) {
-          const float y = pn_forward(vals[p2], ep.median[tab + p2], ep.b[tab + p2], ep.eps, ep.min_val, ep.max_val);
+          const float y = pn_forward(vals[p2], med[p2], bb[p2], ep.eps, ep.min_val, ep.max_val);
           bits |= (y > 0.0f ? 1u : 0u) << p2;
           if (sk.norm) sk.norm[tok * PP + j * P + p2] = y;
           if (ny) ny[p2] = y;
@@ -154,8 +175,7 @@ __device__ __forceinline__ void token_epilogue_p(const EncParams& ep, int c, int
       }
     }
   }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
+  amax = row16_nanmax(amax);
   if (j == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
   if (ep.median && sk.codes) {
     if (ep.cb_dim == P && ep.ncb == P) {
@@ -200,8 +220,7 @@ __device__ __forceinline__ void token_epilogue_thr(const EncParams& ep, int c, i
       for (int p2 = 0; p2 < P; ++p2) sk.raw[tok * PP + j * P + p2] = vals[p2];
     }
   }
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) amax = nanmax(amax, __shfl_xor(amax, o, 64));
+  amax = row16_nanmax(amax);
   if (j == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(amax, ep.mw), __fdiv_rn(-(float)(h + w), ep.ci[c]));
   if (sk.codes && j < P) sk.codes[tok * P + j] = (uint16_t)(__builtin_bitreverse32(bits) >> (32 - P));
 }
