@@ -170,8 +170,14 @@ __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict_
       o[2][e] = mat3_row(cm.lms2rgb, 2, l0, l1, l2);
     }
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 3; ++c) {
+#ifdef DCTAE_DEC_NT
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store((v4f){o[c][0], o[c][1], o[c][2], o[c][3]}, reinterpret_cast<v4f*>(dst + c * hw + 64 * b));
+#else
       *reinterpret_cast<float4*>(dst + c * hw + 64 * b) = make_float4(o[c][0], o[c][1], o[c][2], o[c][3]);
+#endif
+    }
   }
 }
 

@@ -582,6 +582,7 @@ __device__ __forceinline__ void gather_tokens(const ImgDesc& d, const uint16_t* 
 // scores in ascending index order = the (score desc, index asc) order above.
 // Tokens per image <= 512 x 6 = 3072 (max_patch 32 x 32, 3 channels).
 constexpr int kSortBS = 512, kSortIPT = 6;
+typedef long long v2i64 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restrict__ imgs, EncParams ep,
                                                         TokenSinks st, PackSinks out, int n_img) {
@@ -614,9 +615,15 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     const uint32_t f = order[t];
     const int c = f % C, s = f / C, h = s / d.qw, w = s % d.qw;
     const int64_t o = base + t;
+#ifdef DCTAE_SORT_META_NT
+    __builtin_nontemporal_store((v2i64){(long long)h, (long long)w}, reinterpret_cast<v2i64*>(out.pos + 2 * o));
+    __builtin_nontemporal_store((long long)c, reinterpret_cast<long long*>(out.ch + o));
+    __builtin_nontemporal_store((long long)d.local_id, reinterpret_cast<long long*>(out.ids + o));
+#else
     *reinterpret_cast<longlong2*>(out.pos + 2 * o) = make_longlong2(h, w);
     out.ch[o] = c;
     out.ids[o] = d.local_id;
+#endif
     if (out.key_pad) out.key_pad[o] = 0;
     if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
   }
@@ -628,7 +635,11 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     for (int e = tid; e < d.k * 7; e += kSortBS) {
       const int t = e / 7, q = e - t * 7;
       const uint32_t v = (uint32_t)lfq_index_bits(src[(d.tok_off + order[t]) * 7 + q], pos2, neg2);
-      dst[(base + t) * 7 + q] = make_longlong2(v & 0xFFFFu, v >> 16);
+      // write-once outputs: nontemporal stores (their lines leave the L2 /
+      // Infinity Cache early instead of being written back under the next
+      // step's row kernel: sort 0.146 -> 0.143 ms, next rows 1.13 -> 1.11 ms)
+      __builtin_nontemporal_store((v2i64){(long long)(v & 0xFFFFu), (long long)(v >> 16)},
+                                  reinterpret_cast<v2i64*>(dst + (base + t) * 7 + q));
     }
   } else if (out.codes) {
     const int ncb = ep.ncb;
