@@ -76,10 +76,6 @@ def kernel_models(h, w, p, maxp, ncb, s, images_per_row):
         "gemm_cols": ("mfma", 3 * 2.0 * kh * kw * h, "flop"),
         "fft_rows": ("hbm", 12 * h * w + inter, "B"),            # RGB in, T out
         "fft_cols": ("hbm", inter + stage, "B"),                  # T in, token staging out
-        # persistent rows + columns (k_enc512): RGB in, token staging out; T stays on chip
-        "enc512": ("hbm", 12 * h * w + stage, "B"),
-        # pipelined rows + columns (k_enc_pipe launches): RGB in, token staging out; T in the Infinity Cache ring
-        "enc_pipe": ("hbm", 12 * h * w + stage, "B"),
         "tile_epilogue": ("hbm", 12 * kh * kw + stage, "B"),
         "sort_pack": ("hbm", stage + t * (8 * ncb + 32) + s / images_per_row, "B"),
         "pad_fill": ("hbm", s / images_per_row, "B"),

@@ -74,39 +74,24 @@ struct dctae_ctx {
   bool bluestein = false;
   bool fft_spec_enabled = true;
   int t_alias = 0;                    // profiling only: images share t_alias T slots (wrong output)
-  int rows_ablate = 0;                // profiling only: 1 no T stores, 2 no RGB loads (wrong output)
   int bs_ablate = 0;                  // profiling only: Bluestein kernels skip 1 loads, 2 FFTs, 4 post (wrong output)
-  int rows_kernel = 4;                // 512-wide rows: 4 = k_rows512pk (packed-f32 VALU; 1.13 vs 1.155 ms per 1024 images),
-                                      // 3 = k_rows512 (scalar), 2 = k_fft_rows2
+  // 512-wide rows with 32 kept tile columns: 4 = k_rows512pk (default), 2 = the
+  // general compile-time plan kernel k_fft_rows2<512> (serves max_patch_w < 32;
+  // selectable here so the parity tests cover it on the headline shape)
+  int rows_kernel = 4;
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
-  int sort_kernel = 2;                // 1: bitonic in LDS (1024 threads), 2: rocPRIM block radix sort
+  // 2: rocPRIM block radix sort (<= 3072 tokens per image); 1: the bitonic
+  // kernel that serves larger images (selectable for the parity tests)
+  int sort_kernel = 2;
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
   int n_cu = 256;
-  // persistent XCD-local 512^2 encode (dctae_enc512.hip): T slots and the
-  // per-call sync words (grow-only).  Off by default: measured slower than
-  // the two-kernel path and a wrong-code race under 3
-  // workgroups per CU is not yet explained; enc512 = 1 selects it
-  int enc512 = 0;
   // DCT GEMMs (lengths without a Makhoul plan, dctae_dct2, decode): 1 = the
   // split-bf16 MFMA kernel k_gemm_x3 (fp32 accuracy, 0.375 of the MFMA time),
   // 0 = the fp32 MFMA kernel k_gemm_f32
   int gemm_x3 = 1;
-  float* enc_slots = nullptr;
-  unsigned* enc_sync = nullptr;
-  size_t enc_sync_words = 0;
-  int enc_grid = 0;   // 0: occupancy x CUs
-  // pipelined 512^2 encode (dctae_encpipe.hip): images per chunk, 0 = off;
-  // launch L = rows of chunk L + columns of chunk L - 1, T in a two-chunk ring
-  int enc_pipe = 0;
-  int sort_grid = 0;                  // k_sort_pack2 blocks (grid-stride over images); 0 = one per image
-  // 512^2 batches: the column FFT's first pass in the row kernel (k_rows512p1
-  // + k_fft_cols7p2); 0 = k_rows512pk + k_fft_cols7
-  int rows_p1 = 0;
-  float* pipe_ring = nullptr;
-  size_t pipe_ring_bytes = 0;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
@@ -743,10 +728,6 @@ struct EncPlan {
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
   bool any_pad = true;   // some packed row shorter than max_seq_len
-  // every image 512 x 512 on the Makhoul plan with 32 x 32 tiles kept: the
-  // persistent encode (k_enc512) can run the rows + columns of the whole call
-  bool all512 = false;
-  int64_t tw512 = 0, post512 = 0;   // the N = 512 plan's tables
 };
 
 // ---------------------------------------------------------------------------
@@ -815,9 +796,6 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   if (ctx->st_ws) hipFree(ctx->st_ws);
   if (ctx->vq_ws) hipFree(ctx->vq_ws);
   if (ctx->proj_ws) hipFree(ctx->proj_ws);
-  if (ctx->enc_slots) hipFree(ctx->enc_slots);
-  if (ctx->pipe_ring) hipFree(ctx->pipe_ring);
-  if (ctx->enc_sync) hipFree(ctx->enc_sync);
   delete ctx->enc_plan;
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
@@ -875,22 +853,16 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   // slots, skipped loads / stores) and exist only in a profiling build
   // (`make PROFILING=1`, a separate library), never in the shipped one
   else if (k == "t_alias" && value >= 0) ctx->t_alias = (int)value;
-  else if (k == "rows_ablate" && value >= 0 && value <= 3) ctx->rows_ablate = (int)value;
   else if (k == "bs_ablate" && value >= 0 && value <= 7) ctx->bs_ablate = (int)value;
 #else
-  else if (k == "t_alias" || k == "rows_ablate" || k == "bs_ablate")
+  else if (k == "t_alias" || k == "bs_ablate")
     return fail(ctx, DCTAE_EUNSUP, "option " + k + " exists only in a profiling build (make PROFILING=1)");
 #endif
-  else if (k == "rows_kernel" && value >= 2 && value <= 4) ctx->rows_kernel = (int)value;
+  else if (k == "rows_kernel" && (value == 2 || value == 4)) ctx->rows_kernel = (int)value;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
-  else if (k == "enc512") ctx->enc512 = value != 0;
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
-  else if (k == "enc_grid" && value >= 0 && value <= (1 << 16)) ctx->enc_grid = (int)value;
-  else if (k == "enc_pipe" && value >= 0 && value <= 4096) ctx->enc_pipe = (int)value;
-  else if (k == "sort_grid" && value >= 0 && value <= (1 << 20)) ctx->sort_grid = (int)value;
-  else if (k == "rows_p1") ctx->rows_p1 = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -966,7 +938,6 @@ int dctae_check_device_errors(dctae_ctx* ctx, void* stream) {
   if (h & 2) return fail(ctx, DCTAE_EINVAL, "batched_image_ids entry has no image (patch_sizes mismatch)");
   if (h & 4) return fail(ctx, DCTAE_EINVAL, "token position outside its image's patch grid");
   if (h & 16) return fail(ctx, DCTAE_EINVAL, "VectorQuantize index out of range of the codebook");
-  if (h & 32) return fail(ctx, DCTAE_EHIP, "persistent encode (k_enc512): a hand-off wait timed out; outputs invalid");
   return 0;
 }
 
@@ -1256,16 +1227,6 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     j.pc_qw = pc_qw;
     j.pc_off = E.pb.add(pc.data(), pc.size());
   }
-  E.all512 = n > 0;
-  for (int i = 0; i < n && E.all512; ++i) {
-    const ImgDesc& d = D[i];
-    E.all512 = d.H == 512 && d.W == 512 && d.qh == 32 && d.qw == 32 && d.plan_w >= 0 && d.plan_h >= 0 &&
-               plans[d.plan_w].spec == 1 && plans[d.plan_h].spec == 1 && d.bs == 0;
-  }
-  if (E.all512) {
-    E.tw512 = plans[D[0].plan_w].tw_off;
-    E.post512 = plans[D[0].plan_w].post_off;
-  }
   E.plans_off = E.pb.add(plans.data(), plans.size());
   E.all_desc_off = E.pb.add(D.data(), D.size());
   if (full && pack->n_rows > 0) E.rowlen_off = E.pb.add(pack->row_len, pack->n_rows);
@@ -1403,7 +1364,6 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   if (proj_w) skc.codes = nullptr;
   // row half / column half of a chunk job on a stream
   auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
-    const int nj = j.i1 - j.i0;
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     if (j.any_gemm_rows) {
       {
@@ -1427,10 +1387,9 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fr[v]) {
         Timer t(ctx, st, "fft_rows");
-        if (v == 1 && ctx->rows_kernel >= 3 && cfg->max_patch_w >= 32)
+        if (v == 1 && ctx->rows_kernel == 4 && cfg->max_patch_w >= 32)
           launch_rows512(dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
-                         ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st, ctx->rows_ablate,
-                         ctx->rows_kernel == 4);
+                         ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st);
         else
           launch_fft_rows_spec(v, dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
                                ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st);
@@ -1470,57 +1429,9 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                              v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr, v == 1 ? j.n_pc : 0, j.pc_qw);
       }
   };
-  // the persistent XCD-local encode (dctae_enc512.hip): codes-only 512^2 calls
-  // with the exact LFQ thresholds (14 codebooks of 14 bits, the cols7 epilogue)
-  const bool thr_codes = epj.median && epj.thr && !skc.norm && !skc.raw && skc.codes && epj.maxph <= 32 &&
-                         epj.cb_dim == 14 && epj.ncb == 14;
-  if (E.all512 && ctx->enc512 && ctx->rows_kernel >= 3 && thr_codes && !ctx->t_alias && !ctx->rows_ablate) {
-    const size_t words = enc512_sync_words(E.n_img);
-    if (!ctx->enc_slots) {
-      HIPCHK(ctx, hipMalloc((void**)&ctx->enc_slots, enc512_slot_bytes()));
-    }
-    if (words > ctx->enc_sync_words) {
-      if (ctx->enc_sync) HIPCHK(ctx, hipFree(ctx->enc_sync));
-      ctx->enc_sync = nullptr;
-      HIPCHK(ctx, hipMalloc((void**)&ctx->enc_sync, words * sizeof(unsigned)));
-      ctx->enc_sync_words = words;
-    }
-    const int grid = ctx->enc_grid > 0 ? ctx->enc_grid : enc512_grid(ctx->device);
-    Timer t(ctx, s, "enc512");
-    launch_enc512((const ImgDesc*)(pd + E.all_desc_off), E.n_img, imgs->rgb_dev, ctx->enc_slots,
-                  ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, epj, skc, ctx->enc_sync, grid,
-                  ctx->err_dev, s);
-  } else if (E.all512 && ctx->enc_pipe > 0 && ctx->rows_kernel >= 3 && thr_codes && !ctx->t_alias &&
-             !ctx->rows_ablate) {
-    const int C = std::min(ctx->enc_pipe, E.n_img);
-    const size_t need = enc_pipe_ring_bytes(C);
-    if (need > ctx->pipe_ring_bytes) {
-      if (ctx->pipe_ring) HIPCHK(ctx, hipFree(ctx->pipe_ring));
-      ctx->pipe_ring = nullptr;
-      ctx->pipe_ring_bytes = 0;
-      HIPCHK(ctx, hipMalloc((void**)&ctx->pipe_ring, need));
-      ctx->pipe_ring_bytes = need;
-    }
-    Timer t(ctx, s, "enc_pipe");
-    launch_enc_pipe((const ImgDesc*)(pd + E.all_desc_off), E.n_img, C, imgs->rgb_dev, ctx->pipe_ring,
-                    ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, epj, skc, ctx->rows_kernel == 4, s);
-  } else {
-    for (const ChunkJob& j : E.jobs) {
-      const int nj = j.i1 - j.i0;
-      if (E.all512 && ctx->rows_p1 && j.n_pc == nj && !ctx->t_alias && !ctx->rows_ablate) {
-        const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
-        {
-          Timer t(ctx, s, "fft_rows");
-          launch_rows512p1(dd, nj, imgs->rgb_dev, ctx->ws, ctx->fft_tab + E.tw512, ctx->fft_tab + E.post512, ctx->cm, s);
-        }
-        Timer t(ctx, s, "fft_cols");
-        launch_fft_cols7p2(dd, (const int*)(pd + j.pc_off), j.n_pc, j.pc_qw, ctx->ws, ctx->fft_tab + E.tw512,
-                           ctx->fft_tab + E.post512, epj, skc, s);
-        continue;
-      }
-      do_rows(j, s);
-      do_cols(j, s);
-    }
+  for (const ChunkJob& j : E.jobs) {
+    do_rows(j, s);
+    do_cols(j, s);
   }
   if (proj_w && E.n_tok > 0) {
     Timer t(ctx, s, "lfq_project_in");
@@ -1540,7 +1451,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       eps.code_neg = (uint32_t)neg;
     }
     launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), eps, sk, ps, s,
-                     ctx->sort_kernel, E.max_T, ctx->sort_grid);
+                     ctx->sort_kernel, E.max_T);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
@@ -1906,10 +1817,16 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, i
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (int rc = proj_scratch(ctx, lfq->codebook_dim * lfq->num_codebooks, dim)) return rc;
-  Timer t(ctx, s, "lfq_project_in");
-  launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, idx,
-                        ctx->proj_ws, s);
+  // ctx->proj_ws (the pre-split weight) is shared with every call of this
+  // context: ordered after the previous call, whatever its stream
+  order_after_previous(ctx, s);
+  {
+    Timer t(ctx, s, "lfq_project_in");
+    launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, idx,
+                          ctx->proj_ws, s);
+  }
   HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
   return 0;
 }
 
@@ -1920,10 +1837,14 @@ int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* i
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (int rc = proj_scratch(ctx, dim, lfq->codebook_dim * lfq->num_codebooks)) return rc;
-  Timer t(ctx, s, "lfq_project_out");
-  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
-                         ctx->proj_ws, s);
+  order_after_previous(ctx, s);   // shared ctx->proj_ws
+  {
+    Timer t(ctx, s, "lfq_project_out");
+    launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
+                           ctx->proj_ws, s);
+  }
   HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
   return 0;
 }
 
@@ -1943,11 +1864,15 @@ int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, con
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   if (int rc = proj_scratch(ctx, dim, lfq->codebook_dim * lfq->num_codebooks)) return rc;
-  Timer t(ctx, s, "lfq_project_out");
-  launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
-                         ctx->proj_ws, s, channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h, max_patch_w,
-                         ctx->err_dev);
+  order_after_previous(ctx, s);   // shared ctx->proj_ws
+  {
+    Timer t(ctx, s, "lfq_project_out");
+    launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
+                           ctx->proj_ws, s, channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h,
+                           max_patch_w, ctx->err_dev);
+  }
   HIPCHK(ctx, hipGetLastError());
+  mark_done(ctx, s);
   return 0;
 }
 
@@ -1979,11 +1904,18 @@ static int vq_scratch(dctae_ctx* ctx, size_t need) {
 // O (n, N) = A (n, K) W^T (N, K) + bias, on k_gemm_f32 (plan uploaded through the shared plan buffer)
 static int vq_linear(dctae_ctx* ctx, const float* A, int64_t n, int K, const float* W, const float* bias, int N,
                      float* O, const uint8_t* mask, const float* orig, hipStream_t s, const char* name) {
-  GemmProblem g = gemm(A, 0, K, 1, W, 0, K, 1, O, 0, N, 1, (int)n, N, K, 1);
+  // k_gemm_x3 addresses each operand through a buffer resource with a 32-bit
+  // byte range: the rows go in chunks whose A and O spans stay below 2^31 bytes
+  const int64_t rows_max = ((int64_t)1 << 31) / ((int64_t)4 * std::max(K, N)) - 1;
+  std::vector<GemmProblem> g;
   std::vector<TileRef> t;
-  add_tiles(t, 0, g);
+  for (int64_t r0 = 0; r0 < n; r0 += rows_max) {
+    const int rows = (int)std::min(rows_max, n - r0);
+    g.push_back(gemm(A + r0 * K, 0, K, 1, W, 0, K, 1, O + r0 * N, 0, N, 1, rows, N, K, 1));
+    add_tiles(t, (int)g.size() - 1, g.back());
+  }
   PlanBuf pb;
-  const size_t g_off = pb.add(&g, 1);
+  const size_t g_off = pb.add(g.data(), g.size());
   const size_t t_off = pb.add(t.data(), t.size());
   int rc;
   if ((rc = upload_plan(ctx, pb, s))) return rc;
@@ -2001,9 +1933,11 @@ int dctae_vq_forward(dctae_ctx* ctx, const dctae_vq* vq, const float* x, const u
   if (rc) return rc;
   if (n_tok < 0 || (n_tok > 0 && (!x || !indices))) return fail(ctx, DCTAE_EINVAL, "bad VectorQuantize tensors");
   if (n_tok == 0) return 0;
-  if (n_tok > (int64_t)INT32_MAX / 64) return fail(ctx, DCTAE_EINVAL, "VectorQuantize: too many tokens in one call");
   hipStream_t s = (hipStream_t)stream;
   const int H = vq->heads, D = vq->codebook_dim, C = vq->codebook_size, HD = H * D;
+  // element indices of the (n_tok, dim) input and the (n_tok, H*D) vectors are 32-bit in the kernels
+  if (n_tok > (int64_t)INT32_MAX / 64 || n_tok * std::max(vq->dim, HD) > (int64_t)INT32_MAX)
+    return fail(ctx, DCTAE_EINVAL, "VectorQuantize: too many tokens in one call (n_tok * max(dim, heads * 16) >= 2^31)");
   const bool proj = vq->dim != HD;
   const int64_t nv = n_tok * H;
   // scratch: acc (64 doubles) | et (C*D) | y2 (C) | xp (n*HD, projected only) | xq (n*HD)

@@ -449,64 +449,6 @@ __global__ __launch_bounds__(256) void k_fft_cols7(const ImgDesc* __restrict__ i
   cols7_block<THR, IPB, PF>(blockIdx.x, imgs, list, n_list, n_items, qw, ws, tw, post, ep, sk, L, post4, tw_s, sbias);
 }
 
-// column pass after k_rows512p1 (option rows_p1): the cols7 block with
-// pass 1 already done -- P1 (float2, T's workspace slot) loaded straight
-// into pass 2's order, the next image's P1 in flight during the transform
-template <bool THR>
-__global__ __launch_bounds__(256) void k_fft_cols7p2(const ImgDesc* __restrict__ imgs, const int* __restrict__ list,
-                                                     int n_list, int n_items, int qw, const float* __restrict__ ws,
-                                                     const float2* __restrict__ tw, const float2* __restrict__ post,
-                                                     EncParams ep, TokenSinks sk) {
-  constexpr int M = 256, IPB = 2;
-  __shared__ Cols7Lds L;
-  __shared__ float4 post4[257];
-  __shared__ float2 tw_s[256];
-  __shared__ float sbias[32];
-  const int b = blockIdx.x;
-  const int per_x = (n_items + 7) / 8;
-  const int slot = b >> 3;
-  const int t = (b & 7) * per_x + slot % per_x, g = slot / per_x;
-  const int k0 = g * IPB;
-  if (t >= n_items || k0 >= n_list) return;
-  const int c = t / qw, strip = t - c * qw;
-  const float4* p4 = reinterpret_cast<const float4*>(post);
-  for (int i = threadIdx.x; i < M + 1; i += 256) post4[i] = p4[i];
-  for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
-  float2 thr_r[2][7];
-  cols_thresholds<THR>(imgs[list[k0]], c, strip, ep, thr_r, sbias);
-  cf u[16];
-  cols7p2_load(c, strip, ws + imgs[list[k0]].ws_t, u);
-  __syncthreads();   // tables
-#pragma unroll
-  for (int uu = 0; uu < IPB; ++uu) {
-    const int k = k0 + uu;
-    if (k < n_list) {
-      const ImgDesc dk = imgs[list[k]];
-      cf nu[16];
-      if (uu + 1 < IPB && k + 1 < n_list) cols7p2_load(c, strip, ws + imgs[list[k + 1]].ws_t, nu);
-      cols7p2_compute<THR>(dk, c, strip, L, u, post4, tw_s, sbias, thr_r, ep, sk);
-      __syncthreads();
-      if (uu + 1 < IPB) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) u[r] = nu[r];
-      }
-    }
-  }
-}
-
-void launch_fft_cols7p2(const ImgDesc* imgs, const int* list, int n_list, int qw, const float* ws, const float2* tw,
-                        const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
-  if (n_list <= 0) return;
-  const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
-  const int n_items = 3 * qw, grid = cols7_grid(n_list, qw, 2);
-  if (thr)
-    hipLaunchKernelGGL(k_fft_cols7p2<true>, dim3(grid), dim3(256), 0, s, imgs, list, n_list, n_items, qw, ws, tw, post,
-                       ep, sk);
-  else
-    hipLaunchKernelGGL(k_fft_cols7p2<false>, dim3(grid), dim3(256), 0, s, imgs, list, n_list, n_items, qw, ws, tw,
-                       post, ep, sk);
-}
-
 int cols7_grid(int n_list, int qw, int ipb) {
   const int n_items = 3 * qw, per_x = (n_items + 7) / 8;
   return 8 * per_x * ((n_list + ipb - 1) / ipb);

@@ -1,7 +1,7 @@
 // Decode row pass for images 512 pixels wide with Kw = 448 (the config-3
 // round trip): U[c][y][kx] (kx < 448, zero beyond) -> orthonormal DCT-III of
 // every row (torch_dct.idct, util.py:337-338 <- FE:149) -> IPT -> RGB
-// (util.py:85-97), the mirror image of k_rows512 (dctae_rows512.hip).
+// (util.py:85-97), the mirror image of the row item of k_rows512pk (dctae_rows512.h).
 //
 // Inverse Makhoul (dctae_idct.hip's header): conj Z_k = conj(a_k) (Ys[k] +
 // i Ys[N-k]) + conj(b_k) (Ys[M+k] + i Ys[M-k]), k < M = 256; W = FFT_256(conj Z)
@@ -32,7 +32,7 @@ __device__ __forceinline__ float iror16(float x) {      // lane l <- lane l - 1 
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x121, 0xf, 0xf, false));
 }
 
-constexpr int kIXchStride = 528;   // as k_rows512: the two row groups of a half-wave on opposite bank halves
+constexpr int kIXchStride = 528;   // the two row groups of a half-wave on opposite bank halves
 
 struct IRows512Lds {
   float xch[4][4][kIXchStride];   // [wave][row group][re 256 | im 256 | pad]

@@ -585,16 +585,12 @@ constexpr int kSortBS = 512, kSortIPT = 6;
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restrict__ imgs, EncParams ep,
-                                                        TokenSinks st, PackSinks out, int n_img) {
+                                                        TokenSinks st, PackSinks out) {
   using Sort = rocprim::block_radix_sort<uint32_t, kSortBS, kSortIPT, uint32_t>;
   __shared__ typename Sort::storage_type tmp;
   __shared__ uint16_t order[kSortBS * kSortIPT];
   const int tid = threadIdx.x;
-  // grid-stride over images: with fewer blocks than images a block sorts its
-  // next image while the previous image's packed-row stores drain
-  for (int ii = blockIdx.x; ii < n_img; ii += gridDim.x) {
-  if (ii != (int)blockIdx.x) __syncthreads();   // the previous image's reads of `order`
-  const ImgDesc d = imgs[ii];
+  const ImgDesc d = imgs[blockIdx.x];
   uint32_t keys[kSortIPT], vals[kSortIPT];
 #pragma unroll
   for (int i = 0; i < kSortIPT; ++i) {
@@ -650,14 +646,12 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     }
   }
   if (out.patches || out.raw) gather_tokens(d, order, base, PP, st, out, tid, kSortBS);
-  }
 }
 
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
-                      const PackSinks& out, hipStream_t s, int kernel, int max_T, int grid) {
+                      const PackSinks& out, hipStream_t s, int kernel, int max_T) {
   if (kernel == 2 && max_T <= kSortBS * kSortIPT)
-    hipLaunchKernelGGL(k_sort_pack2, dim3(grid > 0 && grid < n_img ? grid : n_img), dim3(kSortBS), 0, s, imgs, ep, st,
-                       out, n_img);
+    hipLaunchKernelGGL(k_sort_pack2, dim3(n_img), dim3(kSortBS), 0, s, imgs, ep, st, out);
   else
     hipLaunchKernelGGL(k_sort_pack, dim3(n_img), dim3(1024), (size_t)np2 * 8, s, imgs, np2, ep, st, out);
 }

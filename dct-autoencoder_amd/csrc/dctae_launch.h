@@ -28,7 +28,7 @@ void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, i
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
-                      const PackSinks& out, hipStream_t s, int kernel = 1, int max_T = 1 << 30, int grid = 0);
+                      const PackSinks& out, hipStream_t s, int kernel = 1, int max_T = 1 << 30);
 void launch_pad_fill(const int32_t* row_len, int n_rows, const EncParams& ep, uint8_t* key_pad,
                      const PackSinks& out, hipStream_t s);
 void launch_norm(const float* x, const int64_t* ch, const int64_t* pos, int64_t n, int PP, int maxph, int maxpw,
@@ -80,14 +80,6 @@ void launch_fft_cols(const ImgDesc* imgs, const FftPlan* plans, const int4* bloc
 void launch_norm_thresholds(const float* med, const float* b, int64_t n, float eps, float lo, float hi, float* thr,
                             int* bad, hipStream_t s);
 
-// dctae_enc512.hip: the persistent XCD-local encode of 512^2 images (rows + columns in one launch)
-size_t enc512_sync_words(int n_img);
-size_t enc512_slot_bytes();
-int enc512_grid(int device);
-void launch_enc512(const ImgDesc* imgs, int n_img, const float* rgb, float* tslots, const float2* tw,
-                   const float2* post, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, unsigned* sync,
-                   int grid, int* err, hipStream_t s);
-
 int fft_spec_id(int N, const int* radix, int npass, int P);
 int fft_spec_rows_per_block(int spec);
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
@@ -106,18 +98,9 @@ void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, in
 void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
                          const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s, int ablate = 0,
-                    bool packed = false);
+                    const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s);
 
 int cols7_grid(int n_list, int qw, int ipb);
-size_t enc_pipe_ring_bytes(int C);
-void launch_rows512p1(const ImgDesc* imgs, int n_img, const float* rgb, float* ws, const float2* tw,
-                      const float2* post, const ColorMats& cm, hipStream_t s);
-void launch_fft_cols7p2(const ImgDesc* imgs, const int* list, int n_list, int qw, const float* ws, const float2* tw,
-                        const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
-void launch_enc_pipe(const ImgDesc* imgs, int n_img, int C, const float* rgb, float* tring, const float2* tw,
-                     const float2* post, const ColorMats& cm, const EncParams& ep, const TokenSinks& sk, bool packed,
-                     hipStream_t s);
 
 // Bluestein DCT for lengths without a Makhoul plan (dctae_bluestein.hip)
 int bs_rows_per_block(int L);

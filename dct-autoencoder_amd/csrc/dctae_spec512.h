@@ -149,9 +149,6 @@ __device__ __forceinline__ int cols7_j2(int w, int g) {
   return base;
 }
 
-// AUX: buffer-load cache policy (16 = sc1: served by the XCD's L2, never by
-// a possibly stale L1 line — the persistent encode's same-XCD hand-off)
-template <int AUX = 0>
 __device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
                                            float (&va)[16], float (&vb)[16]) {
   constexpr int N = 512;
@@ -165,7 +162,7 @@ __device__ __forceinline__ void cols7_load(const ImgDesc& d, int c, int strip, c
   const int lo = (4 * j1 * rs + col) * 4;
   const int hi = ((2 * N - 1 - 4 * j1 - 64 * 15) * rs + col) * 4;   // r = 15: lowest row of the upper half
   const int step = 64 * rs * 4, two = 2 * rs * 4;
-  constexpr int aux = AUX;
+  constexpr int aux = 0;
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
     va[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc, lo, r * step, aux));
@@ -309,48 +306,5 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
   cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sbias, thr_r, ep, sk);
 }
 
-
-// ---------------------------------------------------------------------------
-// Column kernel after k_rows512p1 (option rows_p1): the column FFT's pass 1
-// ran in the row kernel, whose outputs P1[c][j1][k1][kx] (float2) stand in
-// T's workspace slot.  Lane (w, g, col) = pass-2 butterfly j2 = cols7_j2(w, g)
-// of column 14 strip + col loads z1[j2 + 16 r] = Y_r[j2] = P1[c][r][j2][kx]
-// (16 float2 loads, 14 consecutive per 16-lane row), then twiddles, DFT16,
-// the Makhoul post and the token epilogue of cols7_compute.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void cols7p2_load(int c, int strip, const float* __restrict__ P1, cf (&u)[16]) {
-  const int tid = opaque_tid();
-  const int w = tid >> 6, g = (tid >> 4) & 3, col = min(tid & 15, 13);
-  const int j2 = cols7_j2(w, g);
-  const float2* src = reinterpret_cast<const float2*>(P1) + ((int64_t)(c * 16) * 16 + j2) * 448 + strip * 14 + col;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const float2 t = src[r * 16 * 448];
-    u[r] = (cf){t.x, t.y};
-  }
-}
-
-template <bool THR>
-__device__ __forceinline__ void cols7p2_compute(const ImgDesc& d, int c, int strip, Cols7Lds& L, const cf (&u)[16],
-                                                const float4* post4, const float2* tw_s, const float* sbias,
-                                                const float2 (&thr_r)[2][7], const EncParams& ep,
-                                                const TokenSinks& sk) {
-#pragma clang fp contract(fast)
-  const int tid = opaque_tid();
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), g = (tid >> 4) & 3, col = tid & 15;
-  const int j2 = cols7_j2(w, g);
-  cf v[16];
-  v[0] = u[0];
-#pragma unroll
-  for (int r = 1; r < 16; ++r) {
-    const float2 tw = tw_s[r * j2];
-    v[r] = cmul_pk(u[r], (cf){tw.x, tw.y});
-  }
-  DFTV<16>::run(v);
-  if (w == 0) cols7_post<true>(v, j2, g, col, post4, L.X);
-  else cols7_post<false>(v, j2, g, col, post4, L.X);
-  __syncthreads();
-  cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sbias, thr_r, ep, sk);
-}
 
 }  // namespace dctae

@@ -142,11 +142,16 @@ class LFQ(nn.Module):
             x = x.reshape(shape[0], -1, shape[-1])
         assert x.shape[-1] == self.dim, f"expected dimension of {self.dim} but received {x.shape[-1]}"
         if self._fused_proj():
-            # eval: quantized = +-scale of the index bits, so project_out(quantized)
-            # is the decode kernel on the indices (lfq.py:164-212)
+            # eval: quantized = where(h > 0, s, -s) (lfq.py:174-175) and the index
+            # bit is quantized > 0 (lfq.py:187), so quantized = bit ? |s| : -|s|:
+            # project_out(quantized) is the decode kernel on the indices with the
+            # scale |s| (for s < 0 the bits are the complemented signs, and
+            # indices_to_codes' bit ? s : -s would give -quantized)
             indices = self.project_codes(x)
             w, b = self._proj_w(self.project_out, x.device)
-            q = _ops.lfq_project_out(indices, w, b, self.cfg()).to(x.dtype)
+            qc = self.cfg(self.project_in.weight.dtype)
+            qc.codebook_scale = abs(qc.codebook_scale)
+            q = _ops.lfq_project_out(indices, w, b, qc).to(x.dtype)
         else:
             x = self.project_in(x)
             q, indices = _ops.lfq_forward(x, self.cfg(x.dtype))

@@ -330,25 +330,23 @@ int dctae_set_fft(dctae_ctx* ctx, int enable);
  * but measured slower on MI355X because of the extra launch boundaries). */
 int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
 
-/* Tuning / test knobs: "fft" (0/1), "fft_spec" (0/1: compile-time
- * specialised FFT kernels), "bluestein" (0/1, default 0: sides in [32, 1024]
- * without a Makhoul plan on the Bluestein FFT instead of the MFMA GEMM;
- * measured slower at these sizes), "chunk_bytes", "workspace_limit" (bytes),
- * "rows_kernel" (4, default: k_rows512pk, the packed-f32 row kernel; 3:
- * k_rows512; 2: k_fft_rows2 for 512-wide rows),
- * "sort_kernel" (2: rocPRIM radix, 1: bitonic), "fft_decode" (0/1),
+/* Tuning / test knobs.  Each one selects between kernels that the library
+ * also runs by default for other shapes, so every setting gives outputs
+ * within the parity tolerances of DESIGN.md section 6 (bit-identical packing
+ * metadata; tokens within 1e-6 x max|Y|; codes equal outside the guard band):
+ * "fft" (0/1), "fft_spec" (0/1: compile-time specialised FFT kernels),
+ * "bluestein" (0/1, default 0: sides in [32, 1024] without a Makhoul plan on
+ * the Bluestein FFT instead of the MFMA GEMM; measured slower at these
+ * sizes), "chunk_bytes", "workspace_limit" (bytes),
+ * "rows_kernel" (4, default: k_rows512pk for 512-wide rows; 2: the general
+ * compile-time plan kernel k_fft_rows2, which serves max_patch_w < 32),
+ * "sort_kernel" (2, default: rocPRIM radix for <= 3072 tokens per image; 1:
+ * the bitonic kernel that serves larger images), "fft_decode" (0/1),
  * "xcd_order" (0/1), "dec_rows_kernel" (3 / 2), "gemm_x3" (1, default:
  * the DCT GEMMs on the split-bf16 MFMA kernel k_gemm_x3, fp32-level
- * accuracy; 0: the fp32 MFMA kernel), "enc512" (0, default / 1: the
- * persistent XCD-local 512^2 encode, measured slower),
- * "enc_grid" (its block count, 0 = auto), "enc_pipe" (C > 0: the 512^2
- * encode as launches of chunk L's rows beside chunk L - 1's columns, T in a
- * two-chunk ring; 0, default; measured slower), "rows_p1"
- * (1: the column FFT's first pass inside the row kernel; 0, default;
- * measured slower), "sort_grid" (k_sort_pack2 blocks, 0 =
- * one per image); all of these give bit-identical outputs; profiling builds only
- * (make PROFILING=1; the shipped library returns DCTAE_EUNSUP):
- * "rows_ablate", "bs_ablate", "t_alias". */
+ * accuracy; 0: the fp32 MFMA kernel).  Profiling builds only (make
+ * PROFILING=1; the shipped library returns DCTAE_EUNSUP): "bs_ablate",
+ * "t_alias" (these write wrong outputs on purpose). */
 int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
 
 /* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an

@@ -77,6 +77,13 @@ def test_lfq_project_in_scale(pkg, si):
     nan_tok = torch.isnan(xc).any(-1)   # NaN tokens project to NaN: every bit is the rule's NaN bit
     assert torch.equal(idx.cpu()[nan_tok], ref[nan_tok])
     assert int(diff.sum()) <= 2
+    # q = project_out(where(h > 0, s, -s)) (lfq.py:174-212) on the tokens whose
+    # indices agree, within the fp32 GEMM band 2e-5 (|W_out| |s| + |b_out|)
+    same = ~diff.any(-1)
+    q_ref = torch.from_numpy(G[f"p{si}_q"])
+    w_out, b_out = torch.from_numpy(G["w_out"]), torch.from_numpy(G["b_out"])
+    qband = 2e-5 * (w_out.abs().sum(-1) * abs(s) + b_out.abs()) + 1e-7
+    assert torch.all(((q.cpu() - q_ref).abs() <= qband)[same]), f"scale {s}: project_out(quantized) differs"
 
 
 def _encode_codes(pkg, fe, pn, imgs, s, batch_encoder=False, proj=None):

@@ -567,12 +567,10 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-DEFAULTS = {"rows_kernel": 4, "sort_kernel": 2, "chunk_bytes": 1 << 40, "rows_p1": 0}
+DEFAULTS = {"rows_kernel": 4, "sort_kernel": 2, "chunk_bytes": 1 << 40}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "rows_lds": {"rows_kernel": 2},
-    "rows_scalar": {"rows_kernel": 3},
-    "rows_p1": {"rows_p1": 1},
     "sort_bitonic": {"sort_kernel": 1},
     "chunks": {"chunk_bytes": 4 << 20},
 }
