@@ -79,6 +79,10 @@ struct dctae_ctx {
   // general compile-time plan kernel k_fft_rows2<512> (serves max_patch_w < 32;
   // selectable here so the parity tests cover it on the headline shape)
   int rows_kernel = 4;
+  // 512 x 512 images at 32 x 32 kept tiles: 1 = the row pass writes the band
+  // layout T'[c][y/4][kx][y%4] and the columns run k_cols512b (16-byte loads,
+  // DESIGN.md section 4); 0 = row-major T and k_fft_cols7
+  int cols512b = 1;
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
@@ -705,6 +709,8 @@ struct ChunkJob {
   int n_rows_tiles, n_cols_tiles;
   size_t pc_off;      // k_fft_cols7 list: the spec-1 images of the job (one tile-column count qw)
   int n_pc, pc_qw;
+  size_t pb_off;      // k_cols512b list: the band-layout images of the job
+  int n_pb;
   int max_T, any_gemm_rows, any_gemm_cols, fold_t, any_bs_cols;
   size_t ipt_off;            // k_rgb_to_ipt blocks (local image, first group)
   int n_ipt;
@@ -859,6 +865,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
     return fail(ctx, DCTAE_EUNSUP, "option " + k + " exists only in a profiling build (make PROFILING=1)");
 #endif
   else if (k == "rows_kernel" && (value == 2 || value == 4)) ctx->rows_kernel = (int)value;
+  else if (k == "cols512b") ctx->cols512b = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
@@ -994,6 +1001,10 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     D[i].plan_h = plan_of(D[i].H);
     D[i].bs = (D[i].plan_w >= 0 && plans[D[i].plan_w].kind == 1 ? 1 : 0) |
               (D[i].plan_h >= 0 && plans[D[i].plan_h].kind == 1 ? 2 : 0);
+    // band layout: rows on k_rows512pk (Kw = 448) and columns on k_cols512b (Kh = 448)
+    D[i].tband = ctx->cols512b && ctx->rows_kernel == 4 && cfg->max_patch_w == 32 && cfg->max_patch_h == 32 &&
+                 D[i].H == 512 && D[i].W == 512 && D[i].bs == 0 && D[i].plan_w >= 0 &&
+                 plans[D[i].plan_w].spec == 1 && D[i].plan_h >= 0 && plans[D[i].plan_h].spec == 1;
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
@@ -1076,9 +1087,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     std::vector<int4> bc[4];
     std::vector<int32_t> fold;
     std::vector<int2> ipt;
-    std::vector<int32_t> pc;
+    std::vector<int32_t> pc, pb;
     int pc_qw = 0;
-    bool pc_ok = true;
+    bool pc_ok = cfg->max_patch_h <= 32;   // k_fft_cols7 keeps Kh <= 448 rows
     j.lds_rows = j.lds_cols = 0;
     for (int i = j.i0; i < j.i1; ++i) {
       const ImgDesc& d = D[i];
@@ -1148,6 +1159,10 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         for (int c = 0; c < 3; ++c)
           for (int kx0 = 0; kx0 < d.Kw; kx0 += cpb) bc[bs_lidx(L)].push_back(make_int4(li, c, kx0, 0));
         j.any_bs_cols = 1;
+      } else if (d.tband) {
+        pb.push_back(li);
+        j.tw_off_c[1] = plans[d.plan_h].tw_off;
+        j.post_off_c[1] = plans[d.plan_h].post_off;
       } else {
         const FftPlan& p = plans[d.plan_h];
         // generic kernel: one tile column per block; specialised: groups of
@@ -1226,6 +1241,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     j.n_pc = (pc_ok && (int)pc.size() * 3 * pc_qw == (int)fc[1].size()) ? (int)pc.size() : 0;
     j.pc_qw = pc_qw;
     j.pc_off = E.pb.add(pc.data(), pc.size());
+    j.n_pb = (int)pb.size();
+    j.pb_off = E.pb.add(pb.data(), pb.size());
   }
   E.plans_off = E.pb.add(plans.data(), plans.size());
   E.all_desc_off = E.pb.add(D.data(), D.size());
@@ -1278,7 +1295,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   key.insert(key.end(), {(int64_t)full, n, P, cfg->max_patch_h, cfg->max_patch_w, cfg->max_seq_len, ncb,
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
-                             64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3,
+                             64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3 +
+                             4096 * ctx->cols512b + 8192 * ctx->rows_kernel,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1387,7 +1405,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fr[v]) {
         Timer t(ctx, st, "fft_rows");
-        if (v == 1 && ctx->rows_kernel == 4 && cfg->max_patch_w >= 32)
+        if (v == 1 && ctx->rows_kernel == 4 && cfg->max_patch_w == 32)
           launch_rows512(dd, (const int2*)(pd + j.fr_off[v]), j.n_fr[v], imgs->rgb_dev, ctx->ws,
                          ctx->fft_tab + j.tw_off[v], ctx->fft_tab + j.post_off_r[v], ctx->cm, st);
         else
@@ -1420,6 +1438,11 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       Timer t(ctx, st, "fft_cols");
       launch_fft_cols(dd, plans_d, (const int4*)(pd + j.fc_off[0]), j.n_fc[0], j.lds_cols, ctx->ws, ctx->fft_tab,
                       epj, skc, st);
+    }
+    if (j.n_pb) {
+      Timer t(ctx, st, "fft_cols");
+      launch_cols512b(dd, (const int*)(pd + j.pb_off), j.n_pb, ctx->ws, ctx->fft_tab + j.tw_off_c[1],
+                      ctx->fft_tab + j.post_off_c[1], epj, skc, st);
     }
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fc[v]) {
@@ -2090,14 +2113,19 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
     Timer t(ctx, s, "dec_map");
     launch_dec_map((int64_t)n_rows * S, dd, a, map, s);
   }
+  // band layout of U (k_idct_cols512b -> k_idct_rows512<448, true>) at Kw = 448
+  const bool band = ctx->cols512b && ctx->dec_rows_kernel == 3 && D[0].qw == 32;
   {
     Timer t(ctx, s, "idct_cols");
-    launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
+    if (band)
+      launch_idct_cols512b(dd, n_img, ctx->ws, map, tw, pre, a, s);
+    else
+      launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
   }
   {
     Timer t(ctx, s, "idct_rows");
     if (ctx->dec_rows_kernel == 3 && D[0].qw == 32)
-      launch_idct_rows512(dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
+      launch_idct_rows512(dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s, band);
     else
       launch_idct_rows_spec(1, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
   }

@@ -419,9 +419,11 @@ __device__ __forceinline__ void cols7_block(int b, const ImgDesc* __restrict__ i
     if (k < n_list) {
       const ImgDesc dk = imgs[list[k]];
       if (u > 0 && !PF) cols7_load(dk, c, strip, ws + dk.ws_t, va, vb);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(va[r]), "+v"(vb[r]));   // see k_cols512b
       float na[16], nb[16];
-      if (PF && u + 1 < IPB && k + 1 < n_list) {
-        const ImgDesc dn = imgs[list[k + 1]];
+      if (PF && u + 1 < IPB) {   // unconditional (the last image reloads itself), see k_cols512b
+        const ImgDesc dn = imgs[list[min(k + 1, n_list - 1)]];
         cols7_load(dn, c, strip, ws + dn.ws_t, na, nb);   // in flight during the transform
       }
       cols7_compute<THR>(dk, c, strip, L, va, vb, post4, tw_s, sbias, thr_r, ep, sk);
@@ -447,6 +449,85 @@ __global__ __launch_bounds__(256) void k_fft_cols7(const ImgDesc* __restrict__ i
   __shared__ float2 tw_s[256];
   __shared__ float sbias[32];
   cols7_block<THR, IPB, PF>(blockIdx.x, imgs, list, n_list, n_items, qw, ws, tw, post, ep, sk, L, post4, tw_s, sbias);
+}
+
+// k_cols512b: the band-layout column pass (dctae_spec512.h).  Block b of the
+// grid: (channel, tile strip) item t and IPB consecutive images of `list`;
+// XCD-aware: blocks b and b + 8 share an XCD, each XCD lane owns 12 adjacent
+// items (neighbouring strips share L2 lines; their threshold tables stay in
+// that XCD's L2), the next image's T' loads in flight during the transform.
+#ifndef DCTAE_C5B_IPB
+#define DCTAE_C5B_IPB 2
+#endif
+template <bool THR, int IPB>
+__global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ imgs, const int* __restrict__ list,
+                                                  int n_list, const float* __restrict__ ws,
+                                                  const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                  EncParams ep, TokenSinks sk) {
+  constexpr int M = 256, per_x = 12;   // 96 items = 3 channels x 32 strips, 12 per XCD lane
+  __shared__ Cols512bLds L;
+  const int b = blockIdx.x;
+  const int slot = b >> 3;
+  const int t = (b & 7) * per_x + slot % per_x, k0 = (slot / per_x) * IPB;
+  if (k0 >= n_list) return;
+  const int c = t >> 5, strip = t & 31;
+  const int tid = threadIdx.x;
+  L.tw2[tid >> 4][tid & 15] = tw[(tid >> 4) * (tid & 15)];
+  const float4* p4 = reinterpret_cast<const float4*>(post);
+  {
+    const float4 ab = p4[tid];   // (al.x, al.y, be.x, be.y) -> c1..c4
+    L.pc[tid] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
+  }
+  const float4 abM = p4[M];
+  const float4 pcM = make_float4(abM.x + abM.z, abM.x - abM.z, abM.y + abM.w, abM.y - abM.w);
+  float2 thr_r[2][7];
+  cols_thresholds<THR>(imgs[list[k0]], c, strip, ep, thr_r, nullptr);
+  float sb[2] = {0.0f, 0.0f};
+  if (THR) {
+    const int g16 = tid >> 4;
+    sb[0] = __fdiv_rn(-(float)(g16 + strip), ep.ci[c]);
+    sb[1] = __fdiv_rn(-(float)(g16 + 16 + strip), ep.ci[c]);
+  }
+  float4 qa[8];
+  cols512b_load(c, strip, ws + imgs[list[k0]].ws_t, qa);
+  __syncthreads();   // tables
+#pragma unroll
+  for (int u = 0; u < IPB; ++u) {
+    const int k = k0 + u;
+    if (k < n_list) {
+      const ImgDesc dk = imgs[list[k]];
+      // the loads of this image (prefetched during the previous one) become
+      // opaque values here: without it the compiler moves their register
+      // shuffles up to the loads and waits for the NEXT image's prefetch
+      // before computing this one (no overlap at all)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(qa[r].x), "+v"(qa[r].y), "+v"(qa[r].z), "+v"(qa[r].w));
+      // the next image's loads in flight during this one; unconditional (the
+      // last image of the list reloads itself): a conditional load makes the
+      // compiler merge qn / qa with register copies right behind the loads
+      float4 qn[8];
+      if (u + 1 < IPB) cols512b_load(c, strip, ws + imgs[list[min(k + 1, n_list - 1)]].ws_t, qn);
+      cols512b_compute<THR>(dk, c, strip, L, qa, pcM, sb, thr_r, ep, sk);
+      __syncthreads();   // epilogue reads of X before the next image's transposes
+      if (u + 1 < IPB) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) qa[r] = qn[r];
+      }
+    }
+  }
+}
+
+void launch_cols512b(const ImgDesc* imgs, const int* list, int n_list, const float* ws, const float2* tw,
+                     const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
+  if (n_list <= 0) return;
+  const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
+  const int ipb = thr ? DCTAE_C5B_IPB : 2;
+  const int grid = 96 * ((n_list + ipb - 1) / ipb);
+  if (thr)
+    hipLaunchKernelGGL((k_cols512b<true, DCTAE_C5B_IPB>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, ws, tw,
+                       post, ep, sk);
+  else
+    hipLaunchKernelGGL((k_cols512b<false, 2>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, ws, tw, post, ep, sk);
 }
 
 int cols7_grid(int n_list, int qw, int ipb) {

@@ -31,7 +31,7 @@ struct ImgDesc {
   int32_t row, col, k, local_id;  // packing
   int32_t plan_w, plan_h;         // FFT plan index for rows (length W) / cols (length H); -1 = GEMM
   int32_t bs;        // bit 0: rows, bit 1: columns on the Bluestein kernels (columns: Y + k_tile_epilogue)
-  int32_t pad1;
+  int32_t tband;     // 1: the row pass writes T in the band layout T'[c][y/4][kx][y%4] (512 x 512 on k_rows512pk + k_cols512b)
 };
 
 // Generic batched strided fp32 GEMM problem:

@@ -167,16 +167,18 @@ __device__ __forceinline__ void xpose4_rows(float (&r)[4]) {
 
 // Row pass output layouts (the channel plane is H x 448 floats either way):
 //  * row-major T[c][y][kx] (band = false): read by the generic column kernels;
-//  * band layout T'[c][y / 4][kx][y % 4] (band = true, H = 512 with the
-//    columns on k_cols512b): the four rows of a wave are one band, so after a
+//  * band layout T'[c][y / 4][kx][slot] (band = true, H = 512 with the
+//    columns on k_cols512b), rows 4 b + (0, 2, 3, 1) in slots 0..3 -- the
+//    order of the Makhoul pairs (x0, x2) / (x3, x1) that the column kernel
+//    needs in adjacent registers: the four rows of a wave are one band, so after a
 //    4 x 4 cross-row transpose (xpose4_rows) every lane stores a float4
 //    (rows 4b .. 4b + 3 of one column) and a wave's store covers 64 adjacent
 //    columns = 1 KB contiguous (7 float4 stores + one 4-byte X[M] store per
 //    lane and channel, against 29 scattered 4-byte stores); k_cols512b's
 //    lane j of column kx then loads rows 64 b' + 4 j .. + 3 as one float4.
+template <bool band>
 __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Tab& L, const float* __restrict__ img,
-                                                int H, int y0, float* T, uint32_t plane_bytes, const ColorMats& cm,
-                                                bool band) {
+                                                int H, int y0, float* T, uint32_t plane_bytes, const ColorMats& cm) {
 #pragma clang fp contract(fast)
   constexpr int N = 512, M = 256, KW = 448;
   const int tid = threadIdx.x;
@@ -235,7 +237,7 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
   const int bk = (bo + s + 16 * g) * 16;                 // + 1024 q
   const int bn = (bo + N - s - 16 * g) * 16 - 3072;      // + 1024 (3 - q)
   const int bn1 = (g == 0 && s == 0) ? 0x7ffffff0 : bn;  // q = 1: column 448 (k = 64) is not kept
-  const int bm = j == 0 ? ((bo + M) * 4 + g) * 4 : 0x7ffffff0;
+  const int bm = j == 0 ? ((bo + M) * 4 + ((0x2130 >> (4 * g)) & 3)) * 4 : 0x7ffffff0;   // slot of row g: 0, 3, 1, 2
 
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -249,7 +251,7 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
     fft256_group(v, xr, j, s, L.tw2);
     // ---- Makhoul post: k = s + 16 i, A = Z[k] = v[i], P = Z[M - k]
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(T + (int64_t)c * H * KW, 0, plane_bytes, 0x00020000);
-    if (band) {
+    if constexpr (band) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         float rk[4], rn[4];
@@ -261,12 +263,12 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
         }
         xpose4_rows(rk);
         __builtin_amdgcn_raw_buffer_store_b128(
-            (v4u){__float_as_uint(rk[0]), __float_as_uint(rk[1]), __float_as_uint(rk[2]), __float_as_uint(rk[3])},
+            (v4u){__float_as_uint(rk[0]), __float_as_uint(rk[2]), __float_as_uint(rk[3]), __float_as_uint(rk[1])},
             rsrc, bk, 1024 * q, 0);
         if (q >= 1) {   // X[N - k], k = s + 16 i, is kept for k > 64
           xpose4_rows(rn);
           __builtin_amdgcn_raw_buffer_store_b128(
-              (v4u){__float_as_uint(rn[0]), __float_as_uint(rn[1]), __float_as_uint(rn[2]), __float_as_uint(rn[3])},
+              (v4u){__float_as_uint(rn[0]), __float_as_uint(rn[2]), __float_as_uint(rn[3]), __float_as_uint(rn[1])},
               rsrc, q == 1 ? bn1 : bn, 1024 * (3 - q), 0);
         }
       }

@@ -4,6 +4,7 @@
 #pragma once
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
+#include "dctae_rows512.h"
 
 namespace dctae {
 
@@ -22,7 +23,8 @@ __device__ __forceinline__ int opaque_tid() {
 // ---------------------------------------------------------------------------
 typedef float f2v __attribute__((ext_vector_type(2)));
 
-// Thresholds of this thread's epilogue rows: tiles h = g16 + 16 r, row jl.
+// Thresholds of this thread's epilogue rows: tiles h = g16 + 16 r, row jl;
+// sbias (nullable): the score's -(h + strip) / ci[c] per tile row h (FE:411-416)
 template <bool THR>
 __device__ __forceinline__ void cols_thresholds(const ImgDesc& d, int c, int strip, const EncParams& ep,
                                                  float2 (&thr_r)[2][7], float* sbias) {
@@ -35,7 +37,7 @@ __device__ __forceinline__ void cols_thresholds(const ImgDesc& d, int c, int str
     for (int r = 0; r < EPR; ++r)
 #pragma unroll
       for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = make_float2(0.001f * (p + r), -0.002f * (p + jl));
-    if (tid < 32) sbias[tid] = 0.0f;
+    if (sbias && tid < 32) sbias[tid] = 0.0f;
     return;
   }
 #endif
@@ -51,14 +53,15 @@ __device__ __forceinline__ void cols_thresholds(const ImgDesc& d, int c, int str
       }
     }
   }
-  if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
+  if (THR && sbias && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
 }
 
 // token epilogue of one (channel, tile column) item: X2 = the 448 x 14 kept
 // coefficients (float index k * 14 + col) in LDS; tile (h, strip) per 16-lane
-// group g16 (+16 r), tile row jl; codes from the thresholds held in registers
+// group g16 (+16 r), tile row jl; codes from the thresholds held in registers;
+// sb[r]: the score bias of tile row h = g16 + 16 r
 template <bool THR>
-__device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip, const f2v* X2, const float* sbias,
+__device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip, const f2v* X2, const float (&sb)[2],
                                                const float2 (&thr_r)[2][7], const EncParams& ep,
                                                const TokenSinks& sk) {
   constexpr int KS = 14, EPR = 2;
@@ -98,7 +101,7 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
         am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x122, 0xf, 0xf, false));
         am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x121, 0xf, 0xf, false));
         const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
-        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sbias[h]);
+        if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sb[r]);
         if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
       }
     }
@@ -303,8 +306,100 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
 #if defined(DCTAE_PROFILING) && defined(DCTAE_C7_ABL)
   if (DCTAE_C7_ABL & 1) return;
 #endif
-  cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sbias, thr_r, ep, sk);
+  const int g16 = tid >> 4;
+  const float sb[2] = {sbias[g16], sbias[g16 + 16]};
+  cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.X), sb, thr_r, ep, sk);
 }
 
+
+// ---------------------------------------------------------------------------
+// k_cols512b (N = 512 columns of 512 x 512 images whose row pass wrote the band
+// layout T'[c][y / 4][kx][y % 4], dctae_rows512.h): the column transform runs
+// exactly like the row kernel's, one 16-lane group per column.  Block = 4 waves
+// = 16 groups over the 14 columns of one tile strip (groups 14 / 15 repeat
+// column 13 and store the same values to the same slots).
+//  * lane j of column kx loads float4 T'[c][16 b + j][kx] = rows 64 b + 4 j +
+//    (0, 2, 3, 1) (b < 8): the Makhoul pairs z[j + 16 b] = (x0, x2), mirror lane (x3, x1) --
+//    8 16-byte loads per lane and image against k_fft_cols7's 32 4-byte loads;
+//  * fft256_group (pass 1, one LDS transpose in the group's region, pass 2),
+//    Makhoul post (makhoul_step) into the strip's 448 x 14 coefficients in LDS
+//    (aliasing the transpose regions), then the token epilogue (cols_epilogue).
+// ---------------------------------------------------------------------------
+struct Cols512bLds {
+  union {
+    cf xch[16][kXchStridePk];   // per group transpose region (34,816 B)
+    float X[449 * 14];          // 448 kept rows + the spare row of the k = 64 store
+  } u;
+  float2 tw2[16][16];
+  float4 pc[256];               // c1..c4 of the Makhoul post, k < M (k = M in registers)
+};                              // 40,960 B: 4 blocks per CU
+
+__device__ __forceinline__ void cols512b_load(int c, int strip, const float* __restrict__ T, float4 (&q)[8]) {
+  const int tid = opaque_tid();
+  const int G = tid >> 4, j = tid & 15;
+  const int kx = 14 * strip + min(G, 13);
+  constexpr int KW = 448;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
+                                                      0x00020000);
+  const int o = (j * KW + kx) * 16;
+#if defined(DCTAE_PROFILING) && defined(DCTAE_C5B_ABL)
+  if (DCTAE_C5B_ABL & 4) {   // profiling ablation: no T' loads (wrong outputs)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) q[b] = make_float4(0.001f * (b + j), 0.002f * kx, 0.003f * c, 0.0004f * b);
+    return;
+  }
+#endif
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * 16 * KW * 16, 0));
+}
+
+template <bool THR>
+__device__ __forceinline__ void cols512b_compute(const ImgDesc& d, int c, int strip, Cols512bLds& L,
+                                                 const float4 (&q)[8], const float4 pcM, const float (&sb)[2],
+                                                 const float2 (&thr_r)[2][7], const EncParams& ep,
+                                                 const TokenSinks& sk) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14;
+  const int tid = opaque_tid();
+  const int G = tid >> 4, j = tid & 15;
+  const int colc = min(G, KS - 1);
+  const int s = sigma16(j);
+  const bool self0 = (j == 0), self8 = (j == 15);
+  cf v[16];
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {   // q[b] = rows 64 b + 4 j + (0, 2, 3, 1)
+    v[b] = (cf){q[b].x, q[b].y};
+    v[15 - b] = (cf){mirror16(q[b].z), mirror16(q[b].w)};
+  }
+  fft256_group(v, L.u.xch[G], j, s, L.tw2);
+  // X aliases the transpose regions: every group's pass-2 reads before any post write
+  __syncthreads();
+#if defined(DCTAE_PROFILING) && defined(DCTAE_C5B_ABL)
+  if (DCTAE_C5B_ABL & 2) {   // profiling ablation: no Makhoul post, no epilogue (wrong outputs)
+    cf acc = v[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) acc += v[i];
+    L.u.X[tid] = acc.x + acc.y;
+    __syncthreads();
+    return;
+  }
+#endif
+  float* xa = L.u.X + s * KS + colc;                 // X[s + 16 i] at + 224 i
+  float* xb = L.u.X + (N - s) * KS + colc;           // X[N - s - 16 i] at - 224 i
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const cf xx = makhoul_step(v, i, s, self0, self8, L.pc);
+    xa[224 * i] = xx.x;
+    // X[N - k] kept for k > 64; i = 4, s = 0 (k = 64) lands on the spare row 448
+    if (i >= 4) xb[-224 * i] = xx.y;
+  }
+  if (self0) L.u.X[M * KS + colc] = (pcM.x + pcM.y) * v[0].x + (pcM.w - pcM.z) * v[0].y;
+  __syncthreads();
+#if defined(DCTAE_PROFILING) && defined(DCTAE_C5B_ABL)
+  if (DCTAE_C5B_ABL & 1) return;   // profiling ablation: no token epilogue (wrong outputs)
+#endif
+  cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.u.X), sb, thr_r, ep, sk);
+}
 
 }  // namespace dctae

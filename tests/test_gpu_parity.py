@@ -148,7 +148,10 @@ def _image_slots(kp, ids):
 
 @pytest.mark.parametrize("case", ["sq224", "ragged", "real"])
 def test_encode_batch_vs_oracle(fe, pn, lfq, ref_tables, case):
-    imgs = _case_images(case)
+    _encode_vs_oracle(fe, pn, lfq, ref_tables, _case_images(case), CFG, case)
+
+
+def _encode_vs_oracle(fe, pn, lfq, ref_tables, imgs, CFG, case):
     ((dp, codes),) = fe.encode_batch([torch.from_numpy(x).to(DEV) for x in imgs], pn, lfq, return_raw=True)
     raw = dp.patches.cpu()
     codes = codes.cpu()
@@ -190,6 +193,30 @@ def test_encode_batch_vs_oracle(fe, pn, lfq, ref_tables, case):
         n_codes += gc.numel()
     print(f"[{case}] code mismatches inside the guard band: {flips} / {n_codes}")
     assert flips <= max(2, n_codes // 10000)
+
+
+@pytest.mark.parametrize("caps", [(36, 36), (32, 36), (36, 32), (20, 32), (32, 20)])
+def test_encode_512_patch_caps_vs_oracle(pkg, lfq, ref_tables, caps):
+    """512-wide / 512-high images at max_patch_h / max_patch_w != 32: the kept
+    corner is 14 * min(36, cap) (FE:312-345, 392-399), so the 512^2 kernels that
+    assume 448 kept rows / columns (k_rows512pk, k_fft_cols7, k_cols512b) must
+    hand these to the general kernels.  Tables: the reference fit extended to
+    the 36 x 36 grid by repeating the last row / column."""
+    mh, mw = caps
+    cfg = ref_cpu.FEConfig(max_patch_h=mh, max_patch_w=mw, max_seq_len=3 * mh * mw)
+    ih = torch.clamp(torch.arange(mh), max=31)
+    iw = torch.clamp(torch.arange(mw), max=31)
+    med = ref_tables.median[:, ih][:, :, iw].contiguous()
+    b = ref_tables.b[:, ih][:, :, iw].contiguous()
+    tables = ref_cpu.NormTables(ref_tables.n[:, ih][:, :, iw].contiguous(), med, b)
+    pn = pkg.PatchNorm(mh, mw, 14, 3).to(DEV)
+    pn.median.data.copy_(med)
+    pn.b.data.copy_(b)
+    pn.frozen = True
+    pn.eval()
+    fe = pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, mh, mw, 3 * mh * mw)
+    imgs = rng.synth_images(57, [(512, 512), (512, 512), (512, 300), (300, 512)])
+    _encode_vs_oracle(fe, pn, lfq, tables, imgs, cfg, f"caps {caps}")
 
 
 def test_norm_lfq_bit_exact_on_reference_tokens(pkg, pn, lfq):
@@ -567,10 +594,11 @@ def test_thresholds_are_exact(pn):
     assert torch.all(y_at > 0) and torch.all(y_below <= 0)
 
 
-DEFAULTS = {"rows_kernel": 4, "sort_kernel": 2, "chunk_bytes": 1 << 40}
+DEFAULTS = {"rows_kernel": 4, "sort_kernel": 2, "chunk_bytes": 1 << 40, "cols512b": 1}
 SPEC_VARIANTS = {  # option sets of the specialised kernels (reset to DEFAULTS afterwards)
     "default": {},
     "rows_lds": {"rows_kernel": 2},
+    "cols7": {"cols512b": 0},
     "sort_bitonic": {"sort_kernel": 1},
     "chunks": {"chunk_bytes": 4 << 20},
 }

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Iteration: parity tests selected by TESTS (pytest -k), then a same-box A/B of
+# the encode bench over option sets ("opt=v opt=v" per argument; a leading
+# "lib=<path>" selects another libdctae.so build).  DEC=1 adds the config-3
+# decode leg.  Each GPU step time-limited; stop at the first failure.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+if [ -n "${TESTS:-}" ]; then
+  timeout -k 10 600 python -u -m pytest ${TFILES:-tests/test_gpu_parity.py} -m gpu -x -q -rf --timeout 200 \
+      --timeout-method thread -k "$TESTS" > gpurun_out/try_tests.log 2>&1
+  rc=$?; tail -4 gpurun_out/try_tests.log
+  if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED|error" gpurun_out/try_tests.log | head -40; exit $rc; fi
+fi
+for opts in "$@"; do
+  args=""
+  unset DCTAE_LIBRARY
+  for o in $opts; do
+    case $o in lib=*) export DCTAE_LIBRARY="${o#lib=}";; *) args="$args --opt $o";; esac
+  done
+  dec="--no-decode"; [ -n "${DEC:-}" ] && dec=""
+  timeout -k 10 300 python bench.py --steps ${STEPS:-30} --warmup 3 --no-cpu-baseline $dec --no-stats \
+      --no-configs --no-model $args > gpurun_out/try_bench.log 2>&1
+  rc=$?
+  echo "=== [$opts] rc=$rc"
+  if [ $rc -ne 0 ]; then tail -20 gpurun_out/try_bench.log; exit $rc; fi
+  grep '^{' gpurun_out/try_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps({k:v['avg_ms'] for k,v in d['kernels'].items()}), json.dumps({k: v.get('avg_ms') for k, v in d.get('decode', {}).get('kernels', {}).items()}), d.get('decode', {}).get('ms_per_step'))"
+done
