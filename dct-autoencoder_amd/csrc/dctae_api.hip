@@ -1005,6 +1005,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     D[i].tband = ctx->cols512b && ctx->rows_kernel == 4 && cfg->max_patch_w == 32 && cfg->max_patch_h == 32 &&
                  D[i].H == 512 && D[i].W == 512 && D[i].bs == 0 && D[i].plan_w >= 0 &&
                  plans[D[i].plan_w].spec == 1 && D[i].plan_h >= 0 && plans[D[i].plan_h].spec == 1;
+    // packed encodes of band images: item-major token staging (stage_pos; the
+    // staging is internal there, while dctae_spectrum_tokens hands it out in flat order)
+    if (full && D[i].tband) D[i].tband |= 2;
   }
   if (full)
     for (int r = 0; r < pack->n_rows; ++r)
@@ -2113,19 +2116,14 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
     Timer t(ctx, s, "dec_map");
     launch_dec_map((int64_t)n_rows * S, dd, a, map, s);
   }
-  // band layout of U (k_idct_cols512b -> k_idct_rows512<448, true>) at Kw = 448
-  const bool band = ctx->cols512b && ctx->dec_rows_kernel == 3 && D[0].qw == 32;
   {
     Timer t(ctx, s, "idct_cols");
-    if (band)
-      launch_idct_cols512b(dd, n_img, ctx->ws, map, tw, pre, a, s);
-    else
-      launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
+    launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
   }
   {
     Timer t(ctx, s, "idct_rows");
     if (ctx->dec_rows_kernel == 3 && D[0].qw == 32)
-      launch_idct_rows512(dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s, band);
+      launch_idct_rows512(dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
     else
       launch_idct_rows_spec(1, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
   }

@@ -18,7 +18,6 @@
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
 #include "dctae_launch.h"
-#include "dctae_rows512.h"
 
 namespace dctae {
 
@@ -300,171 +299,6 @@ __global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// Band-layout column pass (k_idct_cols512b; 512 x 512 images at Kw = 448, the
-// mirror of the encode's k_cols512b): one 16-lane group per column of the
-// strip, the DCT-III of the column exactly as k_idct_rows512 runs a row, and
-// U written in the band layout U'[c][y/4][kx][y%4] that k_idct_rows512<448,
-// true> reads (each lane's output pixels 64 b + 4 j .. + 3 are one float4).
-// A block = 512 threads = two images at a time (halves of 16 groups):
-//   1. every lane expands ONE tile row (h = tid / 16, row jl) of both images:
-//      tokens -> X[img][ky][col] (ky < 448; zero for tiles h >= qh and absent
-//      tokens), with the row's inverse-PatchNorm values of code bits 1 / 0 held
-//      in registers for all the block's images (28 VGPRs: one tile row per
-//      lane instead of two keeps the kernel at 4 waves / SIMD);
-//   2. block barrier; lane j of column col (its half's image): Ys[k], Ys[M + k],
-//      Ys[M - k], Ys[N - k] of k = j + 16 r from X (14-float rows: the 16 lanes
-//      of a column hit 16 distinct even banks; pairs M * 14 floats apart are
-//      ds_read2st64), conj Z_k;
-//   3. block barrier (X is aliased by the transpose regions); fft256_group
-//      (natural butterflies: lane j ends with W[j + 16 i]);
-//   4. output quads -> 8 float4 stores per lane; block barrier.
-// ---------------------------------------------------------------------------
-struct IColsBLds {
-  union {
-    float x[448 * 14];                // 25,088 B
-    cf xch[16][kXchStridePk];         // 34,816 B (the row kernel's transpose regions)
-  } u[2];
-  float2 tw2[16][16];
-  float4 pre[256];
-};                                    // 75,776 B: 2 blocks (16 waves) per CU
-
-__device__ __forceinline__ float bmirror16(float x) {   // lane l <- lane 15 - l of its 16-lane row
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float bror16(float x) {      // lane l <- lane l - 1 (mod 16)
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x121, 0xf, 0xf, false));
-}
-
-// step 1 for one image: this lane's tile row (h, jl) -> X rows 14 h + jl
-// (CODES: LFQ codes -> +-scale -> inverse PatchNorm; else normalised patches)
-template <bool CODES>
-__device__ __forceinline__ void idct_colb_expand(int img, int qh, int c, int strip, const int32_t* __restrict__ map,
-                                                 const DecodeArgs& a, const float2 (&vt)[14], float* __restrict__ X) {
-  constexpr int KS = 14, PP = KS * KS;
-  const int tid = itid();
-  const int h = tid >> 4, jl = tid & 15;
-  int32_t sl = map[(((int64_t)img * 3 + c) * a.maxph + (h < qh ? h : 0)) * a.maxpw + strip];
-  if (h >= qh) sl = -1;
-  const int64_t s0 = sl >= 0 ? sl : 0;   // unconditional loads
-  int32_t code = 0;
-  float pv[KS];
-  if constexpr (CODES) {
-    code = (int32_t)a.codes[s0 * a.ncb + (jl < KS ? jl : 0)];
-  } else {
-    const float* pt = a.patches + s0 * PP + (jl < KS ? jl : 0) * KS;
-#pragma unroll
-    for (int p = 0; p < KS; ++p) pv[p] = pt[p];
-  }
-  if (jl < KS) {
-    f2v* xr = reinterpret_cast<f2v*>(X + (KS * h + jl) * KS);
-#pragma unroll
-    for (int p = 0; p < KS / 2; ++p) {
-      float v0, v1;
-      if constexpr (CODES) {
-        // bit select by masks: a ?: on the pair lets the compiler select the
-        // address instead and move vt to scratch
-        const uint32_t m0 = 0u - ((uint32_t)(code >> (KS - 1 - 2 * p)) & 1u);
-        const uint32_t m1 = 0u - ((uint32_t)(code >> (KS - 2 - 2 * p)) & 1u);
-        v0 = __uint_as_float((__float_as_uint(vt[2 * p].x) & m0) | (__float_as_uint(vt[2 * p].y) & ~m0));
-        v1 = __uint_as_float((__float_as_uint(vt[2 * p + 1].x) & m1) | (__float_as_uint(vt[2 * p + 1].y) & ~m1));
-      } else {
-        v0 = pv[2 * p];
-        v1 = pv[2 * p + 1];
-      }
-      xr[p] = sl >= 0 ? (f2v){v0, v1} : (f2v){0.0f, 0.0f};
-    }
-  }
-}
-
-// steps 2 - 4 for the image of this thread's half (X = that image's strip)
-__device__ __forceinline__ void idct_colb_columns(const ImgDesc& d, int c, int strip, float* __restrict__ ws,
-                                                  IColsBLds& L, int half) {
-#pragma clang fp contract(fast)
-  constexpr int N = 512, M = 256, KS = 14, KW = 448;
-  const int t2 = itid() & 255;
-  const int G = t2 >> 4, j = t2 & 15, col = min(G, KS - 1);   // groups 14 / 15 redo column 13
-  cf v[16];
-  {
-    // conj Z_k, k = j + 16 r, straight from X: rows k / M + k and M - k / N - k
-    // are M * 14 floats apart (ds_read2st64 pairs); rows >= Kh = 448 are zero
-    const float* xc = L.u[half].x + col;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k = j + 16 * r;
-      float yk = xc[k * KS];
-      const float ymk = r < 12 ? xc[(M + k) * KS] : 0.0f;           // Ys[M + k]
-      const float ymk2 = xc[(M - k) * KS];                           // Ys[M - k] (k = 0: Ys[M])
-      const float ynk = (r > 4 || (r == 4 && j > 0)) ? xc[(N - k) * KS] : 0.0f;   // Ys[N - k], N - k < 448
-      if (r == 0 && j == 0) yk *= 1.41421356237309515f;
-      v[r] = pre_z(yk, ynk, ymk, ymk2, L.pre[k]);
-    }
-  }
-  __syncthreads();   // every group's X reads before the transpose regions (aliased on X) are written
-  fft256_group(v, L.u[half].xch[G], j, j, L.tw2);
-  const int kx = KS * strip + col;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws + d.ws_t + (int64_t)c * N * KW, 0, N * KW * 4, 0x00020000);
-  const int o = (j * KW + kx) * 16;
-#pragma unroll
-  for (int b = 0; b < 8; ++b) {
-    const float mr = bmirror16(v[15 - b].x), mi = bmirror16(v[15 - b].y);
-    __builtin_amdgcn_raw_buffer_store_b128(
-        (v4u){__float_as_uint(v[b].x), __float_as_uint(-mi), __float_as_uint(-v[b].y), __float_as_uint(mr)}, rsrc, o,
-        b * 16 * KW * 16, 0);
-  }
-}
-
-// block = (channel, strip) item x IPB consecutive images, two at a time; items
-// dealt so the 8 XCD groups (b % 8) own contiguous runs of 12 strips
-#ifndef DCTAE_IC5B_WPE
-#define DCTAE_IC5B_WPE 4   // 2 blocks (16 waves) per CU: 128 VGPRs (12 spilled, the expansion's table values)
-#endif
-template <int IPB, bool CODES>
-__global__ __launch_bounds__(512, DCTAE_IC5B_WPE) void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
-                                                       float* __restrict__ ws, const int32_t* __restrict__ map,
-                                                       const float2* __restrict__ tw, const float4* __restrict__ pre,
-                                                       DecodeArgs a) {
-  constexpr int KS = 14, PP = KS * KS, per_x = 12;   // 96 items = 3 channels x 32 strips
-  static_assert(IPB % 2 == 0, "two images per round");
-  __shared__ IColsBLds L;
-  const int b = blockIdx.x, slot = b >> 3;
-  const int t = (b & 7) * per_x + slot % per_x, i0 = (slot / per_x) * IPB;
-  if (i0 >= n_img) return;
-  const int c = t >> 5, strip = t & 31;
-  const int tid = threadIdx.x;
-  if (tid < 256) {
-    L.tw2[tid >> 4][tid & 15] = tw[(tid >> 4) * (tid & 15)];
-    L.pre[tid] = pre[tid];
-  }
-  // image-independent values of this thread's tile row: inverse PatchNorm of
-  // y = +scale (code bit 1) and y = -scale (bit 0), patchnorm.py:167-177
-  float2 vt[KS];
-  if constexpr (CODES) {
-    const int h = min(tid >> 4, a.maxph - 1), jl = tid & 15;
-    const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + (jl < KS ? jl : 0) * KS;
-    const float yp = __fsub_rn(__fmul_rn(1.0f, a.scale * 2.0f), a.scale);   // lfq.py:105-134
-    const float yn = __fsub_rn(__fmul_rn(0.0f, a.scale * 2.0f), a.scale);
-#pragma unroll
-    for (int p = 0; p < KS; ++p) {
-      const float m = a.median[tab + p], bb = a.b[tab + p];
-      vt[p] = make_float2(pn_inverse(yp, m, bb, a.eps), pn_inverse(yn, m, bb, a.eps));
-    }
-  }
-  const int half = tid >> 8;
-#pragma unroll 1
-  for (int u = 0; u < IPB; u += 2) {
-    const int ia = i0 + u;
-    if (ia >= n_img) break;
-    const bool two = ia + 1 < n_img;
-    idct_colb_expand<CODES>(ia, imgs[ia].qh, c, strip, map, a, vt, L.u[0].x);
-    if (two) idct_colb_expand<CODES>(ia + 1, imgs[ia + 1].qh, c, strip, map, a, vt, L.u[1].x);
-    __syncthreads();   // X of both images (and the tables, first round)
-    if (half == 0 || two) idct_colb_columns(imgs[ia + half], c, strip, ws, L, half);
-    else __syncthreads();   // the column step's barrier, joined by the idle half
-    __syncthreads();   // transpose-region reads before the next round's X writes
-  }
-}
-
-// ---------------------------------------------------------------------------
 // rows: one wave = one image row, 3 channels; 16 rows per block.
 //   U[c][y][kx] (kx < Kw, zero beyond) -> conj Z_k -> FFT -> x[px] -> IPT -> RGB
 // ---------------------------------------------------------------------------
@@ -615,20 +449,6 @@ void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, cons
   if (n_img > 0)
     hipLaunchKernelGGL((k_idct_cols512<IPB>), dim3(grid), dim3(256), 0, s, imgs, n_img, n_items, qw, ws, map, tw,
                        pre, a);
-}
-
-void launch_idct_cols512b(const ImgDesc* imgs, int n_img, float* ws, const int32_t* map, const float2* tw,
-                          const float4* pre, const DecodeArgs& a, hipStream_t s) {
-#ifndef DCTAE_IC5B_IPB
-#define DCTAE_IC5B_IPB 4
-#endif
-  constexpr int IPB = DCTAE_IC5B_IPB;
-  const int grid = 96 * ((n_img + IPB - 1) / IPB);
-  if (n_img > 0)
-    if (a.use_codes)
-      hipLaunchKernelGGL((k_idct_cols512b<IPB, true>), dim3(grid), dim3(512), 0, s, imgs, n_img, ws, map, tw, pre, a);
-    else
-      hipLaunchKernelGGL((k_idct_cols512b<IPB, false>), dim3(grid), dim3(512), 0, s, imgs, n_img, ws, map, tw, pre, a);
 }
 
 void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,

@@ -42,9 +42,7 @@ struct IRows512Lds {
 
 }  // namespace
 
-// BAND: U in the band layout U'[c][y/4][kx][y%4] (k_idct_cols512b): the 64
-// lanes of a wave (4 rows x 16 kx) then read 256 contiguous bytes per load
-template <int KW, bool BAND>
+template <int KW>
 __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                       const float* __restrict__ ws, float* __restrict__ rgb,
                                                       const float2* __restrict__ tw, const float4* __restrict__ pre,
@@ -67,18 +65,16 @@ __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict_
   const int H = d.H;
   const int yl = min(y, H - 1);   // rows past H compute a duplicate and store nothing
   const int64_t cstride = (int64_t)H * KW;
-  // element kx of row y: row-major at y KW + kx; band layout at ((y / 4) KW + kx) 4 + y % 4
-  const float* src = BAND ? ws + d.ws_t + ((int64_t)(yl >> 2) * KW + j) * 4 + (yl & 3) : ws + d.ws_t + (int64_t)yl * KW + j;
-  constexpr int KST = BAND ? 4 : 1;   // float step per kx
+  const float* src = ws + d.ws_t + (int64_t)yl * KW + j;
 
   // ---- loads: A[c][r] = Ys[j + 16 r], B[c][r] = Ys[256 + j + 16 r] (r < NB)
   float A[3][16], B[3][NB];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) A[c][r] = src[c * cstride + KST * 16 * r];
+    for (int r = 0; r < 16; ++r) A[c][r] = src[c * cstride + 16 * r];
 #pragma unroll
-    for (int r = 0; r < NB; ++r) B[c][r] = src[c * cstride + KST * (M + 16 * r)];
+    for (int r = 0; r < NB; ++r) B[c][r] = src[c * cstride + M + 16 * r];
   }
   __syncthreads();   // tables
 
@@ -186,13 +182,9 @@ __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict_
 }
 
 void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
-                         const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s, bool band) {
+                         const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s) {
   if (n_blocks <= 0) return;
-  if (band)
-    hipLaunchKernelGGL((k_idct_rows512<448, true>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre, cm);
-  else
-    hipLaunchKernelGGL((k_idct_rows512<448, false>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre,
-                       cm);
+  hipLaunchKernelGGL(k_idct_rows512<448>, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre, cm);
 }
 
 }  // namespace dctae

@@ -31,8 +31,21 @@ struct ImgDesc {
   int32_t row, col, k, local_id;  // packing
   int32_t plan_w, plan_h;         // FFT plan index for rows (length W) / cols (length H); -1 = GEMM
   int32_t bs;        // bit 0: rows, bit 1: columns on the Bluestein kernels (columns: Y + k_tile_epilogue)
-  int32_t tband;     // 1: the row pass writes T in the band layout T'[c][y/4][kx][y%4] (512 x 512 on k_rows512pk + k_cols512b)
+  int32_t tband;     // bit 0: the row pass writes T in the band layout T' (512 x 512 on k_rows512pk + k_cols512b);
+                     // bit 1: item-major token staging (stage_pos), packed encodes of band images only (qh = qw = 32)
 };
+
+// Token staging position of flat token f = (h qw + w) 3 + c (FE:374-380 order,
+// the sort's tie order): flat, or with tband bit 1 item-major (c qw + w) qh + h,
+// so the 32 tokens of one column-kernel item (channel c, tile strip w) are
+// contiguous staging (full cache lines from one workgroup instead of 28-byte
+// pieces shared by the three channels' items on three XCDs).  C = 3.
+__host__ __device__ inline int stage_pos(const ImgDesc& d, int f) {
+  if (!(d.tband & 2)) return f;
+  // band images have qh = qw = 32 (512 x 512 at max_patch 32 x 32): no runtime division
+  const int c = f % 3, s = f / 3, h = s >> 5, w = s & 31;
+  return ((c << 5) + w) * 32 + h;
+}
 
 // Generic batched strided fp32 GEMM problem:
 //   O[c][m][n] = sum_k A[c][m][k] * B[c][n][k]     (c < C)

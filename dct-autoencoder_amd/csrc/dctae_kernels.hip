@@ -499,7 +499,8 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int i = tid; i < np2; i += nt) {
     uint64_t k = 0;
-    if (i < d.T) k = ((uint64_t)float_key(st.scores[d.tok_off + i]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
+    if (i < d.T)
+      k = ((uint64_t)float_key(st.scores[d.tok_off + stage_pos(d, i)]) << 32) | (uint64_t)(0xFFFFFFFFu - (uint32_t)i);
     keys[i] = k;
   }
   // bitonic sort, descending
@@ -530,13 +531,13 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
     out.ch[o] = c;
     out.ids[o] = d.local_id;
     if (out.key_pad) out.key_pad[o] = 0;
-    if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
+    if (out.scores) out.scores[o] = st.scores[d.tok_off + stage_pos(d, f)];
   }
   if (out.codes) {
     const int ncb = ep.ncb;
     for (int e = tid; e < d.k * ncb; e += nt) {
       const int t = e / ncb, q = e % ncb;
-      const uint32_t f = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu);
+      const uint32_t f = stage_pos(d, 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu));
       out.codes[(base + t) * ncb + q] = (int64_t)lfq_index_bits(st.codes[(d.tok_off + f) * ncb + q], ep.code_pos,
                                                                 ep.code_neg);
     }
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(1024) void k_sort_pack(const ImgDesc* __restrict__ 
   if (out.patches || out.raw) {
     for (int64_t e = tid; e < (int64_t)d.k * PP; e += nt) {
       const int t = (int)(e / PP), q = (int)(e % PP);
-      const uint32_t f = 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu);
+      const uint32_t f = stage_pos(d, 0xFFFFFFFFu - (uint32_t)(keys[t] & 0xFFFFFFFFu));
       if (out.patches) out.patches[(base + t) * PP + q] = st.norm[(d.tok_off + f) * PP + q];
       if (out.raw) out.raw[(base + t) * PP + q] = st.raw[(d.tok_off + f) * PP + q];
     }
@@ -588,21 +589,25 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
                                                         TokenSinks st, PackSinks out) {
   using Sort = rocprim::block_radix_sort<uint32_t, kSortBS, kSortIPT, uint32_t>;
   __shared__ typename Sort::storage_type tmp;
-  __shared__ uint16_t order[kSortBS * kSortIPT];
+  __shared__ uint16_t order[kSortBS * kSortIPT];   // flat token index f of rank t
+  __shared__ uint16_t spos[kSortBS * kSortIPT];    // its staging position (stage_pos)
   const int tid = threadIdx.x;
   const ImgDesc d = imgs[blockIdx.x];
   uint32_t keys[kSortIPT], vals[kSortIPT];
 #pragma unroll
   for (int i = 0; i < kSortIPT; ++i) {
     const int idx = tid * kSortIPT + i;   // blocked: input order = index order (stability -> index asc)
-    keys[i] = idx < d.T ? float_key(st.scores[d.tok_off + idx]) : 0u;
+    keys[i] = idx < d.T ? float_key(st.scores[d.tok_off + stage_pos(d, idx)]) : 0u;
     vals[i] = (uint32_t)idx;
   }
   Sort().sort_desc_to_striped(keys, vals, tmp);
 #pragma unroll
   for (int i = 0; i < kSortIPT; ++i) {
     const int rank = tid + kSortBS * i;
-    if (rank < d.k) order[rank] = (uint16_t)vals[i];
+    if (rank < d.k) {
+      order[rank] = (uint16_t)vals[i];
+      spos[rank] = (uint16_t)stage_pos(d, (int)vals[i]);
+    }
   }
   __syncthreads();
   const int S = ep.S, PP = ep.P * ep.P, C = ep.C;
@@ -621,7 +626,7 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     out.ids[o] = d.local_id;
 #endif
     if (out.key_pad) out.key_pad[o] = 0;
-    if (out.scores) out.scores[o] = st.scores[d.tok_off + f];
+    if (out.scores) out.scores[o] = st.scores[d.tok_off + spos[t]];
   }
   if (out.codes && ep.ncb == 14) {
     // two codes per lane: one u32 of the u16 staging -> one 16-byte int64 pair (coalesced)
@@ -630,7 +635,7 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     const uint32_t pos2 = ep.code_pos | (ep.code_pos << 16), neg2 = ep.code_neg | (ep.code_neg << 16);
     for (int e = tid; e < d.k * 7; e += kSortBS) {
       const int t = e / 7, q = e - t * 7;
-      const uint32_t v = (uint32_t)lfq_index_bits(src[(d.tok_off + order[t]) * 7 + q], pos2, neg2);
+      const uint32_t v = (uint32_t)lfq_index_bits(src[(d.tok_off + spos[t]) * 7 + q], pos2, neg2);
       // write-once outputs: nontemporal stores (their lines leave the L2 /
       // Infinity Cache early instead of being written back under the next
       // step's row kernel: sort 0.146 -> 0.143 ms, next rows 1.13 -> 1.11 ms)
@@ -642,10 +647,10 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     for (int e = tid; e < d.k * ncb; e += kSortBS) {
       const int t = e / ncb, q = e - t * ncb;
       out.codes[(base + t) * ncb + q] =
-          (int64_t)lfq_index_bits(st.codes[(d.tok_off + order[t]) * ncb + q], ep.code_pos, ep.code_neg);
+          (int64_t)lfq_index_bits(st.codes[(d.tok_off + spos[t]) * ncb + q], ep.code_pos, ep.code_neg);
     }
   }
-  if (out.patches || out.raw) gather_tokens(d, order, base, PP, st, out, tid, kSortBS);
+  if (out.patches || out.raw) gather_tokens(d, spos, base, PP, st, out, tid, kSortBS);
 }
 
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,

@@ -96,10 +96,7 @@ void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, in
                            float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 
 void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
-                         const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s, bool band = false);
-// band-layout decode columns (U' for k_idct_rows512<448, true>); 512 x 512 at Kw = 448
-void launch_idct_cols512b(const ImgDesc* imgs, int n_img, float* ws, const int32_t* map, const float2* tw,
-                          const float4* pre, const DecodeArgs& a, hipStream_t s);
+                         const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                     const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s);
 

@@ -35,6 +35,28 @@ namespace dctae {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+// Layout of the band-layout T' (float4 = 4 rows of one column kx; band4 = y / 4):
+//   0: [band4][448 kx][4]                 (a wave's store: 1 KB contiguous)
+//   1: [kx / 14][band4][14][4]            (strip-major: a column block reads 3.5 KB runs)
+//   2: [band4 / 4][448 kx][16]            (a row block's channel: 28 KB contiguous)
+//   3: [kx / 112][band4 / 4][112][16]     (7 KB granules on both sides)
+#ifndef DCTAE_TLAYOUT
+#define DCTAE_TLAYOUT 0
+#endif
+__device__ __forceinline__ int t4_index(int band4, int kx) {
+#if DCTAE_TLAYOUT == 0
+  return band4 * 448 + kx;
+#elif DCTAE_TLAYOUT == 1
+  const int st = (kx * 4682) >> 16;   // kx / 14 for kx < 2048
+  return (st * 128 + band4) * 14 + kx - 14 * st;
+#elif DCTAE_TLAYOUT == 2
+  return ((band4 >> 2) * 448 + kx) * 4 + (band4 & 3);
+#else
+  const int sg = (kx * 586) >> 16;    // kx / 112 for kx < 783
+  return ((sg * 32 + (band4 >> 2)) * 112 + kx - 112 * sg) * 4 + (band4 & 3);
+#endif
+}
+
 __device__ __forceinline__ float mirror16(float x) {   // lane l <- lane 15 - l of its 16-lane row
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, false));
 }
@@ -233,11 +255,15 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
   const int rown4 = s >= 1 ? rown : 0x7ffffff0;   // i = 4: k = 64 + s, X[N - k] kept iff s >= 1
   // band stores (bytes): after xpose4_rows lane (g, s) of block q holds the
   // wave's four rows of column s + 16 (4 q + g) (X[k]) / N - s - 16 (4 q + g) (X[N - k])
-  const int bo = ((y0 >> 2) + wv) * KW;   // first float4 of this wave's band
-  const int bk = (bo + s + 16 * g) * 16;                 // + 1024 q
-  const int bn = (bo + N - s - 16 * g) * 16 - 3072;      // + 1024 (3 - q)
-  const int bn1 = (g == 0 && s == 0) ? 0x7ffffff0 : bn;  // q = 1: column 448 (k = 64) is not kept
-  const int bm = j == 0 ? ((bo + M) * 4 + ((0x2130 >> (4 * g)) & 3)) * 4 : 0x7ffffff0;   // slot of row g: 0, 3, 1, 2
+  const int bnd = (y0 >> 2) + wv;
+  int bkq[4], bnq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bkq[q] = t4_index(bnd, s + 16 * (4 * q + g)) * 16;
+    bnq[q] = t4_index(bnd, N - s - 16 * (4 * q + g)) * 16;
+  }
+  bnq[1] = (g == 0 && s == 0) ? 0x7ffffff0 : bnq[1];   // column 448 (k = 64) is not kept
+  const int bm = j == 0 ? t4_index(bnd, M) * 16 + 4 * ((0x2130 >> (4 * g)) & 3) : 0x7ffffff0;   // slot of row g: 0, 3, 1, 2
 
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -248,9 +274,47 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
       v[b] = A[c][b];
       v[15 - b] = (cf){mirror16(B[c][b].x), mirror16(B[c][b].y)};
     }
+#if DCTAE_TLAYOUT == 2
+    if (band && c > 0) __syncthreads();   // the previous channel's staged-output reads (aliased on xch)
+#endif
     fft256_group(v, xr, j, s, L.tw2);
     // ---- Makhoul post: k = s + 16 i, A = Z[k] = v[i], P = Z[M - k]
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(T + (int64_t)c * H * KW, 0, plane_bytes, 0x00020000);
+#if DCTAE_TLAYOUT == 2
+    if constexpr (band) {
+      // band16 layout [y / 16][kx][16 rows]: the block's 16 rows of a channel are
+      // one contiguous 28 KB piece; staged through LDS (aliasing the transpose
+      // regions) so every wave stores whole 1 KB pieces.  Row r = 4 w + g of
+      // column kx at kx 16 + 4 (w ^ ((kx >> 1) & 3)) + slot(g) (slots 0, 3, 1, 2:
+      // the column kernel's Makhoul pairs (x0, x2) / (x3, x1) adjacent; the XOR
+      // spreads a group's 16 lanes over 8 bank pairs)
+      float* ob = reinterpret_cast<float*>(&X.xch[0][0][0]);
+      const int sg = (0x2130 >> (4 * g)) & 3;
+      // (kx >> 1) & 3 of kx = s + 16 i / N - s - 16 i does not depend on i
+      float* oa = ob + s * 16 + 4 * (wv ^ ((s >> 1) & 3)) + sg;              // + 256 i
+      float* on = ob + (N - s) * 16 + 4 * (wv ^ (((N - s) >> 1) & 3)) + sg;  // - 256 i
+      __syncthreads();   // every group's pass-2 reads of xch
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const cf xx = makhoul_step(v, i, s, self0, self8, L.pc);
+        oa[256 * i] = xx.x;
+        if (i >= 5 || (i == 4 && s >= 1)) on[-256 * i] = xx.y;
+      }
+      if (self0) {
+        const float4 cc = L.pc[M];
+        ob[M * 16 + 4 * wv + sg] = (cc.x + cc.y) * v[0].x + (cc.w - cc.z) * v[0].y;   // (M >> 1) & 3 = 0
+      }
+      __syncthreads();
+      // wave wv stores 16-column chunks wv * 7 .. wv * 7 + 6 (1 KB each)
+      const int l = tid & 63;
+      const int kx0 = 112 * wv + (l >> 2), qd = l & 3;   // + 16 it; (kx >> 1) & 3 = (l >> 3) & 3
+      const float4* rd = reinterpret_cast<const float4*>(ob + kx0 * 16 + 4 * (qd ^ ((l >> 3) & 3)));
+      const int go = (((y0 >> 4) * KW + kx0) * 4 + qd) * 16;
+#pragma unroll
+      for (int it = 0; it < 7; ++it)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, rd[64 * it]), rsrc, go, 1024 * it, 0);
+    } else
+#endif
     if constexpr (band) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -264,12 +328,12 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
         xpose4_rows(rk);
         __builtin_amdgcn_raw_buffer_store_b128(
             (v4u){__float_as_uint(rk[0]), __float_as_uint(rk[2]), __float_as_uint(rk[3]), __float_as_uint(rk[1])},
-            rsrc, bk, 1024 * q, 0);
+            rsrc, bkq[q], 0, 0);
         if (q >= 1) {   // X[N - k], k = s + 16 i, is kept for k > 64
           xpose4_rows(rn);
           __builtin_amdgcn_raw_buffer_store_b128(
               (v4u){__float_as_uint(rn[0]), __float_as_uint(rn[2]), __float_as_uint(rn[3]), __float_as_uint(rn[1])},
-              rsrc, q == 1 ? bn1 : bn, 1024 * (3 - q), 0);
+              rsrc, bnq[q], 0, 0);
         }
       }
     } else {
@@ -282,7 +346,7 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
       }
     }
     // k = M (s = 0, lane 0): A = P = Z[0]: X[M] = (c1 + c2) Z0.x + (c4 - c3) Z0.y
-    {
+    if (!(band && DCTAE_TLAYOUT == 2)) {   // band16: X[M] went through LDS
       const float4 cc = L.pc[M];
       const float xm = (cc.x + cc.y) * v[0].x + (cc.w - cc.z) * v[0].y;
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(xm), rsrc,

@@ -67,6 +67,11 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
   constexpr int KS = 14, EPR = 2;
   const int tid = opaque_tid();
   const int g16 = tid >> 4, jl = tid & 15;
+  // staging index of tile (h, strip) of channel c (flat or item-major, stage_pos)
+  const bool im = (d.tband & 2) != 0;
+  auto tok_of = [&](int h) -> int64_t {
+    return d.tok_off + (im ? (c * d.qw + strip) * d.qh + h : (h * d.qw + strip) * ep.C + c);
+  };
   // token outputs (raw DCT / PatchNorm) leave through LDS: tile h's 14 rows
   // of 14 are the 196 contiguous floats X[196 h ..], the token's staged
   // layout, so the whole block stores them as 16-byte pieces (49 per token)
@@ -75,7 +80,7 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
   auto store_tokens = [&](float* dst) {
     for (int e = tid; e < d.qh * 49; e += 256) {
       const int h = e / 49, q = e - h * 49;
-      const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
+      const int64_t tok = tok_of(h);
       reinterpret_cast<float4*>(dst + tok * (KS * KS))[q] = reinterpret_cast<const float4*>(Xf + KS * KS * h)[q];
     }
   };
@@ -100,7 +105,7 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
         am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x124, 0xf, 0xf, false));
         am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x122, 0xf, 0xf, false));
         am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x121, 0xf, 0xf, false));
-        const int64_t tok = d.tok_off + (h * d.qw + strip) * ep.C + c;
+        const int64_t tok = tok_of(h);
         if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sb[r]);
         if (jl < KS && sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
       }
@@ -124,16 +129,16 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
         vals[2 * p] = v2.x;
         vals[2 * p + 1] = v2.y;
       }
-      const int f = (h * d.qw + strip) * ep.C + c;
+      const int64_t tok = tok_of(h);
       if (norm) {   // scores, codes and the PatchNorm values (patchnorm.py:157-165), written back in place
         float y[KS];
-        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sc, y);
+        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, tok, sc, y);
         if (jl < KS) {
 #pragma unroll
           for (int p = 0; p < KS / 2; ++p) row[p] = (f2v){y[2 * p], y[2 * p + 1]};
         }
       } else {
-        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, d.tok_off + f, sc);   // scores, codes
+        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, tok, sc);   // scores, codes
       }
     }
     if (norm) {
@@ -337,11 +342,13 @@ struct Cols512bLds {
 __device__ __forceinline__ void cols512b_load(int c, int strip, const float* __restrict__ T, float4 (&q)[8]) {
   const int tid = opaque_tid();
   const int G = tid >> 4, j = tid & 15;
-  const int kx = 14 * strip + min(G, 13);
   constexpr int KW = 448;
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
                                                       0x00020000);
-  const int o = (j * KW + kx) * 16;
+  const int kx = 14 * strip + min(G, 13);
+  const int o = t4_index(j, kx) * 16;                                 // band4 = 16 b + j
+  constexpr int bstep = (DCTAE_TLAYOUT == 0 ? 16 * KW : DCTAE_TLAYOUT == 1 ? 16 * 14
+                         : DCTAE_TLAYOUT == 2 ? 16 * KW : 16 * 112) * 16;   // t4_index(16, kx) - t4_index(0, kx)
 #if defined(DCTAE_PROFILING) && defined(DCTAE_C5B_ABL)
   if (DCTAE_C5B_ABL & 4) {   // profiling ablation: no T' loads (wrong outputs)
 #pragma unroll
@@ -351,7 +358,7 @@ __device__ __forceinline__ void cols512b_load(int c, int strip, const float* __r
 #endif
 #pragma unroll
   for (int b = 0; b < 8; ++b)
-    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * 16 * KW * 16, 0));
+    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, 0));
 }
 
 template <bool THR>

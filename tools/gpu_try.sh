@@ -25,5 +25,5 @@ for opts in "$@"; do
   rc=$?
   echo "=== [$opts] rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 gpurun_out/try_bench.log; exit $rc; fi
-  grep '^{' gpurun_out/try_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps({k:v['avg_ms'] for k,v in d['kernels'].items()}), json.dumps({k: v.get('avg_ms') for k, v in d.get('decode', {}).get('kernels', {}).items()}), d.get('decode', {}).get('ms_per_step'))"
+  grep '^{' gpurun_out/try_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], json.dumps({k:v['avg_ms'] for k,v in d['kernels'].items()}), json.dumps({k: v.get('avg_ms') for k, v in (d.get('decode') or {}).get('kernels', {}).items()}), (d.get('decode') or {}).get('ms_per_step'))"
 done
