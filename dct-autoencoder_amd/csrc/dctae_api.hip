@@ -1003,7 +1003,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
               (D[i].plan_h >= 0 && plans[D[i].plan_h].kind == 1 ? 2 : 0);
     // band layout: rows on k_rows512pk (Kw = 448) and columns on k_cols512b (Kh = 448)
     D[i].tband = ctx->cols512b && ctx->rows_kernel == 4 && cfg->max_patch_w == 32 && cfg->max_patch_h == 32 &&
-                 D[i].H == 512 && D[i].W == 512 && D[i].bs == 0 && D[i].plan_w >= 0 &&
+                 D[i].H == 512 && D[i].W == 512 && D[i].Kh == 448 && D[i].Kw == 448 && D[i].bs == 0 && D[i].plan_w >= 0 &&
                  plans[D[i].plan_w].spec == 1 && D[i].plan_h >= 0 && plans[D[i].plan_h].spec == 1;
     // packed encodes of band images: item-major token staging (stage_pos; the
     // staging is internal there, while dctae_spectrum_tokens hands it out in flat order)

@@ -36,24 +36,23 @@ namespace dctae {
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // Layout of the band-layout T' (float4 = 4 rows of one column kx; band4 = y / 4):
-//   0: [band4][448 kx][4]                 (a wave's store: 1 KB contiguous)
-//   1: [kx / 14][band4][14][4]            (strip-major: a column block reads 3.5 KB runs)
-//   2: [band4 / 4][448 kx][16]            (a row block's channel: 28 KB contiguous)
-//   3: [kx / 112][band4 / 4][112][16]     (7 KB granules on both sides)
+//   2 (default): [band4 / 4][448 kx][16]  -- band16: a row block's channel is one
+//       contiguous 28 KB piece (staged through LDS, 1 KB stores), a column
+//       block's 14 columns are 896-byte runs;
+//   0: [band4][448 kx][4]  -- direct 16-byte stores after a 4 x 4 cross-row
+//       transpose; the column block reads 224-byte runs 7 KB apart.
+// Measured (1024 x 512^2, same box): layout 0 rows 1.11 / cols 0.735 ms,
+// layout 2 rows 1.08-1.09 / cols 0.607 ms.  Layout 2 at
+// 207 VGPRs (2 waves / SIMD) still beats layout 0 at 156 (3 waves).
 #ifndef DCTAE_TLAYOUT
-#define DCTAE_TLAYOUT 0
+#define DCTAE_TLAYOUT 2
 #endif
+static_assert(DCTAE_TLAYOUT == 0 || DCTAE_TLAYOUT == 2, "T' layouts: 0 or 2");
 __device__ __forceinline__ int t4_index(int band4, int kx) {
 #if DCTAE_TLAYOUT == 0
   return band4 * 448 + kx;
-#elif DCTAE_TLAYOUT == 1
-  const int st = (kx * 4682) >> 16;   // kx / 14 for kx < 2048
-  return (st * 128 + band4) * 14 + kx - 14 * st;
-#elif DCTAE_TLAYOUT == 2
-  return ((band4 >> 2) * 448 + kx) * 4 + (band4 & 3);
 #else
-  const int sg = (kx * 586) >> 16;    // kx / 112 for kx < 783
-  return ((sg * 32 + (band4 >> 2)) * 112 + kx - 112 * sg) * 4 + (band4 & 3);
+  return ((band4 >> 2) * 448 + kx) * 4 + (band4 & 3);
 #endif
 }
 
@@ -276,8 +275,14 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
     }
 #if DCTAE_TLAYOUT == 2
     if (band && c > 0) __syncthreads();   // the previous channel's staged-output reads (aliased on xch)
-#endif
+    // lane indices made opaque per channel: the transpose addresses derived
+    // from them are rebuilt in each channel instead of being held across all three
+    int jo = j, so = s;
+    if (band) asm volatile("" : "+v"(jo), "+v"(so));
+    fft256_group(v, xr, jo, so, L.tw2);
+#else
     fft256_group(v, xr, j, s, L.tw2);
+#endif
     // ---- Makhoul post: k = s + 16 i, A = Z[k] = v[i], P = Z[M - k]
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(T + (int64_t)c * H * KW, 0, plane_bytes, 0x00020000);
 #if DCTAE_TLAYOUT == 2
@@ -299,6 +304,8 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
         const cf xx = makhoul_step(v, i, s, self0, self8, L.pc);
         oa[256 * i] = xx.x;
         if (i >= 5 || (i == 4 && s >= 1)) on[-256 * i] = xx.y;
+        // without it the 16 post-coefficient reads (64 VGPRs) are all hoisted up
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       if (self0) {
         const float4 cc = L.pc[M];
@@ -313,6 +320,7 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
 #pragma unroll
       for (int it = 0; it < 7; ++it)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, rd[64 * it]), rsrc, go, 1024 * it, 0);
+      __builtin_amdgcn_sched_barrier(0);   // keep the next channel's inputs from being built up here
     } else
 #endif
     if constexpr (band) {

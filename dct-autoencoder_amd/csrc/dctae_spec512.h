@@ -42,18 +42,39 @@ __device__ __forceinline__ void cols_thresholds(const ImgDesc& d, int c, int str
   }
 #endif
   if (THR) {
+    const int jlc = min(jl, KS - 1);   // lanes 14 / 15 hold row 13's thresholds (cols512b_epilogue)
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
       const int h = g16 + 16 * r;
-      if (h < d.qh && jl < KS) {
+      if (h < d.qh) {
         const float2* t2 = reinterpret_cast<const float2*>(
-            ep.thr + ((((int64_t)c * ep.maxph + h) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jl * KS);
+            ep.thr + ((((int64_t)c * ep.maxph + h) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jlc * KS);
 #pragma unroll
         for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
       }
     }
   }
   if (THR && sbias && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
+}
+
+// staging index of tile (h, strip) of channel c: flat (h, strip, c) or
+// item-major (c, strip, h) order (stage_pos, dctae_internal.h)
+__device__ __forceinline__ int64_t cols_tok(const ImgDesc& d, int c, int strip, int h, int C) {
+  return d.tok_off + ((d.tband & 2) ? (c * d.qw + strip) * d.qh + h : (h * d.qw + strip) * C + c);
+}
+
+// token outputs (raw DCT / PatchNorm) leave through LDS: tile h's 14 rows of
+// 14 are the 196 contiguous floats Xf[196 h ..], the token's staged layout, so
+// the whole block stores them as 16-byte pieces (49 per token) instead of 14
+// scattered 4-byte stores per lane
+__device__ __forceinline__ void cols_store_tokens(const ImgDesc& d, int c, int strip, const float* Xf, float* dst,
+                                                  int C) {
+  constexpr int KS = 14;
+  for (int e = opaque_tid(); e < d.qh * 49; e += 256) {
+    const int h = e / 49, q = e - h * 49;
+    reinterpret_cast<float4*>(dst + cols_tok(d, c, strip, h, C) * (KS * KS))[q] =
+        reinterpret_cast<const float4*>(Xf + KS * KS * h)[q];
+  }
 }
 
 // token epilogue of one (channel, tile column) item: X2 = the 448 x 14 kept
@@ -67,23 +88,9 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
   constexpr int KS = 14, EPR = 2;
   const int tid = opaque_tid();
   const int g16 = tid >> 4, jl = tid & 15;
-  // staging index of tile (h, strip) of channel c (flat or item-major, stage_pos)
-  const bool im = (d.tband & 2) != 0;
-  auto tok_of = [&](int h) -> int64_t {
-    return d.tok_off + (im ? (c * d.qw + strip) * d.qh + h : (h * d.qw + strip) * ep.C + c);
-  };
-  // token outputs (raw DCT / PatchNorm) leave through LDS: tile h's 14 rows
-  // of 14 are the 196 contiguous floats X[196 h ..], the token's staged
-  // layout, so the whole block stores them as 16-byte pieces (49 per token)
-  // instead of 14 scattered 4-byte stores per lane
+  auto tok_of = [&](int h) -> int64_t { return cols_tok(d, c, strip, h, ep.C); };
   float* Xf = reinterpret_cast<float*>(const_cast<f2v*>(X2));
-  auto store_tokens = [&](float* dst) {
-    for (int e = tid; e < d.qh * 49; e += 256) {
-      const int h = e / 49, q = e - h * 49;
-      const int64_t tok = tok_of(h);
-      reinterpret_cast<float4*>(dst + tok * (KS * KS))[q] = reinterpret_cast<const float4*>(Xf + KS * KS * h)[q];
-    }
-  };
+  auto store_tokens = [&](float* dst) { cols_store_tokens(d, c, strip, Xf, dst, ep.C); };
   if (THR) {
 #pragma unroll
     for (int r = 0; r < EPR; ++r) {
@@ -146,6 +153,77 @@ __device__ __forceinline__ void cols_epilogue(const ImgDesc& d, int c, int strip
       store_tokens(sk.norm);
     }
   }
+}
+
+// Threshold (codes-only) epilogue of k_cols512b: the same outputs as
+// cols_epilogue<true> for its images (qh = qw = 32, so tiles h = g16 and
+// g16 + 16 both exist) in about half the instructions:
+//  * |x| max as a NaN-propagating v_maximum3_f32 (abs modifiers, two elements
+//    per instruction; NaN scores as the reference's amax);
+//  * each code bit is a v_cmp_ge_f32 into an SGPR pair plus a v_addc_co_u32
+//    (code + code + carry): MSB first (lfq.py:187), two tile rows interleaved so
+//    every carry read is >= 3 instructions after its compare (the VALU-SGPR
+//    hazard) with no s_nop;
+//  * lanes 14 / 15 repeat row 13 (its values and thresholds, cols_thresholds)
+//    and store row 13's code and the row's score to the same addresses:
+//    no divergent branches;
+//  * stores through buffer descriptors on the item's first token: 32-bit lane
+//    offsets, no 64-bit address math.
+__device__ __forceinline__ void code_bits4(uint32_t& c0, uint32_t& c1, float& a0, float& a1, f2v x, f2v y,
+                                           float2 tx, float2 ty) {
+  uint64_t m0, m1, m2, m3;
+  asm("v_cmp_ge_f32_e64 %[m0], %[x0], %[t0]\n\t"
+      "v_cmp_ge_f32_e64 %[m1], %[x1], %[t1]\n\t"
+      "v_cmp_ge_f32_e64 %[m2], %[y0], %[u0]\n\t"
+      "v_cmp_ge_f32_e64 %[m3], %[y1], %[u1]\n\t"
+      "v_maximum3_f32 %[a0], |%[x0]|, |%[x1]|, %[a0]\n\t"
+      "v_maximum3_f32 %[a1], |%[y0]|, |%[y1]|, %[a1]\n\t"
+      "v_addc_co_u32_e64 %[c0], %[m0], %[c0], %[c0], %[m0]\n\t"
+      "v_addc_co_u32_e64 %[c0], %[m1], %[c0], %[c0], %[m1]\n\t"
+      "v_addc_co_u32_e64 %[c1], %[m2], %[c1], %[c1], %[m2]\n\t"
+      "v_addc_co_u32_e64 %[c1], %[m3], %[c1], %[c1], %[m3]"
+      : [c0] "+v"(c0), [c1] "+v"(c1), [a0] "+v"(a0), [a1] "+v"(a1), [m0] "=&s"(m0), [m1] "=&s"(m1),
+        [m2] "=&s"(m2), [m3] "=&s"(m3)
+      : [x0] "v"(x.x), [x1] "v"(x.y), [y0] "v"(y.x), [y1] "v"(y.y), [t0] "v"(tx.x), [t1] "v"(tx.y),
+        [u0] "v"(ty.x), [u1] "v"(ty.y));
+}
+
+__device__ __forceinline__ void cols512b_epilogue(const ImgDesc& d, int c, int strip, const f2v* X2,
+                                                  const float (&sb)[2], const float2 (&thr_r)[2][7],
+                                                  const EncParams& ep, const TokenSinks& sk) {
+  constexpr int KS = 14;
+  const int tid = opaque_tid();
+  const int g16 = tid >> 4, jl = min(tid & 15, KS - 1);
+  // token of tile h = tok0 + h * hs (cols_tok)
+  const bool im = (d.tband & 2) != 0;
+  const int64_t tok0 = d.tok_off + (im ? (int64_t)(c * d.qw + strip) * d.qh : (int64_t)strip * ep.C + c);
+  const uint32_t hs = im ? 1u : (uint32_t)(d.qw * ep.C);
+  const f2v* row0 = X2 + (KS * g16 + jl) * (KS / 2);   // tile g16, row jl
+  const f2v* row1 = row0 + 16 * KS * (KS / 2);          // tile g16 + 16
+  uint32_t code0 = 0, code1 = 0;
+  float am0 = 0.0f, am1 = 0.0f;
+#pragma unroll
+  for (int p = 0; p < KS / 2; ++p) code_bits4(code0, code1, am0, am1, row0[p], row1[p], thr_r[0][p], thr_r[1][p]);
+  // max over the 16-lane row (non-negative floats and +NaN: integer order)
+  uint32_t u0 = __float_as_uint(am0), u1 = __float_as_uint(am1);
+#define DCTAE_ROR_MAX(ctl)                                                        \
+  u0 = max(u0, (uint32_t)__builtin_amdgcn_mov_dpp((int)u0, ctl, 0xf, 0xf, false)); \
+  u1 = max(u1, (uint32_t)__builtin_amdgcn_mov_dpp((int)u1, ctl, 0xf, 0xf, false));
+  DCTAE_ROR_MAX(0x128) DCTAE_ROR_MAX(0x124) DCTAE_ROR_MAX(0x122) DCTAE_ROR_MAX(0x121)
+#undef DCTAE_ROR_MAX
+  const uint32_t span = 31 * hs + 1;   // tokens from tok0 to tile 31's
+  const uint32_t o0 = (uint32_t)g16 * hs, o1 = o0 + 16 * hs;
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(sk.scores + tok0, 0, (int)(span * 4), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(__fadd_rn(__fmul_rn(__uint_as_float(u0), ep.mw), sb[0])),
+                                        srs, o0 * 4, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(__fadd_rn(__fmul_rn(__uint_as_float(u1), ep.mw), sb[1])),
+                                        srs, o1 * 4, 0, 0);
+  if (sk.codes) {
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(sk.codes + tok0 * KS, 0, (int)(span * KS * 2), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)code0, crs, (o0 * KS + jl) * 2, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)code1, crs, (o1 * KS + jl) * 2, 0, 0);
+  }
+  if (sk.raw) cols_store_tokens(d, c, strip, reinterpret_cast<const float*>(X2), sk.raw, ep.C);
 }
 
 __device__ __forceinline__ constexpr int z7addr(int m) { return 16 * (m ^ ((m >> 3) & 1)); }
@@ -347,8 +425,7 @@ __device__ __forceinline__ void cols512b_load(int c, int strip, const float* __r
                                                       0x00020000);
   const int kx = 14 * strip + min(G, 13);
   const int o = t4_index(j, kx) * 16;                                 // band4 = 16 b + j
-  constexpr int bstep = (DCTAE_TLAYOUT == 0 ? 16 * KW : DCTAE_TLAYOUT == 1 ? 16 * 14
-                         : DCTAE_TLAYOUT == 2 ? 16 * KW : 16 * 112) * 16;   // t4_index(16, kx) - t4_index(0, kx)
+  constexpr int bstep = 16 * KW * 16;   // t4_index(16 b + j, kx) - t4_index(16 (b - 1) + j, kx), both layouts
 #if defined(DCTAE_PROFILING) && defined(DCTAE_C5B_ABL)
   if (DCTAE_C5B_ABL & 4) {   // profiling ablation: no T' loads (wrong outputs)
 #pragma unroll
@@ -406,7 +483,10 @@ __device__ __forceinline__ void cols512b_compute(const ImgDesc& d, int c, int st
 #if defined(DCTAE_PROFILING) && defined(DCTAE_C5B_ABL)
   if (DCTAE_C5B_ABL & 1) return;   // profiling ablation: no token epilogue (wrong outputs)
 #endif
-  cols_epilogue<THR>(d, c, strip, reinterpret_cast<const f2v*>(L.u.X), sb, thr_r, ep, sk);
+  if (THR)
+    cols512b_epilogue(d, c, strip, reinterpret_cast<const f2v*>(L.u.X), sb, thr_r, ep, sk);
+  else
+    cols_epilogue<false>(d, c, strip, reinterpret_cast<const f2v*>(L.u.X), sb, thr_r, ep, sk);
 }
 
 }  // namespace dctae

@@ -667,6 +667,36 @@ def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables):
         assert ok, ("fft vs gemm", dmax, scale)
 
 
+def test_fft_decode_duplicate_tokens_last_wins(fe, pn, lfq, ref_tables):
+    """Two tokens of one image at the same (channel, h, w): the reference's
+    revert_patching assigns tokens in packed order (FE:639-643), so the later
+    one wins.  FFT decode (item-major map by atomicMax + staged codes) against
+    the oracle's per-token loop on the same edited batch."""
+    x = torch.from_numpy(np.stack(rng.synth_images(83, [(512, 512)] * 2))).to(DEV)
+    ((dp, codes),) = fe.encode_batch(x, pn, lfq)
+    pos, chs, codes = dp.patch_positions.clone(), dp.patch_channels.clone(), codes.clone()
+    ids, kp = dp.batched_image_ids, dp.key_pad_mask
+    # image of row 0's first token: copy (c, h, w) of its slot j0 onto three later slots of the same image
+    img0 = int(ids[0, 0])
+    js = [j for j in range(ids.shape[1]) if int(ids[0, j]) == img0 and not bool(kp[0, j])]
+    j0, later = js[3], [js[100], js[1000], js[len(js) - 1]]
+    for n, j in enumerate(later):
+        pos[0, j] = pos[0, j0]
+        chs[0, j] = chs[0, j0]
+        codes[0, j] = (codes[0, j0] + 977 * (n + 1)) % (2 ** 14)   # distinguishable codes
+    dp.patch_positions, dp.patch_channels = pos, chs
+    imgs = fe.decode_batch(dp, codes, pn, lfq)
+    _ops().check_device_errors(x.device)
+    y = ref_cpu.lfq_indices_to_codes(codes.cpu(), ref_cpu.LFQConfig())
+    xin = ref_cpu.norm_inverse(ref_tables, y, chs.cpu(), pos.cpu()[..., 0], pos.cpu()[..., 1])
+    batch = ref_cpu.Batch(xin, kp.cpu(), None, ids.cpu(), chs.cpu(), pos.cpu(), dp.patch_sizes, dp.original_sizes)
+    refs = ref_cpu.postprocess(batch, CFG, per_token_loop=True)
+    for a, r in zip(imgs, refs):
+        scale = max(1.0, float(r.abs().max()))
+        ok, dmax = _rgb_close(a.cpu(), r, atol=1e-5 * scale, rtol=2e-5)
+        assert ok, (dmax, scale)
+
+
 def test_fft_decode_patches_roundtrip_512(fe):
     """postprocess (patch-space decode) of a 512^2 preprocess on the FFT path is
     the inverse of the kept-corner DCT: equal to the oracle's round trip."""
