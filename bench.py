@@ -191,7 +191,8 @@ def stats_fit_leg(pkg, fe, dev, rank, world, dist, steps, n_img=8, size=512):
         tdist.all_reduce(flag, op=tdist.ReduceOp.MIN)
         table_bytes = 3 * 32 * 32 * (14 * 14 + 1) * 4
         return {"workload": f"config 5 stats fit: PatchNorm running statistics of {n_img} x {size}x{size} images "
-                            f"per rank, 2 all_gathers over RCCL + local replay of the update chain",
+                            f"per rank, 2 all_gathers over {'RCCL' if tdist.get_backend() == 'nccl' else tdist.get_backend()} "
+                            f"+ local replay of the update chain",
                 "ranks": world, "ms_per_step": round(float(el.item()) / steps * 1e3, 4),
                 "gathered_bytes_per_rank_per_step": 2 * table_bytes * world,
                 "tables_bit_equal_to_sequential_fit": bool(flag.item()),

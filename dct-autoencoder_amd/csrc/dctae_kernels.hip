@@ -584,6 +584,7 @@ __device__ __forceinline__ void gather_tokens(const ImgDesc& d, const uint16_t* 
 // Tokens per image <= 512 x 6 = 3072 (max_patch 32 x 32, 3 channels).
 constexpr int kSortBS = 512, kSortIPT = 6;
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restrict__ imgs, EncParams ep,
                                                         TokenSinks st, PackSinks out) {
@@ -594,11 +595,18 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
   const int tid = threadIdx.x;
   const ImgDesc d = imgs[blockIdx.x];
   uint32_t keys[kSortIPT], vals[kSortIPT];
+  {
+    // all six score loads in flight at once (unconditional: past-the-end lanes
+    // read 0 through the descriptor's num_records)
+    const auto krs = __builtin_amdgcn_make_buffer_rsrc(st.scores + d.tok_off, 0, d.T * 4, 0x00020000);
 #pragma unroll
-  for (int i = 0; i < kSortIPT; ++i) {
-    const int idx = tid * kSortIPT + i;   // blocked: input order = index order (stability -> index asc)
-    keys[i] = idx < d.T ? float_key(st.scores[d.tok_off + stage_pos(d, idx)]) : 0u;
-    vals[i] = (uint32_t)idx;
+    for (int i = 0; i < kSortIPT; ++i) {
+      const int idx = tid * kSortIPT + i;   // blocked: input order = index order (stability -> index asc)
+      keys[i] = __builtin_amdgcn_raw_buffer_load_b32(krs, idx < d.T ? stage_pos(d, idx) * 4 : 0x7ffffff0, 0, 0);
+      vals[i] = (uint32_t)idx;
+    }
+#pragma unroll
+    for (int i = 0; i < kSortIPT; ++i) keys[i] = (int)vals[i] < d.T ? float_key(__uint_as_float(keys[i])) : 0u;
   }
   Sort().sort_desc_to_striped(keys, vals, tmp);
 #pragma unroll
@@ -629,18 +637,34 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
     if (out.scores) out.scores[o] = st.scores[d.tok_off + spos[t]];
   }
   if (out.codes && ep.ncb == 14) {
-    // two codes per lane: one u32 of the u16 staging -> one 16-byte int64 pair (coalesced)
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(st.codes);
-    longlong2* dst = reinterpret_cast<longlong2*>(out.codes);
+    // two codes per lane: one u32 of the u16 staging -> one 16-byte int64 pair
+    // (coalesced).  kCU gathers in flight per lane before any is used (one
+    // gather + wait per iteration exposed the load latency 42 times per lane),
+    // buffer descriptors on the image's staging / packed span (32-bit offsets;
+    // past-the-end lanes clipped by num_records)
+    constexpr int kCU = 14;
     const uint32_t pos2 = ep.code_pos | (ep.code_pos << 16), neg2 = ep.code_neg | (ep.code_neg << 16);
-    for (int e = tid; e < d.k * 7; e += kSortBS) {
-      const int t = e / 7, q = e - t * 7;
-      const uint32_t v = (uint32_t)lfq_index_bits(src[(d.tok_off + spos[t]) * 7 + q], pos2, neg2);
-      // write-once outputs: nontemporal stores (their lines leave the L2 /
-      // Infinity Cache early instead of being written back under the next
-      // step's row kernel: sort 0.146 -> 0.143 ms, next rows 1.13 -> 1.11 ms)
-      __builtin_nontemporal_store((v2i64){(long long)(v & 0xFFFFu), (long long)(v >> 16)},
-                                  reinterpret_cast<v2i64*>(dst + (base + t) * 7 + q));
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(st.codes + d.tok_off * 14, 0, d.T * 28, 0x00020000);
+    const auto drs = __builtin_amdgcn_make_buffer_rsrc(out.codes + base * 14, 0, d.k * 112, 0x00020000);
+    const int n = d.k * 7;
+    for (int e0 = tid; e0 < n; e0 += kSortBS * kCU) {
+      uint32_t v[kCU];
+#pragma unroll
+      for (int u = 0; u < kCU; ++u) {
+        const int e = e0 + kSortBS * u;
+        const int t = min(e / 7, d.k - 1), q = e - (e / 7) * 7;
+        v[u] = __builtin_amdgcn_raw_buffer_load_b32(srs, (spos[t] * 7 + q) * 4, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kCU; ++u) {
+        const int e = e0 + kSortBS * u;
+        const uint32_t c2 = (uint32_t)lfq_index_bits(v[u], pos2, neg2);
+        // write-once outputs: nontemporal stores (their lines leave the L2 /
+        // Infinity Cache early instead of being written back under the next
+        // step's row kernel: sort 0.146 -> 0.143 ms, next rows 1.13 -> 1.11 ms)
+        __builtin_amdgcn_raw_buffer_store_b128((v4u32){c2 & 0xFFFFu, 0u, c2 >> 16, 0u}, drs,
+                                               e < n ? e * 16 : 0x7ffffff0, 0, 2);
+      }
     }
   } else if (out.codes) {
     const int ncb = ep.ncb;
