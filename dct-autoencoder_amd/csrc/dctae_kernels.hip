@@ -585,6 +585,7 @@ __device__ __forceinline__ void gather_tokens(const ImgDesc& d, const uint16_t* 
 constexpr int kSortBS = 512, kSortIPT = 6;
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
 typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
+typedef unsigned v2u32s __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restrict__ imgs, EncParams ep,
                                                         TokenSinks st, PackSinks out) {
@@ -667,11 +668,25 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
       }
     }
   } else if (out.codes) {
-    const int ncb = ep.ncb;
-    for (int e = tid; e < d.k * ncb; e += kSortBS) {
-      const int t = e / ncb, q = e - t * ncb;
-      out.codes[(base + t) * ncb + q] =
-          (int64_t)lfq_index_bits(st.codes[(d.tok_off + spos[t]) * ncb + q], ep.code_pos, ep.code_neg);
+    // any ncb: one u16 -> one int64 per lane, kCU gathers in flight (as above)
+    constexpr int kCU = 16;
+    const int ncb = ep.ncb, n = d.k * ncb;
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(st.codes + d.tok_off * ncb, 0, d.T * ncb * 2, 0x00020000);
+    const auto drs = __builtin_amdgcn_make_buffer_rsrc(out.codes + base * ncb, 0, n * 8, 0x00020000);
+    for (int e0 = tid; e0 < n; e0 += kSortBS * kCU) {
+      uint32_t v[kCU];
+#pragma unroll
+      for (int u = 0; u < kCU; ++u) {
+        const int e = e0 + kSortBS * u;
+        const int t = min(e / ncb, d.k - 1), q = e - (e / ncb) * ncb;
+        v[u] = __builtin_amdgcn_raw_buffer_load_b16(srs, (spos[t] * ncb + q) * 2, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kCU; ++u) {
+        const int e = e0 + kSortBS * u;
+        const uint32_t cv = (uint32_t)lfq_index_bits(v[u], ep.code_pos, ep.code_neg);
+        __builtin_amdgcn_raw_buffer_store_b64((v2u32s){cv, 0u}, drs, e < n ? e * 8 : 0x7ffffff0, 0, 2);
+      }
     }
   }
   if (out.patches || out.raw) gather_tokens(d, spos, base, PP, st, out, tid, kSortBS);
