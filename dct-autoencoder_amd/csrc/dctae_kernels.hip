@@ -581,12 +581,13 @@ __device__ __forceinline__ void gather_tokens(const ImgDesc& d, const uint16_t* 
 // Same contract with rocPRIM's block radix sort (LSD, stable): 32-bit score
 // keys sorted descending, flat indices as values; stability keeps equal
 // scores in ascending index order = the (score desc, index asc) order above.
-// Tokens per image <= 512 x 6 = 3072 (max_patch 32 x 32, 3 channels).
-constexpr int kSortBS = 512, kSortIPT = 6;
+// Tokens per image <= 512 x 6 = 3072 (max_patch 32 x 32, 3 channels); the
+// 256 x 3 instance covers 224^2 images (768 tokens).
 typedef long long v2i64 __attribute__((ext_vector_type(2)));
 typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
 typedef unsigned v2u32s __attribute__((ext_vector_type(2)));
 
+template <int kSortBS, int kSortIPT>
 __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restrict__ imgs, EncParams ep,
                                                         TokenSinks st, PackSinks out) {
   using Sort = rocprim::block_radix_sort<uint32_t, kSortBS, kSortIPT, uint32_t>;
@@ -694,8 +695,12 @@ __global__ __launch_bounds__(kSortBS) void k_sort_pack2(const ImgDesc* __restric
 
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
                       const PackSinks& out, hipStream_t s, int kernel, int max_T) {
-  if (kernel == 2 && max_T <= kSortBS * kSortIPT)
-    hipLaunchKernelGGL(k_sort_pack2, dim3(n_img), dim3(kSortBS), 0, s, imgs, ep, st, out);
+  // 224^2 images (768 tokens): a quarter-size block (a full one sorted 3072
+  // padded keys per image)
+  if (kernel == 2 && max_T <= 256 * 3)
+    hipLaunchKernelGGL((k_sort_pack2<256, 3>), dim3(n_img), dim3(256), 0, s, imgs, ep, st, out);
+  else if (kernel == 2 && max_T <= 512 * 6)
+    hipLaunchKernelGGL((k_sort_pack2<512, 6>), dim3(n_img), dim3(512), 0, s, imgs, ep, st, out);
   else
     hipLaunchKernelGGL(k_sort_pack, dim3(n_img), dim3(1024), (size_t)np2 * 8, s, imgs, np2, ep, st, out);
 }
