@@ -171,6 +171,35 @@ __device__ __forceinline__ cf makhoul_step(const cf (&v)[16], int i, int s, bool
   return makhoul_pair(v[i], P, (cf){cc.x, cc.y}, (cf){cc.z, cc.w});
 }
 
+// two independent Makhoul pairs with their VOP3P chains interleaved: every
+// dependent op is one instruction behind its producer (the separate chains of
+// makhoul_pair need an s_nop between their dependent ops)
+__device__ __forceinline__ void makhoul_pair2(cf A0, cf P0, float4 c0, cf A1, cf P1, float4 c1, cf& t0, cf& t1) {
+  const cf c12a = (cf){c0.x, c0.y}, c34a = (cf){c0.z, c0.w}, c12b = (cf){c1.x, c1.y}, c34b = (cf){c1.z, c1.w};
+  asm("v_pk_mul_f32 %0, %2, %3 op_sel_hi:[1,0] neg_hi:[1,0]\n\t"
+      "v_pk_mul_f32 %1, %6, %7 op_sel_hi:[1,0] neg_hi:[1,0]\n\t"
+      "v_pk_fma_f32 %0, %4, %3, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+      "v_pk_fma_f32 %1, %8, %7, %1 op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+      "v_pk_fma_f32 %0, %2, %5, %0 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %1, %6, %9, %1 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %0, %4, %5, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]\n\t"
+      "v_pk_fma_f32 %1, %8, %9, %1 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+      : "=&v"(t0), "=&v"(t1)
+      : "v"(A0), "v"(c12a), "v"(P0), "v"(c34a), "v"(A1), "v"(c12b), "v"(P1), "v"(c34b));
+}
+
+// steps i and i + 1 of the Makhoul post with their coefficients c0 / c1
+// already loaded (the caller keeps the next pair's LDS reads in flight)
+__device__ __forceinline__ void makhoul_step2(const cf (&v)[16], int i, bool self0, bool self8, float4 c0, float4 c1,
+                                              cf& x0, cf& x1) {
+  const cf m0 = (cf){mirror16(v[15 - i].x), mirror16(v[15 - i].y)};
+  const cf m1 = (cf){mirror16(v[14 - i].x), mirror16(v[14 - i].y)};
+  const cf o0 = self0 ? v[(16 - i) & 15] : v[15 - i];
+  const cf o1 = self0 ? v[15 - i] : v[14 - i];
+  const cf P0 = (self0 || self8) ? o0 : m0, P1 = (self0 || self8) ? o1 : m1;
+  makhoul_pair2(v[i], P0, c0, v[i + 1], P1, c1, x0, x1);
+}
+
 // 4 x 4 transpose across the four 16-lane rows of a wave: on return r[k] at
 // row g holds the input r[g] of row k.  v_permlane32_swap exchanges rows 2, 3
 // of its first operand with rows 0, 1 of its second; v_permlane16_swap the odd
@@ -299,13 +328,23 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
       float* oa = ob + s * 16 + 4 * (wv ^ ((s >> 1) & 3)) + sg;              // + 256 i
       float* on = ob + (N - s) * 16 + 4 * (wv ^ (((N - s) >> 1) & 3)) + sg;  // - 256 i
       __syncthreads();   // every group's pass-2 reads of xch
+      // steps in pairs, the next pair's coefficients read while this one computes
+      float4 cn0 = L.pc[s], cn1 = L.pc[s + 16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const cf xx = makhoul_step(v, i, s, self0, self8, L.pc);
-        oa[256 * i] = xx.x;
-        if (i >= 5 || (i == 4 && s >= 1)) on[-256 * i] = xx.y;
-        // without it the 16 post-coefficient reads (64 VGPRs) are all hoisted up
-        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < 16; i += 2) {
+        const float4 c0 = cn0, c1 = cn1;
+        if (i + 2 < 16) {
+          cn0 = L.pc[s + 16 * (i + 2)];
+          cn1 = L.pc[s + 16 * (i + 3)];
+        }
+        cf x0, x1;
+        makhoul_step2(v, i, self0, self8, c0, c1, x0, x1);
+        oa[256 * i] = x0.x;
+        oa[256 * (i + 1)] = x1.x;
+        if (i >= 5 || (i == 4 && s >= 1)) on[-256 * i] = x0.y;
+        if (i + 1 >= 5) on[-256 * (i + 1)] = x1.y;
+        // without it the post-coefficient reads of later pairs are all hoisted up
+        if ((i & 3) == 2) __builtin_amdgcn_sched_barrier(0);
       }
       if (self0) {
         const float4 cc = L.pc[M];

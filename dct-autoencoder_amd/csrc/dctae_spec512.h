@@ -471,12 +471,22 @@ __device__ __forceinline__ void cols512b_compute(const ImgDesc& d, int c, int st
 #endif
   float* xa = L.u.X + s * KS + colc;                 // X[s + 16 i] at + 224 i
   float* xb = L.u.X + (N - s) * KS + colc;           // X[N - s - 16 i] at - 224 i
+  // steps in pairs, the next pair's coefficients read while this one computes
+  float4 cn0 = L.pc[s], cn1 = L.pc[s + 16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const cf xx = makhoul_step(v, i, s, self0, self8, L.pc);
-    xa[224 * i] = xx.x;
+  for (int i = 0; i < 16; i += 2) {
+    const float4 c0 = cn0, c1 = cn1;
+    if (i + 2 < 16) {
+      cn0 = L.pc[s + 16 * (i + 2)];
+      cn1 = L.pc[s + 16 * (i + 3)];
+    }
+    cf x0, x1;
+    makhoul_step2(v, i, self0, self8, c0, c1, x0, x1);
+    xa[224 * i] = x0.x;
+    xa[224 * (i + 1)] = x1.x;
     // X[N - k] kept for k > 64; i = 4, s = 0 (k = 64) lands on the spare row 448
-    if (i >= 4) xb[-224 * i] = xx.y;
+    if (i >= 4) xb[-224 * i] = x0.y;
+    if (i + 1 >= 4) xb[-224 * (i + 1)] = x1.y;
   }
   if (self0) L.u.X[M * KS + colc] = (pcM.x + pcM.y) * v[0].x + (pcM.w - pcM.z) * v[0].y;
   __syncthreads();
