@@ -55,6 +55,10 @@ struct dctae_ctx {
   uint64_t plan_last_id = 0, plan_counter = 0;
   hipEvent_t plan_evt = nullptr;
   hipEvent_t done_evt = nullptr;
+  // sort_overlap: the first half's sort / pack on a side stream beside the
+  // second half's column kernel (created on first use)
+  hipStream_t side = nullptr;
+  hipEvent_t side_in = nullptr, side_out = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_done = false;
   int* err_dev = nullptr;
@@ -83,6 +87,7 @@ struct dctae_ctx {
   // layout T'[c][y/4][kx][y%4] and the columns run k_cols512b (16-byte loads,
   // DESIGN.md section 4); 0 = row-major T and k_fft_cols7
   int cols512b = 1;
+  int sort_overlap = 0;
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
@@ -810,6 +815,11 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   for (auto e : ctx->evt_pool) hipEventDestroy(e);
   hipEventDestroy(ctx->plan_evt);
   hipEventDestroy(ctx->done_evt);
+  if (ctx->side) {
+    hipStreamDestroy(ctx->side);
+    hipEventDestroy(ctx->side_in);
+    hipEventDestroy(ctx->side_out);
+  }
   delete ctx;
   return 0;
 }
@@ -866,6 +876,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
 #endif
   else if (k == "rows_kernel" && (value == 2 || value == 4)) ctx->rows_kernel = (int)value;
   else if (k == "cols512b") ctx->cols512b = value != 0;
+  else if (k == "sort_overlap") ctx->sort_overlap = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
@@ -1455,9 +1466,52 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                              v == 1 && j.n_pc ? (const int*)(pd + j.pc_off) : nullptr, v == 1 ? j.n_pc : 0, j.pc_qw);
       }
   };
+  // the pack's parameters (the projection kernel stages raw sign bits: the pack maps them, lfq_index_bits)
+  EncParams eps = ep;
+  if (proj_w) {
+    eps.ncb = lfq->num_codebooks;
+    eps.cb_dim = lfq->codebook_dim;
+    uint64_t pos, neg;
+    lfq_index_masks(lfq->codebook_scale, lfq->codebook_dim, &pos, &neg);
+    eps.code_pos = (uint32_t)pos;
+    eps.code_neg = (uint32_t)neg;
+  }
+  const ImgDesc* all_d = (const ImgDesc*)(pd + E.all_desc_off);
+  // sort_overlap: one job of band images only -> columns in two halves, the
+  // first half's sort / pack on the side stream while the second half's
+  // columns run (the sort is latency-bound, the column kernel issue-bound)
+  int sorted0 = 0;   // images [0, sorted0) packed on the side stream
+  const bool split = full && !proj_w && ctx->sort_overlap && E.jobs.size() == 1 && E.n_img >= 64 &&
+                     E.jobs[0].n_pb == E.n_img && E.jobs[0].i0 == 0;
+  if (split && !ctx->side) {
+    if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->side_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->side_out, hipEventDisableTiming) != hipSuccess)
+      return fail(ctx, DCTAE_EHIP, "side stream allocation failed");
+  }
   for (const ChunkJob& j : E.jobs) {
     do_rows(j, s);
-    do_cols(j, s);
+    if (!split) {
+      do_cols(j, s);
+      continue;
+    }
+    const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
+    const int* list = (const int*)(pd + j.pb_off);
+    const int h = j.n_pb / 2;
+    {
+      Timer t(ctx, s, "fft_cols");
+      launch_cols512b(dd, list, h, ctx->ws, ctx->fft_tab + j.tw_off_c[1], ctx->fft_tab + j.post_off_c[1], epj, skc, s);
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->side_in, s));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+    launch_sort_pack(all_d, h, next_pow2(E.max_T), eps, sk, ps, ctx->side, ctx->sort_kernel, E.max_T);
+    HIPCHK(ctx, hipEventRecord(ctx->side_out, ctx->side));
+    {
+      Timer t(ctx, s, "fft_cols");
+      launch_cols512b(dd, list + h, j.n_pb - h, ctx->ws, ctx->fft_tab + j.tw_off_c[1], ctx->fft_tab + j.post_off_c[1],
+                      epj, skc, s);
+    }
+    sorted0 = h;
   }
   if (proj_w && E.n_tok > 0) {
     Timer t(ctx, s, "lfq_project_in");
@@ -1465,20 +1519,12 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     launch_lfq_project_in16(sk.norm, E.n_tok, PP, proj_w, proj_b, lfq->codebook_dim, lfq->num_codebooks, sk.codes,
                             ctx->proj_ws, s);
   }
-  if (full && E.n_img > 0) {
+  if (full && E.n_img > sorted0) {
     Timer t(ctx, s, "sort_pack");
-    EncParams eps = ep;
-    if (proj_w) {   // the projection kernel staged raw sign bits: the pack maps them (lfq_index_bits)
-      eps.ncb = lfq->num_codebooks;
-      eps.cb_dim = lfq->codebook_dim;
-      uint64_t pos, neg;
-      lfq_index_masks(lfq->codebook_scale, lfq->codebook_dim, &pos, &neg);
-      eps.code_pos = (uint32_t)pos;
-      eps.code_neg = (uint32_t)neg;
-    }
-    launch_sort_pack((const ImgDesc*)(pd + E.all_desc_off), E.n_img, next_pow2(E.max_T), eps, sk, ps, s,
-                     ctx->sort_kernel, E.max_T);
+    launch_sort_pack(all_d + sorted0, E.n_img - sorted0, next_pow2(E.max_T), eps, sk, ps, s, ctx->sort_kernel,
+                     E.max_T);
   }
+  if (sorted0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->side_out, 0));   // every output complete on the caller's stream
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
   return 0;

@@ -192,12 +192,31 @@ __device__ __forceinline__ void makhoul_pair2(cf A0, cf P0, float4 c0, cf A1, cf
 // already loaded (the caller keeps the next pair's LDS reads in flight)
 __device__ __forceinline__ void makhoul_step2(const cf (&v)[16], int i, bool self0, bool self8, float4 c0, float4 c1,
                                               cf& x0, cf& x1) {
-  const cf m0 = (cf){mirror16(v[15 - i].x), mirror16(v[15 - i].y)};
-  const cf m1 = (cf){mirror16(v[14 - i].x), mirror16(v[14 - i].y)};
-  const cf o0 = self0 ? v[(16 - i) & 15] : v[15 - i];
-  const cf o1 = self0 ? v[15 - i] : v[14 - i];
-  const cf P0 = (self0 || self8) ? o0 : m0, P1 = (self0 || self8) ? o1 : m1;
-  makhoul_pair2(v[i], P0, c0, v[i + 1], P1, c1, x0, x1);
+  // partner P = the mirror lane's v[15 - i] (lanes 1 .. 14) or the lane's own
+  // value (lane 0: v[(16 - i) & 15], lane 15: v[15 - i]) -- self0 / self8 are
+  // lanes 0 / 15 of every 16-lane row by construction, so both selects run on
+  // constant lane masks in VCC: the own value by a v_cndmask_b32, then P by a
+  // v_cndmask_b32 whose first source is read through the row_mirror DPP
+  (void)self0;
+  (void)self8;
+  float p0x, p0y, p1x, p1y, q0x, q0y, q1x, q1y;
+  asm("s_mov_b32 vcc_lo, 0x00010001\n\t"
+      "s_mov_b32 vcc_hi, 0x00010001\n\t"
+      "v_cndmask_b32 %4, %8, %12, vcc\n\t"
+      "v_cndmask_b32 %5, %9, %13, vcc\n\t"
+      "v_cndmask_b32 %6, %10, %8, vcc\n\t"
+      "v_cndmask_b32 %7, %11, %9, vcc\n\t"
+      "s_mov_b32 vcc_lo, 0x80018001\n\t"
+      "s_mov_b32 vcc_hi, 0x80018001\n\t"
+      "v_cndmask_b32_dpp %0, %8, %4, vcc row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %1, %9, %5, vcc row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %2, %10, %6, vcc row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_dpp %3, %11, %7, vcc row_mirror row_mask:0xf bank_mask:0xf"
+      : "=&v"(p0x), "=&v"(p0y), "=&v"(p1x), "=&v"(p1y), "=&v"(q0x), "=&v"(q0y), "=&v"(q1x), "=&v"(q1y)
+      : "v"(v[15 - i].x), "v"(v[15 - i].y), "v"(v[14 - i].x), "v"(v[14 - i].y), "v"(v[(16 - i) & 15].x),
+        "v"(v[(16 - i) & 15].y)
+      : "vcc");
+  makhoul_pair2(v[i], (cf){p0x, p0y}, c0, v[i + 1], (cf){p1x, p1y}, c1, x0, x1);
 }
 
 // 4 x 4 transpose across the four 16-lane rows of a wave: on return r[k] at

@@ -667,6 +667,24 @@ def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables):
         assert ok, ("fft vs gemm", dmax, scale)
 
 
+def test_sort_overlap_bit_identical(fe, pn, lfq):
+    """Option sort_overlap (the columns of a band-image batch in two halves,
+    the first half's sort / pack on a side stream beside the second half's
+    column kernel): every packed output equal to the one-stream encode."""
+    ops = _ops()
+    x = ops.synth_images(96, 512, 512, seed=77, device=torch.device(DEV))
+    ((dp0, c0),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_option("sort_overlap", 1)
+    try:
+        ((dp1, c1),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    finally:
+        ops.set_option("sort_overlap", 0)
+    torch.cuda.synchronize()
+    assert torch.equal(c0, c1)
+    for f in ("patches", "key_pad_mask", "batched_image_ids", "patch_channels", "patch_positions"):
+        assert torch.equal(getattr(dp0, f), getattr(dp1, f)), f
+
+
 def test_fft_decode_duplicate_tokens_last_wins(fe, pn, lfq, ref_tables):
     """Two tokens of one image at the same (channel, h, w): the reference's
     revert_patching assigns tokens in packed order (FE:639-643), so the later
