@@ -342,7 +342,11 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * compile-time plan kernel k_fft_rows2, which serves max_patch_w < 32),
  * "cols512b" (1, default: 512 x 512 images at max_patch 32 x 32 pass the
  * row-pass output in the band16 layout T'[c][y/16][kx][16] from k_rows512pk
- * to k_cols512b; 0: row-major T and k_fft_cols7),
+ * to k_cols512b; 0: row-major T and k_fft_cols7), "sort_overlap" (0,
+ * default / 1: a batch of >= 64 such images runs its column pass in two
+ * halves and the first half's sort / pack on a context-owned side stream
+ * beside the second half; the caller's stream waits for it, outputs
+ * bit-identical),
  * "sort_kernel" (2, default: rocPRIM radix for <= 3072 tokens per image; 1:
  * the bitonic kernel that serves larger images), "fft_decode" (0/1),
  * "xcd_order" (0/1), "dec_rows_kernel" (3 / 2), "gemm_x3" (1, default:
