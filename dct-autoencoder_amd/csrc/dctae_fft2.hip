@@ -40,7 +40,11 @@ __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const 
 #ifndef DCTAE_RPW224
 #define DCTAE_RPW224 1   // 224-wide rows: one row per wave (0.074 vs 0.081 ms at 4 rows per wave, config 2)
 #endif
+#ifndef DCTAE_ROWPF224
+#define DCTAE_ROWPF224 0
+#endif
   constexpr int RPW = N == 224 ? DCTAE_RPW224 : 4;   // rows per wave (block = 4 RPW rows)
+  constexpr bool ROWPF = N == 224 && DCTAE_ROWPF224 && RPW > 1;   // next row's pixels prefetched
   static_assert(R1 * R2 == M, "two-pass plan");
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
@@ -88,17 +92,24 @@ __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const 
     }
   };
   int y = y_first + wave;
+  if (ROWPF) fetch(y);
 #pragma unroll 1
   for (int rr = 0; rr < RPW; ++rr, y += 4) {
     if (y >= H) break;
-    fetch(y);
+    // with ROWPF this row's pixels arrived with the previous iteration and the
+    // next row's loads are in flight during this row's transform
+    if (!ROWPF) fetch(y);
+    float cr[PX], cg[PX], cb[PX];
+#pragma unroll
+    for (int i = 0; i < PX; ++i) cr[i] = pr[i], cg[i] = pg[i], cb[i] = pb[i];
+    if (ROWPF && rr + 1 < RPW) fetch(y + 4);
     // ---- IPT (util.py:70-82) + Makhoul reorder into LDS
 #pragma unroll
     for (int i = 0; i < PX; ++i) {
       if (lane + 64 * i < N) {
-        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, pr[i], pg[i], pb[i]), gam);
-        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, pr[i], pg[i], pb[i]), gam);
-        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, pr[i], pg[i], pb[i]), gam);
+        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, cr[i], cg[i], cb[i]), gam);
+        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, cr[i], cg[i], cb[i]), gam);
+        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, cr[i], cg[i], cb[i]), gam);
         zf0[zo[i]] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
         zf1[zo[i]] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
         zf2[zo[i]] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
@@ -191,13 +202,32 @@ struct ColsLds {
   float z[ZROWS * KSP];
 };
 
+typedef float c4f2 __attribute__((ext_vector_type(2)));
+
+// the T slice of column item (d, c, strip): thread (y0 = t / 7, p = t % 7)
+// holds float2 p of rows y0 + 32 k (threads t < 32 * KS / 2)
+template <int N, int KS>
+__device__ __forceinline__ void cols4_fetch(const ImgDesc& d, int c, int strip, const float* __restrict__ T,
+                                            c4f2 (&tv)[N / 32]) {
+  const int tid = opaque_tid();
+  if (tid < 32 * (KS / 2)) {
+    const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
+    const c4f2* src = reinterpret_cast<const c4f2*>(T + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
+    const int64_t rstep = (int64_t)16 * d.Kw;   // 32 rows, in float2
+#pragma unroll
+    for (int k = 0; k < N / 32; ++k) tv[k] = src[k * rstep];
+  }
+}
+
 // one column item: (image d, channel c, tile column strip); T = the image's
 // row-pass output (channel 0, row 0).  Caller: post_s / tw_s loaded, a block
-// barrier since the previous use of zs.
-template <int N, int R2, int KS, bool THR>
+// barrier since the previous use of zs and sbias.  PRE: the item's T slice is
+// already in `pre` (cols4_fetch, issued during the previous item).
+template <int N, int R2, int KS, bool THR, bool PRE = false>
 __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, const float* __restrict__ T, float* zs,
                                            const float2* post_s, const float2* tw_s, float* sbias,
-                                           const EncParams& ep, const TokenSinks& sk) {
+                                           const EncParams& ep, const TokenSinks& sk,
+                                           const c4f2* pre = nullptr) {
 #pragma clang fp contract(fast)
   constexpr int R1 = 16;
   constexpr int M = N / 2;
@@ -228,16 +258,17 @@ __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, c
   if (THR) load_thr();
   if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
   // ---- T slice -> LDS, natural row order
+  c4f2 tv[N / 32];
+  if (PRE) {
+#pragma unroll
+    for (int k = 0; k < N / 32; ++k) tv[k] = pre[k];
+  } else {
+    cols4_fetch<N, KS>(d, c, strip, T, tv);
+  }
   if (tid < 32 * (KS / 2)) {
     // row-major: thread (y0 = t / 7, p = t % 7) copies float2 p of rows y0 + 32k
     const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    const f2v* src = reinterpret_cast<const f2v*>(T + ((int64_t)c * d.H + y0) * d.Kw + strip * KS) + p;
-    const int64_t rstep = (int64_t)16 * d.Kw;   // 32 rows, in float2
     float* dst = zs + y0 * KSP + 2 * p;
-    f2v tv[N / 32];
-#pragma unroll
-    for (int k = 0; k < N / 32; ++k) tv[k] = src[k * rstep];
 #pragma unroll
     for (int k = 0; k < N / 32; ++k) {
       dst[32 * KSP * k] = tv[k].x;
@@ -535,10 +566,13 @@ int cols7_grid(int n_list, int qw, int ipb) {
   return 8 * per_x * ((n_list + ipb - 1) / ipb);
 }
 
-template <int N, int R2, int KS, bool THR>
+// IPB column items per block (items IPB b .. IPB b + IPB - 1 of `blocks`);
+// IPB > 1: the next item's T slice loads during the current item's transform
+template <int N, int R2, int KS, bool THR, int IPB>
 __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
-                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
-                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+                                                   int n_items, const float* __restrict__ ws,
+                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                   EncParams ep, TokenSinks sk) {
   constexpr int M = N / 2;
   __shared__ ColsLds<N> L;
   __shared__ float2 post_s[2 * (M + 1)];
@@ -546,9 +580,36 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   __shared__ float sbias[32];   // -(h + strip) / ci[c] per tile row h (fp32 division, FE:411-416)
   for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
   for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
-  const int4 jb = blocks[blockIdx.x];
-  const ImgDesc d = imgs[jb.x];
-  cols4_item<N, R2, KS, THR>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk);
+  const int i0 = blockIdx.x * IPB;
+  if (IPB == 1) {
+    const int4 jb = blocks[i0];
+    const ImgDesc d = imgs[jb.x];
+    cols4_item<N, R2, KS, THR>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk);
+    return;
+  }
+  c4f2 nv[N / 32];
+  {
+    const int4 jb = blocks[i0];
+    const ImgDesc d = imgs[jb.x];
+    cols4_fetch<N, KS>(d, jb.y, jb.z, ws + d.ws_t, nv);
+  }
+#pragma unroll 1
+  for (int u = 0; u < IPB; ++u) {
+    const int i = i0 + u;
+    if (i >= n_items) break;
+    c4f2 cv[N / 32];
+#pragma unroll
+    for (int k = 0; k < N / 32; ++k) cv[k] = nv[k];
+    const int4 jb = blocks[i];
+    const ImgDesc d = imgs[jb.x];
+    if (u + 1 < IPB && i + 1 < n_items) {
+      const int4 jn = blocks[i + 1];
+      const ImgDesc dn = imgs[jn.x];
+      cols4_fetch<N, KS>(dn, jn.y, jn.z, ws + dn.ws_t, nv);
+    }
+    if (u > 0) __syncthreads();   // the previous item's epilogue is done with zs / sbias
+    cols4_item<N, R2, KS, THR, true>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk, cv);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -596,12 +657,16 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
                          ws, tw, post, ep, sk);
     return;
   }
-#define DCTAE_COLS4(NN, RR, T)                                                                                  \
-  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk)
-  if (spec == 1 && thr) DCTAE_COLS4(512, 16, true);
-  else if (spec == 1) DCTAE_COLS4(512, 16, false);
-  else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true);
-  else if (spec == 2) DCTAE_COLS4(224, 7, false);
+#ifndef DCTAE_C4_IPB224
+#define DCTAE_C4_IPB224 1
+#endif
+#define DCTAE_COLS4(NN, RR, T, IPB)                                                                       \
+  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T, IPB>), dim3((n_blocks + IPB - 1) / IPB), dim3(256), 0, s, \
+                     imgs, blocks, n_blocks, ws, tw, post, ep, sk)
+  if (spec == 1 && thr) DCTAE_COLS4(512, 16, true, 1);
+  else if (spec == 1) DCTAE_COLS4(512, 16, false, 1);
+  else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true, DCTAE_C4_IPB224);
+  else if (spec == 2) DCTAE_COLS4(224, 7, false, DCTAE_C4_IPB224);
 #undef DCTAE_COLS4
 }
 

@@ -2,7 +2,7 @@
 # Iteration: parity tests selected by TESTS (pytest -k), then a same-box A/B of
 # the encode bench over option sets ("opt=v opt=v" per argument; a leading
 # "lib=<path>" selects another libdctae.so build).  DEC=1 adds the config-3
-# decode leg.  Each GPU step time-limited; stop at the first failure.
+# decode leg; CFG2=1 times config 2 only (tools/cfg2_try.py).  Each GPU step time-limited; stop at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -19,6 +19,12 @@ for opts in "$@"; do
   for o in $opts; do
     case $o in lib=*) export DCTAE_LIBRARY="${o#lib=}";; *) args="$args --opt $o";; esac
   done
+  if [ -n "${CFG2:-}" ]; then   # config 2 only (tools/cfg2_try.py)
+    timeout -k 10 200 python tools/cfg2_try.py $args > gpurun_out/try_cfg2.log 2>&1
+    rc=$?; echo "=== cfg2 [$opts] rc=$rc"; tail -1 gpurun_out/try_cfg2.log
+    [ $rc -ne 0 ] && exit $rc
+    continue
+  fi
   dec="--no-decode"; [ -n "${DEC:-}" ] && dec=""
   timeout -k 10 300 python bench.py --steps ${STEPS:-30} --warmup 3 --no-cpu-baseline $dec --no-stats \
       --no-configs --no-model $args > gpurun_out/try_bench.log 2>&1
