@@ -183,6 +183,150 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// k_rows224p: the row pass of 224-wide images (config 2) with THREE rows per
+// wave (nine channel-rows) instead of rows2_item's one: pass 1 (radix 16, 7
+// butterflies per channel-row) fills 63 of 64 lanes instead of 21, the 672
+// pixels of a wave's three (contiguous) rows are 10.5 per lane instead of 3.5
+// of 4, the colour mix runs on pixel pairs (v_pk_fma_f32, splat_mix) and the
+// Makhoul post is makhoul_pair on the (c1, c2, c3, c4) coefficients (4 VALU per
+// coefficient pair).  A block is 12 rows; no block barrier after the tables.
+// ---------------------------------------------------------------------------
+struct Rows224pLds {
+  static constexpr int MP = RowsLds<224>::MP;
+  float2 z[4][9][MP];
+};
+
+__global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                                                  const float* __restrict__ rgb, float* __restrict__ ws,
+                                                  const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                  ColorMats cm) {
+  constexpr int N = 224, M = 112, R1 = 16, R2 = 7, B1 = 7, B2 = 16, RW = 3;
+  constexpr int MP = Rows224pLds::MP;
+  constexpr int PX = (RW * N + 63) / 64;   // 11 pixels per lane (the last half-populated)
+  constexpr int KI = (M + 63) / 64;
+  __shared__ Rows224pLds L;
+  __shared__ float4 pc[M + 1];
+  __shared__ float2 tw_s[M];
+  {
+    const float4* p4 = reinterpret_cast<const float4*>(post);
+    for (int i = threadIdx.x; i < M + 1; i += 256) {
+      const float4 ab = p4[i];   // (al.x, al.y, be.x, be.y)
+      pc[i] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
+    }
+    for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  }
+  __syncthreads();
+  const int2 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  const int tid = opaque_tid();
+  const int wave = tid >> 6, lane = tid & 63;
+  const int H = d.H, Kw = d.Kw;
+  const int y0 = jb.y + RW * wave;
+  if (y0 >= H) return;   // wave-uniform; no block barrier follows
+  float2(*z)[MP] = L.z[wave];
+  float* zf = reinterpret_cast<float*>(&z[0][0]);
+  const int64_t hw = (int64_t)H * N;
+  const float* src = rgb + d.rgb_off + (int64_t)y0 * N;   // the wave's rows are contiguous
+  const int nq = min(RW, H - y0) * N;
+  float pr[PX + 1], pg[PX + 1], pb[PX + 1];
+#pragma unroll
+  for (int i = 0; i < PX; ++i) {
+    // unconditional loads (pixels past the image's last row re-read pixel
+    // lane; their results are never stored): no per-element control flow
+    const int q = lane + 64 * i, qq = q < nq ? q : lane;
+    pr[i] = src[qq];
+    pg[i] = src[hw + qq];
+    pb[i] = src[2 * hw + qq];
+  }
+  pr[PX] = pg[PX] = pb[PX] = 0.0f;
+  // ---- IPT (util.py:70-82) on pixel pairs + Makhoul reorder into LDS
+  const float gam = 0.430000007152557373046875f;
+#pragma unroll
+  for (int i = 0; i < PX; i += 2) {
+    const cf r2 = (cf){pr[i], pr[i + 1]}, g2 = (cf){pg[i], pg[i + 1]}, b2 = (cf){pb[i], pb[i + 1]};
+    const cf l0 = splat_mix(cm.rgb2lms, 0, r2, g2, b2), l1 = splat_mix(cm.rgb2lms, 1, r2, g2, b2),
+             l2 = splat_mix(cm.rgb2lms, 2, r2, g2, b2);
+    const cf q0 = (cf){signed_pow_fast(l0.x, gam), signed_pow_fast(l0.y, gam)};
+    const cf q1 = (cf){signed_pow_fast(l1.x, gam), signed_pow_fast(l1.y, gam)};
+    const cf q2 = (cf){signed_pow_fast(l2.x, gam), signed_pow_fast(l2.y, gam)};
+    const cf o0 = splat_mix(cm.lms2ipt, 0, q0, q1, q2), o1 = splat_mix(cm.lms2ipt, 1, q0, q1, q2),
+             o2 = splat_mix(cm.lms2ipt, 2, q0, q1, q2);
+#pragma unroll
+    for (int h = 0; h < 2 && i + h < PX; ++h) {
+      const int q = lane + 64 * (i + h);
+      if (q < RW * N) {
+        const int r = (q >= N ? 1 : 0) + (q >= 2 * N ? 1 : 0);
+        const int px = q - N * r;
+        const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
+        float* zr = zf + (3 * r) * 2 * MP + 2 * pad16(v >> 1) + (v & 1);
+        zr[0] = h ? o0.y : o0.x;
+        zr[2 * MP] = h ? o1.y : o1.x;
+        zr[4 * MP] = h ? o2.y : o2.x;
+      }
+    }
+  }
+  // ---- pass 1: radix 16, Ns = 1; in place, one butterfly per lane (63 of 64)
+  if (lane < 9 * B1) {
+    const int c = lane / B1, j = lane - c * B1;
+    float2 v[R1];
+#pragma unroll
+    for (int r = 0; r < R1; ++r) v[r] = z[c][pad16(j + r * B1)];
+    DFT<R1>::run(v);
+#pragma unroll
+    for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = v[r];
+  }
+  // ---- pass 2: radix 7, Ns = 16; twiddle W_M^{r j}; 144 butterflies in 3 rounds
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int b = lane + 64 * t;
+    if (b < 9 * B2) {
+      const int c = b >> 4, j = b & 15;
+      float2 v[R2];
+#pragma unroll
+      for (int r = 0; r < R2; ++r) v[r] = z[c][pad16(j + r * B2)];
+#pragma unroll
+      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * j]);
+      DFT<R2>::run(v);
+#pragma unroll
+      for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
+    }
+  }
+  // ---- Makhoul post -> T: (X[k], X[N - k]) = makhoul_pair(Z[k], Z[M - k]), k = lane + 64 i
+  int oa[KI], ob[KI];
+#pragma unroll
+  for (int i = 0; i < KI; ++i) {
+    const int k = lane + 64 * i;
+    oa[i] = (k < M && k < Kw) ? k : -1;
+    ob[i] = (k < M && k >= 1 && N - k < Kw) ? N - k : -1;
+  }
+  const int64_t cstride = (int64_t)H * Kw;
+  float* T = ws + d.ws_t;
+#pragma unroll 1
+  for (int cr = 0; cr < 9; ++cr) {
+    const int rr = cr / 3, c = cr - 3 * rr;
+    const int y = y0 + rr;
+    if (y >= H) break;
+    float* tb = T + c * cstride + (int64_t)y * Kw;
+#pragma unroll
+    for (int i = 0; i < KI; ++i) {
+      const int k = lane + 64 * i;
+      if (k < M) {
+        const float4 cc = pc[k];
+        const float2 A = z[cr][pad16(k)], P = z[cr][pad16(k == 0 ? 0 : M - k)];
+        const cf t = makhoul_pair((cf){A.x, A.y}, (cf){P.x, P.y}, (cf){cc.x, cc.y}, (cf){cc.z, cc.w});
+        if (oa[i] >= 0) tb[oa[i]] = t.x;
+        if (ob[i] >= 0) tb[ob[i]] = t.y;
+      }
+    }
+    if (lane == 0 && M < Kw) {   // k = M: Z[0] with itself
+      const float2 A = z[cr][0];
+      const float4 cc = pc[M];
+      tb[M] = makhoul_pair((cf){A.x, A.y}, (cf){A.x, A.y}, (cf){cc.x, cc.y}, (cf){cc.z, cc.w}).x;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // cols, linear-address form: every LDS address is (lane base) + (compile-time
 // constant), so address arithmetic folds into the ds_read / ds_write offset
 // fields instead of costing VALU (the column kernel is VALU-issue bound).
@@ -613,6 +757,239 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// k_cols224: the column pass of 224-high images (config 2), two column items
+// (image, channel, tile-column strip) per block and 8 lanes per column instead
+// of k_fft_cols4's 16.  k_fft_cols4<224> is VALU-issue bound (666 VALU per
+// wave for 3.5 columns, 1 block per item); here, per wave of 7 columns:
+//  * pass 1 (radix 16, 7 butterflies per column) runs on 7 / 8 of the lanes
+//    instead of 7 / 16; pass 2 (radix 7, 16 butterflies) is two per lane;
+//  * the Makhoul post is makhoul_pair2 on the (c1, c2, c3, c4) coefficients
+//    (VOP3P modifiers for the conjugates and swaps: 4 VALU per coefficient
+//    pair, as the 512 kernels);
+//  * the THR epilogue is cols512b_epilogue's (v_cmp + v_addc code bits, one
+//    v_maximum3_f32 per two |x|, buffer stores), one tile row of each item per
+//    thread; with an odd item count the second item repeats the first (the
+//    same values to the same addresses, no branches).
+// ---------------------------------------------------------------------------
+template <bool THR>
+__global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
+                                                 int n_items, const float* __restrict__ ws,
+                                                 const float2* __restrict__ tw, const float2* __restrict__ post,
+                                                 EncParams ep, TokenSinks sk) {
+#pragma clang fp contract(fast)
+  constexpr int N = 224, M = 112, R1 = 16, R2 = 7, B1 = 7, KS = 14;
+  constexpr int KSP = 2 * KS + 1;                 // 28 columns (two strips) + 1
+  constexpr int ZROWS = 2 * (pad16(M - 1) + 1);   // padded complex layout, in floats per column
+  static_assert(N <= ZROWS, "natural rows fit the complex layout");
+  __shared__ float zs[ZROWS * KSP];
+  __shared__ float4 pc[M + 1];     // (c1, c2, c3, c4) of makhoul_pair (rows512_tables)
+  __shared__ float2 tw_s[M];
+  __shared__ float sbias[2][16];   // -(h + strip) / ci[c] per item and tile row h (fp32 division, FE:411-416)
+  {
+    const float4* p4 = reinterpret_cast<const float4*>(post);
+    for (int i = threadIdx.x; i < M + 1; i += 256) {
+      const float4 ab = p4[i];   // (al.x, al.y, be.x, be.y)
+      pc[i] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
+    }
+    for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  }
+  const int tid = opaque_tid();
+  const int i0 = 2 * blockIdx.x;
+  const int4 ja = blocks[i0], jb = blocks[i0 + 1 < n_items ? i0 + 1 : i0];
+  const ImgDesc da = imgs[ja.x], db = imgs[jb.x];
+  // ---- LFQ-bit thresholds of this thread's epilogue row in each item (lanes
+  //      14 / 15 repeat row 13, as cols_thresholds)
+  const int g16 = tid >> 4, jl = tid & 15, jlc = min(jl, KS - 1);
+  float2 thr_r[2][KS / 2];
+  if (THR) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const ImgDesc& d = u ? db : da;
+      const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
+      if (g16 < d.qh) {
+        const float2* t2 = reinterpret_cast<const float2*>(
+            ep.thr + ((((int64_t)c * ep.maxph + g16) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jlc * KS);
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) thr_r[u][p] = t2[p];
+      }
+    }
+    if (tid < 32) {
+      const int u = tid >> 4, h = tid & 15;
+      const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
+      sbias[u][h] = __fdiv_rn(-(float)(h + strip), ep.ci[c]);
+    }
+  }
+  // ---- T slices -> LDS, natural row order: thread t < 224 of item u = t / 112
+  //      holds float2 p = t % 7 of rows y0 + 16 k, y0 = (t % 112) / 7
+  if (tid < 224) {
+    const int u = tid >= 112 ? 1 : 0, t = tid - 112 * u;
+    const int y0 = t / (KS / 2), p = t - y0 * (KS / 2);
+    const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
+    const int64_t tbase = u ? db.ws_t : da.ws_t;
+    const int H = u ? db.H : da.H, Kw = u ? db.Kw : da.Kw;
+    const c4f2* src = reinterpret_cast<const c4f2*>(ws + tbase + ((int64_t)c * H + y0) * Kw + strip * KS) + p;
+    const int64_t rstep = (int64_t)8 * Kw;   // 16 rows, in float2
+    c4f2 tv[N / 16];
+#pragma unroll
+    for (int k = 0; k < N / 16; ++k) tv[k] = src[k * rstep];
+    float* dst = zs + y0 * KSP + KS * u + 2 * p;
+#pragma unroll
+    for (int k = 0; k < N / 16; ++k) {
+      dst[16 * KSP * k] = tv[k].x;
+      dst[16 * KSP * k + 1] = tv[k].y;
+    }
+  }
+  __syncthreads();
+  const int jj = tid & 7, col = tid >> 3;   // column col of the 28 (item col / 14)
+  const bool on_col = col < 2 * KS;
+  // ---- pass 1 (radix 16, Ns = 1), Makhoul reorder folded into the read addresses (as cols4_item)
+  {
+    cf v[R1];
+    const bool on = on_col && jj < B1;
+    if (on) {
+      const float* lo = zs + 4 * jj * KSP + col;
+      const float* hi = zs + (2 * N - 3 - 4 * jj - 4 * B1 * (R1 - 1)) * KSP + col;
+#pragma unroll
+      for (int r = 0; r < R1 / 2; ++r) v[r] = (cf){lo[4 * B1 * r * KSP], lo[(4 * B1 * r + 2) * KSP]};
+#pragma unroll
+      for (int r = R1 / 2; r < R1; ++r)
+        v[r] = (cf){hi[(4 * B1 * (R1 - 1 - r) + 2) * KSP], hi[4 * B1 * (R1 - 1 - r) * KSP]};
+      DFTV<R1>::run(v);
+    }
+    __syncthreads();
+    if (on) {
+      float* o = zs + 2 * 17 * jj * KSP + col;   // z[16 jj + r]: pad16 = 17 jj + r
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        o[2 * r * KSP] = v[r].x;
+        o[(2 * r + 1) * KSP] = v[r].y;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- pass 2 (radix 7, Ns = 16): butterflies j = jj and jj + 8, z[j + 16 r] at pad16 = j + 17 r
+  {
+    cf v[2][R2];
+    if (on_col) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = jj + 8 * h;
+        const float* z = zs + 2 * jj * KSP + 16 * h * KSP + col;
+#pragma unroll
+        for (int r = 0; r < R2; ++r) v[h][r] = (cf){z[2 * 17 * r * KSP], z[(2 * 17 * r + 1) * KSP]};
+#pragma unroll
+        for (int r = 1; r < R2; ++r) {
+          const float2 w = tw_s[r * j];
+          v[h][r] = cmulv(v[h][r], (cf){w.x, w.y});
+        }
+        DFTV<R2>::run(v[h]);
+      }
+    }
+    __syncthreads();
+    if (on_col) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float* z = zs + 2 * jj * KSP + 16 * h * KSP + col;
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {
+          z[2 * 17 * r * KSP] = v[h][r].x;
+          z[(2 * 17 * r + 1) * KSP] = v[h][r].y;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- Makhoul post-processing: (X[k], X[N - k]) = makhoul_pair(Z[k], Z[M - k])
+  //      for k = jj + 8 i (i < 14): Z[k] at pad16 = jj + 8 i + i / 2; Z[M - k]
+  //      at pad16 = 8 (14 - i) - jj + (13 - i) / 2 for jj >= 1, one more for
+  //      jj = 0 and even i; k = 0 and k = M pair Z[0] with itself
+  constexpr int M8 = M / 8;
+  cf wv[M8 + 1];
+  if (on_col) {
+    const float* za = zs + 2 * jj * KSP + col;
+    const int e = jj == 0 ? 1 : 0;
+    const float* zbo = zs + 2 * (8 - jj) * KSP + col;       // odd i: + 8 (13 - i) + (13 - i) / 2
+    const float* zbe = zs + 2 * (8 - jj + e) * KSP + col;   // even i >= 2
+    const float* zb0 = jj == 0 ? zs + col : zs + 2 * (118 - jj) * KSP + col;   // i = 0: Z[112 - jj] or Z[0]
+    const float4* pcl = pc + jj;
+    cf A[M8], P[M8];
+#pragma unroll
+    for (int i = 0; i < M8; ++i) {
+      const int pa = 8 * i + (i >> 1);
+      A[i] = (cf){za[2 * pa * KSP], za[(2 * pa + 1) * KSP]};
+      const int pb = 8 * (13 - i) + ((13 - i) >> 1);
+      const float* zb = i == 0 ? zb0 : ((i & 1) ? zbo + 2 * pb * KSP : zbe + 2 * pb * KSP);
+      P[i] = (cf){zb[0], zb[KSP]};
+    }
+#pragma unroll
+    for (int i = 0; i < M8; i += 2) makhoul_pair2(A[i], P[i], pcl[8 * i], A[i + 1], P[i + 1], pcl[8 * i + 8], wv[i], wv[i + 1]);
+    if (jj == 0) {   // k = M: Z[0] with itself
+      const cf Z0 = (cf){zs[col], zs[KSP + col]};
+      const float4 cm = pc[M];
+      wv[M8] = makhoul_pair(Z0, Z0, (cf){cm.x, cm.y}, (cf){cm.z, cm.w});
+    }
+  }
+  __syncthreads();
+  if (on_col) {
+    const int Kh = col >= KS ? db.Kh : da.Kh;
+    float* xo = zs + jj * KSP + col;                          // X[k] at row k
+    float* xn = zs + (N - jj - 8 * (M8 - 1)) * KSP + col;     // X[N - k], from the lowest row
+#pragma unroll
+    for (int i = 0; i < M8; ++i) {
+      const int k = jj + 8 * i;
+      if (k < Kh) xo[8 * i * KSP] = wv[i].x;
+      if (k >= 1 && N - k < Kh) xn[8 * (M8 - 1 - i) * KSP] = wv[i].y;
+    }
+    if (jj == 0 && M < Kh) zs[M * KSP + col] = wv[M8].x;
+  }
+  __syncthreads();
+  // ---- token epilogue: tile (h = g16, strip) of each item
+  if (THR) {
+    const float* row0 = zs + (KS * g16 + jlc) * KSP;   // item 0: columns 0 .. 13; item 1: 14 .. 27
+    uint32_t code0 = 0, code1 = 0;
+    float am0 = 0.0f, am1 = 0.0f;
+#pragma unroll
+    for (int p = 0; p < KS / 2; ++p)
+      code_bits4(code0, code1, am0, am1, (f2v){row0[2 * p], row0[2 * p + 1]},
+                 (f2v){row0[KS + 2 * p], row0[KS + 2 * p + 1]}, thr_r[0][p], thr_r[1][p]);
+    uint32_t u0 = __float_as_uint(am0), u1 = __float_as_uint(am1);
+#define DCTAE_ROR_MAX(ctl)                                                        \
+  u0 = max(u0, (uint32_t)__builtin_amdgcn_mov_dpp((int)u0, ctl, 0xf, 0xf, false)); \
+  u1 = max(u1, (uint32_t)__builtin_amdgcn_mov_dpp((int)u1, ctl, 0xf, 0xf, false));
+    DCTAE_ROR_MAX(0x128) DCTAE_ROR_MAX(0x124) DCTAE_ROR_MAX(0x122) DCTAE_ROR_MAX(0x121)
+#undef DCTAE_ROR_MAX
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const ImgDesc& d = u ? db : da;
+      const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
+      if (g16 < d.qh) {
+        const int64_t tok = cols_tok(d, c, strip, g16, ep.C);
+        sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(u ? u1 : u0), ep.mw), sbias[u][g16]);
+        if (sk.codes) sk.codes[tok * KS + jlc] = (uint16_t)(u ? code1 : code0);
+        if (sk.raw) {
+          const float* row = row0 + KS * u;
+#pragma unroll
+          for (int p2 = 0; p2 < KS; ++p2) sk.raw[tok * KS * KS + jlc * KS + p2] = row[p2];
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const ImgDesc& d = u ? db : da;
+      const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
+      for (int h = g16; h < d.qh; h += 16) {
+        float vals[KS];
+        const float* row = zs + (KS * h + jl) * KSP + KS * u;
+#pragma unroll
+        for (int p2 = 0; p2 < KS; ++p2) vals[p2] = row[p2];
+        token_epilogue_p<KS>(ep, c, h, strip, jl, vals, cols_tok(d, c, strip, h, ep.C), sk);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
 
@@ -623,13 +1000,20 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
   return 0;
 }
 
-int fft_spec_rows_per_block(int spec) { return spec == 2 ? 4 * DCTAE_RPW224 : (spec ? 16 : 0); }
+#ifndef DCTAE_ROWS224P
+#define DCTAE_ROWS224P 1
+#endif
+int fft_spec_rows_per_block(int spec) {
+  return spec == 2 ? (DCTAE_ROWS224P ? 12 : 4 * DCTAE_RPW224) : (spec ? 16 : 0);
+}
 
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                           const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s) {
   if (n_blocks <= 0) return;
   if (spec == 1)
     hipLaunchKernelGGL((k_fft_rows2<512, 16, 16>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+  else if (spec == 2 && DCTAE_ROWS224P)
+    hipLaunchKernelGGL(k_rows224p, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
   else if (spec == 2)
     hipLaunchKernelGGL((k_fft_rows2<224, 16, 7>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
 }
@@ -665,6 +1049,15 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
                      imgs, blocks, n_blocks, ws, tw, post, ep, sk)
   if (spec == 1 && thr) DCTAE_COLS4(512, 16, true, 1);
   else if (spec == 1) DCTAE_COLS4(512, 16, false, 1);
+#ifndef DCTAE_COLS224
+#define DCTAE_COLS224 1
+#endif
+  else if (spec == 2 && DCTAE_COLS224 && thr)
+    hipLaunchKernelGGL((k_cols224<true>), dim3((n_blocks + 1) / 2), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw,
+                       post, ep, sk);
+  else if (spec == 2 && DCTAE_COLS224)
+    hipLaunchKernelGGL((k_cols224<false>), dim3((n_blocks + 1) / 2), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw,
+                       post, ep, sk);
   else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true, DCTAE_C4_IPB224);
   else if (spec == 2) DCTAE_COLS4(224, 7, false, DCTAE_C4_IPB224);
 #undef DCTAE_COLS4
