@@ -268,12 +268,15 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
   // ---- pass 1: radix 16, Ns = 1; in place, one butterfly per lane (63 of 64)
   if (lane < 9 * B1) {
     const int c = lane / B1, j = lane - c * B1;
-    float2 v[R1];
+    cf v[R1];
 #pragma unroll
-    for (int r = 0; r < R1; ++r) v[r] = z[c][pad16(j + r * B1)];
-    DFT<R1>::run(v);
+    for (int r = 0; r < R1; ++r) {
+      const float2 x = z[c][pad16(j + r * B1)];
+      v[r] = (cf){x.x, x.y};
+    }
+    DFTV<R1>::run(v);
 #pragma unroll
-    for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = v[r];
+    for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = make_float2(v[r].x, v[r].y);
   }
   // ---- pass 2: radix 7, Ns = 16; twiddle W_M^{r j}; 144 butterflies in 3 rounds
 #pragma unroll
@@ -281,14 +284,20 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
     const int b = lane + 64 * t;
     if (b < 9 * B2) {
       const int c = b >> 4, j = b & 15;
-      float2 v[R2];
+      cf v[R2];
 #pragma unroll
-      for (int r = 0; r < R2; ++r) v[r] = z[c][pad16(j + r * B2)];
+      for (int r = 0; r < R2; ++r) {
+        const float2 x = z[c][pad16(j + r * B2)];
+        v[r] = (cf){x.x, x.y};
+      }
 #pragma unroll
-      for (int r = 1; r < R2; ++r) v[r] = cmul(v[r], tw_s[r * j]);
-      DFT<R2>::run(v);
+      for (int r = 1; r < R2; ++r) {
+        const float2 w = tw_s[r * j];
+        v[r] = cmul_pk(v[r], (cf){w.x, w.y});
+      }
+      DFTV<R2>::run(v);
 #pragma unroll
-      for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = v[r];
+      for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = make_float2(v[r].x, v[r].y);
     }
   }
   // ---- Makhoul post -> T: (X[k], X[N - k]) = makhoul_pair(Z[k], Z[M - k]), k = lane + 64 i
@@ -880,7 +889,7 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
 #pragma unroll
         for (int r = 1; r < R2; ++r) {
           const float2 w = tw_s[r * j];
-          v[h][r] = cmulv(v[h][r], (cf){w.x, w.y});
+          v[h][r] = cmul_pk(v[h][r], (cf){w.x, w.y});
         }
         DFTV<R2>::run(v[h]);
       }
@@ -931,16 +940,25 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
   }
   __syncthreads();
   if (on_col) {
-    const int Kh = col >= KS ? db.Kh : da.Kh;
     float* xo = zs + jj * KSP + col;                          // X[k] at row k
     float* xn = zs + (N - jj - 8 * (M8 - 1)) * KSP + col;     // X[N - k], from the lowest row
+    if (da.Kh >= N && db.Kh >= N) {   // every row kept (wave-uniform): no per-row compares
 #pragma unroll
-    for (int i = 0; i < M8; ++i) {
-      const int k = jj + 8 * i;
-      if (k < Kh) xo[8 * i * KSP] = wv[i].x;
-      if (k >= 1 && N - k < Kh) xn[8 * (M8 - 1 - i) * KSP] = wv[i].y;
+      for (int i = 0; i < M8; ++i) {
+        xo[8 * i * KSP] = wv[i].x;
+        if (i > 0 || jj > 0) xn[8 * (M8 - 1 - i) * KSP] = wv[i].y;
+      }
+      if (jj == 0) zs[M * KSP + col] = wv[M8].x;
+    } else {
+      const int Kh = col >= KS ? db.Kh : da.Kh;
+#pragma unroll
+      for (int i = 0; i < M8; ++i) {
+        const int k = jj + 8 * i;
+        if (k < Kh) xo[8 * i * KSP] = wv[i].x;
+        if (k >= 1 && N - k < Kh) xn[8 * (M8 - 1 - i) * KSP] = wv[i].y;
+      }
+      if (jj == 0 && M < Kh) zs[M * KSP + col] = wv[M8].x;
     }
-    if (jj == 0 && M < Kh) zs[M * KSP + col] = wv[M8].x;
   }
   __syncthreads();
   // ---- token epilogue: tile (h = g16, strip) of each item
