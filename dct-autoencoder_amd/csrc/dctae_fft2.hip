@@ -239,8 +239,19 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
     pb[i] = src[2 * hw + qq];
   }
   pr[PX] = pg[PX] = pb[PX] = 0.0f;
-  // ---- IPT (util.py:70-82) on pixel pairs + Makhoul reorder into LDS
+  // ---- IPT (util.py:70-82) on pixel pairs + Makhoul reorder into LDS.  The
+  //      LDS slot of pixel q = lane + 64 i repeats with period 7 in i (448 =
+  //      7 x 64 pixels = two rows): slot(i + 7) = slot(i) + two rows' channels
   const float gam = 0.430000007152557373046875f;
+  int slot7[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int q = lane + 64 * i;
+    const int r = (q >= N ? 1 : 0) + (q >= 2 * N ? 1 : 0);
+    const int px = q - N * r;
+    const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
+    slot7[i] = (3 * r) * 2 * MP + 2 * pad16(v >> 1) + (v & 1);
+  }
 #pragma unroll
   for (int i = 0; i < PX; i += 2) {
     const cf r2 = (cf){pr[i], pr[i + 1]}, g2 = (cf){pg[i], pg[i + 1]}, b2 = (cf){pb[i], pb[i + 1]};
@@ -255,10 +266,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
     for (int h = 0; h < 2 && i + h < PX; ++h) {
       const int q = lane + 64 * (i + h);
       if (q < RW * N) {
-        const int r = (q >= N ? 1 : 0) + (q >= 2 * N ? 1 : 0);
-        const int px = q - N * r;
-        const int v = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
-        float* zr = zf + (3 * r) * 2 * MP + 2 * pad16(v >> 1) + (v & 1);
+        float* zr = zf + (i + h < 7 ? slot7[i + h] : slot7[i + h - 7] + 6 * 2 * MP);
         zr[0] = h ? o0.y : o0.x;
         zr[2 * MP] = h ? o1.y : o1.x;
         zr[4 * MP] = h ? o2.y : o2.x;
