@@ -1027,7 +1027,7 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
 }
 
 #ifndef DCTAE_ROWS224P
-#define DCTAE_ROWS224P 1
+#define DCTAE_ROWS224P 0   // on after the GPU parity run
 #endif
 int fft_spec_rows_per_block(int spec) {
   return spec == 2 ? (DCTAE_ROWS224P ? 12 : 4 * DCTAE_RPW224) : (spec ? 16 : 0);
@@ -1076,7 +1076,7 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
   if (spec == 1 && thr) DCTAE_COLS4(512, 16, true, 1);
   else if (spec == 1) DCTAE_COLS4(512, 16, false, 1);
 #ifndef DCTAE_COLS224
-#define DCTAE_COLS224 1
+#define DCTAE_COLS224 0   // on after the GPU parity run
 #endif
   else if (spec == 2 && DCTAE_COLS224 && thr)
     hipLaunchKernelGGL((k_cols224<true>), dim3((n_blocks + 1) / 2), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw,
