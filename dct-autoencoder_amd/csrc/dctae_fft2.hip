@@ -183,28 +183,32 @@ __global__ __launch_bounds__(256) void k_fft_rows2(const ImgDesc* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
-// k_rows224p: the row pass of 224-wide images (config 2) with THREE rows per
-// wave (nine channel-rows) instead of rows2_item's one: pass 1 (radix 16, 7
-// butterflies per channel-row) fills 63 of 64 lanes instead of 21, the 672
-// pixels of a wave's three (contiguous) rows are 10.5 per lane instead of 3.5
-// of 4, the colour mix runs on pixel pairs (v_pk_fma_f32, splat_mix) and the
-// Makhoul post is makhoul_pair on the (c1, c2, c3, c4) coefficients (4 VALU per
-// coefficient pair).  A block is 12 rows; no block barrier after the tables.
+// k_rows224p<RW>: the row pass of 224-wide images (config 2) with RW = 2 or 3
+// rows per wave (3 RW channel-rows) instead of rows2_item's one: pass 1 (radix
+// 16, 7 butterflies per channel-row) fills 42 / 63 of 64 lanes instead of 21,
+// a wave's RW contiguous rows are 7 / 10.5 pixels per lane instead of 3.5 of 4,
+// the colour mix runs on pixel pairs (v_pk_fma_f32, splat_mix) and the Makhoul
+// post is makhoul_pair on the (c1, c2, c3, c4) coefficients (4 VALU per
+// coefficient pair).  A block is 4 RW rows; no block barrier after the tables.
 // ---------------------------------------------------------------------------
+template <int RW>
 struct Rows224pLds {
   static constexpr int MP = RowsLds<224>::MP;
-  float2 z[4][9][MP];
+  float2 z[4][3 * RW][MP];
 };
 
+template <int RW>
 __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                   const float* __restrict__ rgb, float* __restrict__ ws,
                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
                                                   ColorMats cm) {
-  constexpr int N = 224, M = 112, R1 = 16, R2 = 7, B1 = 7, B2 = 16, RW = 3;
-  constexpr int MP = Rows224pLds::MP;
-  constexpr int PX = (RW * N + 63) / 64;   // 11 pixels per lane (the last half-populated)
+  constexpr int N = 224, M = 112, R1 = 16, R2 = 7, B1 = 7, B2 = 16;
+  static_assert(RW == 2 || RW == 3, "rows per wave");
+  constexpr int CR = 3 * RW;                 // channel-rows per wave
+  constexpr int MP = Rows224pLds<RW>::MP;
+  constexpr int PX = (RW * N + 63) / 64;   // pixels per lane: 7 (RW = 2) or 11 (the last half-populated)
   constexpr int KI = (M + 63) / 64;
-  __shared__ Rows224pLds L;
+  __shared__ Rows224pLds<RW> L;
   __shared__ float4 pc[M + 1];
   __shared__ float2 tw_s[M];
   {
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
     }
   }
   // ---- pass 1: radix 16, Ns = 1; in place, one butterfly per lane (63 of 64)
-  if (lane < 9 * B1) {
+  if (lane < CR * B1) {
     const int c = lane / B1, j = lane - c * B1;
     cf v[R1];
 #pragma unroll
@@ -288,9 +292,9 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
   }
   // ---- pass 2: radix 7, Ns = 16; twiddle W_M^{r j}; 144 butterflies in 3 rounds
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
+  for (int t = 0; t < (CR * B2 + 63) / 64; ++t) {
     const int b = lane + 64 * t;
-    if (b < 9 * B2) {
+    if (b < CR * B2) {
       const int c = b >> 4, j = b & 15;
       cf v[R2];
 #pragma unroll
@@ -319,7 +323,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
   const int64_t cstride = (int64_t)H * Kw;
   float* T = ws + d.ws_t;
 #pragma unroll 1
-  for (int cr = 0; cr < 9; ++cr) {
+  for (int cr = 0; cr < CR; ++cr) {
     const int rr = cr / 3, c = cr - 3 * rr;
     const int y = y0 + rr;
     if (y >= H) break;
@@ -814,22 +818,8 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
   const int i0 = 2 * blockIdx.x;
   const int4 ja = blocks[i0], jb = blocks[i0 + 1 < n_items ? i0 + 1 : i0];
   const ImgDesc da = imgs[ja.x], db = imgs[jb.x];
-  // ---- LFQ-bit thresholds of this thread's epilogue row in each item (lanes
-  //      14 / 15 repeat row 13, as cols_thresholds)
   const int g16 = tid >> 4, jl = tid & 15, jlc = min(jl, KS - 1);
-  float2 thr_r[2][KS / 2];
   if (THR) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const ImgDesc& d = u ? db : da;
-      const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
-      if (g16 < d.qh) {
-        const float2* t2 = reinterpret_cast<const float2*>(
-            ep.thr + ((((int64_t)c * ep.maxph + g16) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jlc * KS);
-#pragma unroll
-        for (int p = 0; p < KS / 2; ++p) thr_r[u][p] = t2[p];
-      }
-    }
     if (tid < 32) {
       const int u = tid >> 4, h = tid & 15;
       const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
@@ -916,6 +906,24 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
     }
     __syncthreads();
   }
+  // ---- LFQ-bit thresholds of this thread's epilogue row in each item (lanes
+  //      14 / 15 repeat row 13, as cols_thresholds): loaded here, in flight
+  //      during the post-processing (at the top of the kernel they held 28
+  //      VGPRs through both passes: 138 VGPRs, 3 waves / SIMD)
+  float2 thr_r[2][KS / 2];
+  if (THR) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const ImgDesc& d = u ? db : da;
+      const int c = u ? jb.y : ja.y, strip = u ? jb.z : ja.z;
+      if (g16 < d.qh) {
+        const float2* t2 = reinterpret_cast<const float2*>(
+            ep.thr + ((((int64_t)c * ep.maxph + g16) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jlc * KS);
+#pragma unroll
+        for (int p = 0; p < KS / 2; ++p) thr_r[u][p] = t2[p];
+      }
+    }
+  }
   // ---- Makhoul post-processing: (X[k], X[N - k]) = makhoul_pair(Z[k], Z[M - k])
   //      for k = jj + 8 i (i < 14): Z[k] at pad16 = jj + 8 i + i / 2; Z[M - k]
   //      at pad16 = 8 (14 - i) - jj + (13 - i) / 2 for jj >= 1, one more for
@@ -929,17 +937,21 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
     const float* zbe = zs + 2 * (8 - jj + e) * KSP + col;   // even i >= 2
     const float* zb0 = jj == 0 ? zs + col : zs + 2 * (118 - jj) * KSP + col;   // i = 0: Z[112 - jj] or Z[0]
     const float4* pcl = pc + jj;
-    cf A[M8], P[M8];
 #pragma unroll
-    for (int i = 0; i < M8; ++i) {
-      const int pa = 8 * i + (i >> 1);
-      A[i] = (cf){za[2 * pa * KSP], za[(2 * pa + 1) * KSP]};
-      const int pb = 8 * (13 - i) + ((13 - i) >> 1);
-      const float* zb = i == 0 ? zb0 : ((i & 1) ? zbo + 2 * pb * KSP : zbe + 2 * pb * KSP);
-      P[i] = (cf){zb[0], zb[KSP]};
+    for (int i = 0; i < M8; i += 2) {
+      cf A[2], P[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ii = i + h;
+        const int pa = 8 * ii + (ii >> 1);
+        A[h] = (cf){za[2 * pa * KSP], za[(2 * pa + 1) * KSP]};
+        const int pb = 8 * (13 - ii) + ((13 - ii) >> 1);
+        const float* zb = ii == 0 ? zb0 : ((ii & 1) ? zbo + 2 * pb * KSP : zbe + 2 * pb * KSP);
+        P[h] = (cf){zb[0], zb[KSP]};
+      }
+      makhoul_pair2(A[0], P[0], pcl[8 * i], A[1], P[1], pcl[8 * i + 8], wv[i], wv[i + 1]);
+      if ((i & 3) == 2) __builtin_amdgcn_sched_barrier(0);   // bound the LDS reads in flight (registers)
     }
-#pragma unroll
-    for (int i = 0; i < M8; i += 2) makhoul_pair2(A[i], P[i], pcl[8 * i], A[i + 1], P[i + 1], pcl[8 * i + 8], wv[i], wv[i + 1]);
     if (jj == 0) {   // k = M: Z[0] with itself
       const cf Z0 = (cf){zs[col], zs[KSP + col]};
       const float4 cm = pc[M];
@@ -1027,10 +1039,10 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
 }
 
 #ifndef DCTAE_ROWS224P
-#define DCTAE_ROWS224P 0   // on after the GPU parity run
+#define DCTAE_ROWS224P 0   // on after the GPU parity run; rows per wave of k_rows224p (2 or 3)
 #endif
 int fft_spec_rows_per_block(int spec) {
-  return spec == 2 ? (DCTAE_ROWS224P ? 12 : 4 * DCTAE_RPW224) : (spec ? 16 : 0);
+  return spec == 2 ? (DCTAE_ROWS224P ? 4 * DCTAE_ROWS224P : 4 * DCTAE_RPW224) : (spec ? 16 : 0);
 }
 
 void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
@@ -1039,7 +1051,8 @@ void launch_fft_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int
   if (spec == 1)
     hipLaunchKernelGGL((k_fft_rows2<512, 16, 16>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
   else if (spec == 2 && DCTAE_ROWS224P)
-    hipLaunchKernelGGL(k_rows224p, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
+    hipLaunchKernelGGL((k_rows224p<DCTAE_ROWS224P == 3 ? 3 : 2>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb,
+                       ws, tw, post, cm);
   else if (spec == 2)
     hipLaunchKernelGGL((k_fft_rows2<224, 16, 7>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, tw, post, cm);
 }
