@@ -745,7 +745,16 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   __shared__ float sbias[32];   // -(h + strip) / ci[c] per tile row h (fp32 division, FE:411-416)
   for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
   for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
-  const int i0 = blockIdx.x * IPB;
+#ifndef DCTAE_C4_XCD
+#define DCTAE_C4_XCD 0
+#endif
+  int gidx = blockIdx.x;
+  if (DCTAE_C4_XCD) {   // XCD-dealt item groups (as k_cols224)
+    const int n_g = (n_items + IPB - 1) / IPB, per_x = (n_g + 7) / 8;
+    gidx = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+    if (gidx >= n_g) return;
+  }
+  const int i0 = gidx * IPB;
   if (IPB == 1) {
     const int4 jb = blocks[i0];
     const ImgDesc d = imgs[jb.x];
@@ -814,8 +823,14 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
     }
     for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
   }
+  // XCD-dealt pairs: XCD x (blocks b = x + 8 s) runs pairs [x per_x, (x + 1)
+  // per_x) in order, so the neighbouring strips of one (image, channel), which
+  // share T's 128-byte lines, are read through the same L2 at about the same time
+  const int n_pairs = (n_items + 1) / 2, per_x = (n_pairs + 7) / 8;
+  const int pidx = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
+  if (pidx >= n_pairs) return;   // block-uniform, before any barrier
   const int tid = opaque_tid();
-  const int i0 = 2 * blockIdx.x;
+  const int i0 = 2 * pidx;
   const int4 ja = blocks[i0], jb = blocks[i0 + 1 < n_items ? i0 + 1 : i0];
   const ImgDesc da = imgs[ja.x], db = imgs[jb.x];
   const int g16 = tid >> 4, jl = tid & 15, jlc = min(jl, KS - 1);
@@ -1084,7 +1099,9 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
 #define DCTAE_C4_IPB224 1
 #endif
 #define DCTAE_COLS4(NN, RR, T, IPB)                                                                       \
-  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T, IPB>), dim3((n_blocks + IPB - 1) / IPB), dim3(256), 0, s, \
+  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T, IPB>),                                                   \
+                     dim3(DCTAE_C4_XCD ? 8 * (((n_blocks + IPB - 1) / IPB + 7) / 8) : (n_blocks + IPB - 1) / IPB), \
+                     dim3(256), 0, s,                                                                      \
                      imgs, blocks, n_blocks, ws, tw, post, ep, sk)
   if (spec == 1 && thr) DCTAE_COLS4(512, 16, true, 1);
   else if (spec == 1) DCTAE_COLS4(512, 16, false, 1);
@@ -1092,11 +1109,11 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
 #define DCTAE_COLS224 0   // on after the GPU parity run
 #endif
   else if (spec == 2 && DCTAE_COLS224 && thr)
-    hipLaunchKernelGGL((k_cols224<true>), dim3((n_blocks + 1) / 2), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw,
-                       post, ep, sk);
+    hipLaunchKernelGGL((k_cols224<true>), dim3(8 * (((n_blocks + 1) / 2 + 7) / 8)), dim3(256), 0, s, imgs, blocks,
+                       n_blocks, ws, tw, post, ep, sk);
   else if (spec == 2 && DCTAE_COLS224)
-    hipLaunchKernelGGL((k_cols224<false>), dim3((n_blocks + 1) / 2), dim3(256), 0, s, imgs, blocks, n_blocks, ws, tw,
-                       post, ep, sk);
+    hipLaunchKernelGGL((k_cols224<false>), dim3(8 * (((n_blocks + 1) / 2 + 7) / 8)), dim3(256), 0, s, imgs, blocks,
+                       n_blocks, ws, tw, post, ep, sk);
   else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true, DCTAE_C4_IPB224);
   else if (spec == 2) DCTAE_COLS4(224, 7, false, DCTAE_C4_IPB224);
 #undef DCTAE_COLS4
