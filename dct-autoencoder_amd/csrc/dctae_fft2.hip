@@ -40,11 +40,7 @@ __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const 
 #ifndef DCTAE_RPW224
 #define DCTAE_RPW224 1   // 224-wide rows: one row per wave (0.074 vs 0.081 ms at 4 rows per wave, config 2)
 #endif
-#ifndef DCTAE_ROWPF224
-#define DCTAE_ROWPF224 0
-#endif
   constexpr int RPW = N == 224 ? DCTAE_RPW224 : 4;   // rows per wave (block = 4 RPW rows)
-  constexpr bool ROWPF = N == 224 && DCTAE_ROWPF224 && RPW > 1;   // next row's pixels prefetched
   static_assert(R1 * R2 == M, "two-pass plan");
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
@@ -92,24 +88,17 @@ __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const 
     }
   };
   int y = y_first + wave;
-  if (ROWPF) fetch(y);
 #pragma unroll 1
   for (int rr = 0; rr < RPW; ++rr, y += 4) {
     if (y >= H) break;
-    // with ROWPF this row's pixels arrived with the previous iteration and the
-    // next row's loads are in flight during this row's transform
-    if (!ROWPF) fetch(y);
-    float cr[PX], cg[PX], cb[PX];
-#pragma unroll
-    for (int i = 0; i < PX; ++i) cr[i] = pr[i], cg[i] = pg[i], cb[i] = pb[i];
-    if (ROWPF && rr + 1 < RPW) fetch(y + 4);
+    fetch(y);
     // ---- IPT (util.py:70-82) + Makhoul reorder into LDS
 #pragma unroll
     for (int i = 0; i < PX; ++i) {
       if (lane + 64 * i < N) {
-        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, cr[i], cg[i], cb[i]), gam);
-        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, cr[i], cg[i], cb[i]), gam);
-        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, cr[i], cg[i], cb[i]), gam);
+        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, pr[i], pg[i], pb[i]), gam);
+        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, pr[i], pg[i], pb[i]), gam);
+        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, pr[i], pg[i], pb[i]), gam);
         zf0[zo[i]] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
         zf1[zo[i]] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
         zf2[zo[i]] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
@@ -731,13 +720,10 @@ int cols7_grid(int n_list, int qw, int ipb) {
   return 8 * per_x * ((n_list + ipb - 1) / ipb);
 }
 
-// IPB column items per block (items IPB b .. IPB b + IPB - 1 of `blocks`);
-// IPB > 1: the next item's T slice loads during the current item's transform
-template <int N, int R2, int KS, bool THR, int IPB>
+template <int N, int R2, int KS, bool THR>
 __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ imgs, const int4* __restrict__ blocks,
-                                                   int n_items, const float* __restrict__ ws,
-                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
-                                                   EncParams ep, TokenSinks sk) {
+                                                   const float* __restrict__ ws, const float2* __restrict__ tw,
+                                                   const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
   constexpr int M = N / 2;
   __shared__ ColsLds<N> L;
   __shared__ float2 post_s[2 * (M + 1)];
@@ -745,45 +731,9 @@ __global__ __launch_bounds__(256) void k_fft_cols4(const ImgDesc* __restrict__ i
   __shared__ float sbias[32];   // -(h + strip) / ci[c] per tile row h (fp32 division, FE:411-416)
   for (int i = threadIdx.x; i < 2 * (M + 1); i += 256) post_s[i] = post[i];
   for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
-#ifndef DCTAE_C4_XCD
-#define DCTAE_C4_XCD 0
-#endif
-  int gidx = blockIdx.x;
-  if (DCTAE_C4_XCD) {   // XCD-dealt item groups (as k_cols224)
-    const int n_g = (n_items + IPB - 1) / IPB, per_x = (n_g + 7) / 8;
-    gidx = (int)(blockIdx.x & 7) * per_x + (int)(blockIdx.x >> 3);
-    if (gidx >= n_g) return;
-  }
-  const int i0 = gidx * IPB;
-  if (IPB == 1) {
-    const int4 jb = blocks[i0];
-    const ImgDesc d = imgs[jb.x];
-    cols4_item<N, R2, KS, THR>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk);
-    return;
-  }
-  c4f2 nv[N / 32];
-  {
-    const int4 jb = blocks[i0];
-    const ImgDesc d = imgs[jb.x];
-    cols4_fetch<N, KS>(d, jb.y, jb.z, ws + d.ws_t, nv);
-  }
-#pragma unroll 1
-  for (int u = 0; u < IPB; ++u) {
-    const int i = i0 + u;
-    if (i >= n_items) break;
-    c4f2 cv[N / 32];
-#pragma unroll
-    for (int k = 0; k < N / 32; ++k) cv[k] = nv[k];
-    const int4 jb = blocks[i];
-    const ImgDesc d = imgs[jb.x];
-    if (u + 1 < IPB && i + 1 < n_items) {
-      const int4 jn = blocks[i + 1];
-      const ImgDesc dn = imgs[jn.x];
-      cols4_fetch<N, KS>(dn, jn.y, jn.z, ws + dn.ws_t, nv);
-    }
-    if (u > 0) __syncthreads();   // the previous item's epilogue is done with zs / sbias
-    cols4_item<N, R2, KS, THR, true>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk, cv);
-  }
+  const int4 jb = blocks[blockIdx.x];
+  const ImgDesc d = imgs[jb.x];
+  cols4_item<N, R2, KS, THR>(d, jb.y, jb.z, ws + d.ws_t, L.z, post_s, tw_s, sbias, ep, sk);
 }
 
 // ---------------------------------------------------------------------------
@@ -1054,7 +1004,7 @@ int fft_spec_id(int N, const int* radix, int npass, int P) {
 }
 
 #ifndef DCTAE_ROWS224P
-#define DCTAE_ROWS224P 0   // on after the GPU parity run; rows per wave of k_rows224p (2 or 3)
+#define DCTAE_ROWS224P 2   // rows per wave of k_rows224p (2 or 3; 0: k_fft_rows2<224>)
 #endif
 int fft_spec_rows_per_block(int spec) {
   return spec == 2 ? (DCTAE_ROWS224P ? 4 * DCTAE_ROWS224P : 4 * DCTAE_RPW224) : (spec ? 16 : 0);
@@ -1095,18 +1045,12 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
                          ws, tw, post, ep, sk);
     return;
   }
-#ifndef DCTAE_C4_IPB224
-#define DCTAE_C4_IPB224 1
-#endif
-#define DCTAE_COLS4(NN, RR, T, IPB)                                                                       \
-  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T, IPB>),                                                   \
-                     dim3(DCTAE_C4_XCD ? 8 * (((n_blocks + IPB - 1) / IPB + 7) / 8) : (n_blocks + IPB - 1) / IPB), \
-                     dim3(256), 0, s,                                                                      \
-                     imgs, blocks, n_blocks, ws, tw, post, ep, sk)
-  if (spec == 1 && thr) DCTAE_COLS4(512, 16, true, 1);
-  else if (spec == 1) DCTAE_COLS4(512, 16, false, 1);
+#define DCTAE_COLS4(NN, RR, T)                                                                                  \
+  hipLaunchKernelGGL((k_fft_cols4<NN, RR, 14, T>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, tw, post, ep, sk)
+  if (spec == 1 && thr) DCTAE_COLS4(512, 16, true);
+  else if (spec == 1) DCTAE_COLS4(512, 16, false);
 #ifndef DCTAE_COLS224
-#define DCTAE_COLS224 0   // on after the GPU parity run
+#define DCTAE_COLS224 1
 #endif
   else if (spec == 2 && DCTAE_COLS224 && thr)
     hipLaunchKernelGGL((k_cols224<true>), dim3(8 * (((n_blocks + 1) / 2 + 7) / 8)), dim3(256), 0, s, imgs, blocks,
@@ -1114,8 +1058,8 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
   else if (spec == 2 && DCTAE_COLS224)
     hipLaunchKernelGGL((k_cols224<false>), dim3(8 * (((n_blocks + 1) / 2 + 7) / 8)), dim3(256), 0, s, imgs, blocks,
                        n_blocks, ws, tw, post, ep, sk);
-  else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true, DCTAE_C4_IPB224);
-  else if (spec == 2) DCTAE_COLS4(224, 7, false, DCTAE_C4_IPB224);
+  else if (spec == 2 && thr) DCTAE_COLS4(224, 7, true);
+  else if (spec == 2) DCTAE_COLS4(224, 7, false);
 #undef DCTAE_COLS4
 }
 
