@@ -758,7 +758,15 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
                                                  EncParams ep, TokenSinks sk) {
 #pragma clang fp contract(fast)
   constexpr int N = 224, M = 112, R1 = 16, R2 = 7, B1 = 7, KS = 14;
-  constexpr int KSP = 2 * KS + 1;                 // 28 columns (two strips) + 1
+#ifndef DCTAE_C224_KSP
+#define DCTAE_C224_KSP 30
+#endif
+  // LDS row stride (28 columns + pad): ds_read/write_b32 bank = dword mod 32 per
+  // 32-lane half (4 columns x 8 lanes jj): pass 2 and the post step jj by 2 KSP
+  // and pass 1's stores by 34 KSP, conflict-free when those are 4 x odd mod 32,
+  // i.e. KSP = 2 mod 4 (30); 29 made them 2-way (PMC: 0.36 conflict share)
+  constexpr int KSP = DCTAE_C224_KSP;
+  static_assert(KSP >= 2 * KS, "28 columns");
   constexpr int ZROWS = 2 * (pad16(M - 1) + 1);   // padded complex layout, in floats per column
   static_assert(N <= ZROWS, "natural rows fit the complex layout");
   __shared__ float zs[ZROWS * KSP];
