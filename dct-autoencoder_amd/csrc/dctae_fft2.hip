@@ -375,13 +375,11 @@ __device__ __forceinline__ void cols4_fetch(const ImgDesc& d, int c, int strip, 
 
 // one column item: (image d, channel c, tile column strip); T = the image's
 // row-pass output (channel 0, row 0).  Caller: post_s / tw_s loaded, a block
-// barrier since the previous use of zs and sbias.  PRE: the item's T slice is
-// already in `pre` (cols4_fetch, issued during the previous item).
-template <int N, int R2, int KS, bool THR, bool PRE = false>
+// barrier since the previous use of zs and sbias.
+template <int N, int R2, int KS, bool THR>
 __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, const float* __restrict__ T, float* zs,
                                            const float2* post_s, const float2* tw_s, float* sbias,
-                                           const EncParams& ep, const TokenSinks& sk,
-                                           const c4f2* pre = nullptr) {
+                                           const EncParams& ep, const TokenSinks& sk) {
 #pragma clang fp contract(fast)
   constexpr int R1 = 16;
   constexpr int M = N / 2;
@@ -413,12 +411,7 @@ __device__ __forceinline__ void cols4_item(const ImgDesc& d, int c, int strip, c
   if (THR && tid < 32) sbias[tid] = __fdiv_rn(-(float)(tid + strip), ep.ci[c]);
   // ---- T slice -> LDS, natural row order
   c4f2 tv[N / 32];
-  if (PRE) {
-#pragma unroll
-    for (int k = 0; k < N / 32; ++k) tv[k] = pre[k];
-  } else {
-    cols4_fetch<N, KS>(d, c, strip, T, tv);
-  }
+  cols4_fetch<N, KS>(d, c, strip, T, tv);
   if (tid < 32 * (KS / 2)) {
     // row-major: thread (y0 = t / 7, p = t % 7) copies float2 p of rows y0 + 32k
     const int y0 = tid / (KS / 2), p = tid - y0 * (KS / 2);
