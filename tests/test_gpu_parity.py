@@ -505,11 +505,13 @@ def _ops():
     return import_module("dct_autoencoder_amd._ops")
 
 
-@pytest.mark.parametrize("shape", [(512, 512), (224, 224), (100, 300), (30, 700)])
+@pytest.mark.parametrize("shape", [(512, 512), (224, 224), (100, 300), (30, 700), (224, 98), (98, 224), (224, 322)])
 def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
     """The FFT-DCT kernels and the MFMA GEMM DCT are two evaluations of the
     same transform: tokens within 2e-6 * max|Y|, codes equal except inside the
-    guard band."""
+    guard band.  (224, 98) / (224, 322): k_cols224 with an odd column-item
+    count (the last pair repeats its item); (98, 224): k_rows224p with a
+    partial last block."""
     ops = _ops()
     x = torch.from_numpy(np.stack(rng.synth_images(31, [shape] * 2))).to(DEV)
     ((dp_f, c_f),) = fe.encode_batch(x, pn, lfq, return_raw=True)
