@@ -200,27 +200,20 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
   __shared__ Rows224pLds<RW> L;
   __shared__ float4 pc[M + 1];
   __shared__ float2 tw_s[M];
-  {
-    const float4* p4 = reinterpret_cast<const float4*>(post);
-    for (int i = threadIdx.x; i < M + 1; i += 256) {
-      const float4 ab = p4[i];   // (al.x, al.y, be.x, be.y)
-      pc[i] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
-    }
-    for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
-  }
-  __syncthreads();
+  // the wave's pixel loads are issued first: the table loads, their LDS
+  // stores and the block barrier overlap them instead of preceding them
   const int2 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
   const int tid = opaque_tid();
   const int wave = tid >> 6, lane = tid & 63;
   const int H = d.H, Kw = d.Kw;
   const int y0 = jb.y + RW * wave;
-  if (y0 >= H) return;   // wave-uniform; no block barrier follows
+  const bool live = y0 < H;   // wave-uniform; dead waves still reach the barrier
   float2(*z)[MP] = L.z[wave];
   float* zf = reinterpret_cast<float*>(&z[0][0]);
   const int64_t hw = (int64_t)H * N;
-  const float* src = rgb + d.rgb_off + (int64_t)y0 * N;   // the wave's rows are contiguous
-  const int nq = min(RW, H - y0) * N;
+  const float* src = rgb + d.rgb_off + (int64_t)(live ? y0 : 0) * N;   // the wave's rows are contiguous
+  const int nq = live ? min(RW, H - y0) * N : 0;
   float pr[PX + 1], pg[PX + 1], pb[PX + 1];
 #pragma unroll
   for (int i = 0; i < PX; ++i) {
@@ -231,6 +224,16 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
     pg[i] = src[hw + qq];
     pb[i] = src[2 * hw + qq];
   }
+  {
+    const float4* p4 = reinterpret_cast<const float4*>(post);
+    for (int i = threadIdx.x; i < M + 1; i += 256) {
+      const float4 ab = p4[i];   // (al.x, al.y, be.x, be.y)
+      pc[i] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
+    }
+    for (int i = threadIdx.x; i < M; i += 256) tw_s[i] = tw[i];
+  }
+  __syncthreads();
+  if (!live) return;   // no block barrier follows
   pr[PX] = pg[PX] = pb[PX] = 0.0f;
   // ---- IPT (util.py:70-82) on pixel pairs + Makhoul reorder into LDS.  The
   //      LDS slot of pixel q = lane + 64 i repeats with period 7 in i (448 =
