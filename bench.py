@@ -141,6 +141,54 @@ def cpu_config1(threads, reps=10, size=224):
             "reps": reps, "cores": threads, "kind": "port", "roundtrip_max_abs_err": err}
 
 
+def cpu_config_legs(threads, tables, seed=3):
+    """BASELINE.md §3's capped CPU subsets of configs 2-4 on the oracle port
+    (the reference's op sequence: FFT DCT, per-image sort, greedy packing with
+    attn_mask, PatchNorm, LFQ; decode through the reference's per-token revert
+    loop, FE:639-643), each a few seconds of host time:
+      config 2: 256 x 224^2 encode;
+      config 3: 8 x 512^2 round trip (encode, then indices_to_codes ->
+                inverse_norm -> postprocess), encode and decode timed apart;
+      config 4: the first 32 images of the GPU leg's ragged sizes (seed 7)."""
+    from oracle import ref_cpu
+    torch.set_num_threads(threads)
+    cfg, lcfg = ref_cpu.FEConfig(), ref_cpu.LFQConfig()
+    g = torch.Generator().manual_seed(seed)
+    out = {}
+
+    def enc(imgs):
+        t0 = time.perf_counter()
+        res = ref_cpu.encode(imgs, cfg, tables, lcfg, batch_size=None, build_attn_mask=True)
+        return res, time.perf_counter() - t0
+
+    imgs = [torch.rand(3, 224, 224, generator=g) for _ in range(256)]
+    _, el = enc(imgs)
+    out["config2"] = {"workload": "256 x 224x224 encode", "value": round(256 * 224 * 224 / el / 1e6, 3),
+                      "unit": "Mpix/s", "seconds": round(el, 3)}
+    imgs = [torch.rand(3, 512, 512, generator=g) for _ in range(8)]
+    res, el_e = enc(imgs)
+    t0 = time.perf_counter()
+    n_out = 0
+    for batch, idx in res:
+        y = ref_cpu.lfq_indices_to_codes(idx, lcfg)
+        batch.patches = ref_cpu.norm_inverse(tables, y, batch.patch_channels, batch.h_indices, batch.w_indices)
+        n_out += len(ref_cpu.postprocess(batch, cfg, per_token_loop=True))
+    el_d = time.perf_counter() - t0
+    assert n_out == 8
+    pix = 8 * 512 * 512
+    out["config3"] = {"workload": "8 x 512x512 round trip (encode + decode through the per-token revert loop)",
+                      "value": round(pix / (el_e + el_d) / 1e6, 3), "unit": "Mpix/s (round trip)",
+                      "encode_mpix_s": round(pix / el_e / 1e6, 3), "decode_mpix_s": round(pix / el_d / 1e6, 3),
+                      "seconds": round(el_e + el_d, 3)}
+    hw = np.random.default_rng(7).integers(14, 1025, size=(1024, 2))[:32]
+    imgs = [torch.rand(3, int(h), int(w), generator=g) for h, w in hw]
+    _, el = enc(imgs)
+    out["config4"] = {"workload": "32 ragged images, the GPU leg's first 32 sizes (H, W) ~ U{14..1024}^2 seed 7, "
+                                  "encode", "value": round(int((hw[:, 0] * hw[:, 1]).sum()) / el / 1e6, 3),
+                      "unit": "Mpix/s", "seconds": round(el, 3)}
+    return out
+
+
 def stats_fit_leg(pkg, fe, dev, rank, world, dist, steps, n_img=8, size=512):
     """Config 5: one data-parallel PatchNorm fit step per
     iteration — each rank's batch statistics of its own shard, exchanged over
@@ -595,6 +643,16 @@ def main():
                                     torch.from_numpy(tabs["b"]))
         cpu = cpu_baseline(H, args.cpu_seconds, tables, threads)
         cpu["config1"] = cpu_config1(threads)
+        cpu["configs"] = cpu_config_legs(threads, tables)
+        # the GPU figure of each config beside its CPU sample (same units)
+        oc = configs if isinstance(configs, dict) else {}
+        gpu = {"config2": (oc.get("config2") or {}).get("value"), "config4": (oc.get("config4") or {}).get("value")}
+        if decode and decode.get("ms_per_step"):
+            gpu["config3"] = round(B * H * H / ((ms_step + decode["ms_per_step"]) / 1e3) / 1e6, 1)
+        for k, v in gpu.items():
+            if v and k in cpu["configs"]:
+                cpu["configs"][k]["gpu_value"] = v
+                cpu["configs"][k]["gpu_over_cpu"] = round(v / cpu["configs"][k]["value"], 1)
 
     if rank == 0:
         line = {

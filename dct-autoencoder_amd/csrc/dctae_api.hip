@@ -84,7 +84,8 @@ struct dctae_ctx {
   // selectable here so the parity tests cover it on the headline shape)
   int rows_kernel = 4;
   // 512 x 512 images at 32 x 32 kept tiles: 1 = the row pass writes the band
-  // layout T'[c][y/4][kx][y%4] and the columns run k_cols512b (16-byte loads,
+  // layout (band16 T'[c][y/16][kx][16 rows], t4_index in dctae_rows512.h) and
+  // the columns run k_cols512b (16-byte loads,
   // DESIGN.md section 4); 0 = row-major T and k_fft_cols7
   int cols512b = 1;
   int sort_overlap = 0;
@@ -96,6 +97,8 @@ struct dctae_ctx {
   int sort_kernel = 2;
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
+  // decode columns with k_idct_rows512: 2 = k_idct_cols512b (band-layout U, default), 1 = k_idct_cols512
+  int dec_cols_kernel = 2;
   int n_cu = 256;
   // DCT GEMMs (lengths without a Makhoul plan, dctae_dct2, decode): 1 = the
   // split-bf16 MFMA kernel k_gemm_x3 (fp32 accuracy, 0.375 of the MFMA time),
@@ -879,6 +882,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "sort_overlap") ctx->sort_overlap = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
+  else if (k == "dec_cols_kernel" && (value == 1 || value == 2)) ctx->dec_cols_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
@@ -1481,6 +1485,20 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   // first half's sort / pack on the side stream while the second half's
   // columns run (the sort is latency-bound, the column kernel issue-bound)
   int sorted0 = 0;   // images [0, sorted0) packed on the side stream
+  // once work is queued on the side stream, the caller's stream waits for it on
+  // every exit (error returns included), so the next call's order_after_previous
+  // covers it before the workspace is reused
+  struct SideJoin {
+    hipStream_t s = nullptr, side = nullptr;
+    hipEvent_t e = nullptr;
+    bool armed = false;
+    void join() {
+      if (!armed) return;
+      armed = false;
+      if (hipEventRecord(e, side) != hipSuccess || hipStreamWaitEvent(s, e, 0) != hipSuccess) hipStreamSynchronize(side);
+    }
+    ~SideJoin() { join(); }
+  } side_join;
   const bool split = full && !proj_w && ctx->sort_overlap && E.jobs.size() == 1 && E.n_img >= 64 &&
                      E.jobs[0].n_pb == E.n_img && E.jobs[0].i0 == 0;
   if (split && !ctx->side) {
@@ -1504,8 +1522,11 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     }
     HIPCHK(ctx, hipEventRecord(ctx->side_in, s));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+    side_join.s = s;
+    side_join.side = ctx->side;
+    side_join.e = ctx->side_out;
+    side_join.armed = true;
     launch_sort_pack(all_d, h, next_pow2(E.max_T), eps, sk, ps, ctx->side, ctx->sort_kernel, E.max_T);
-    HIPCHK(ctx, hipEventRecord(ctx->side_out, ctx->side));
     {
       Timer t(ctx, s, "fft_cols");
       launch_cols512b(dd, list + h, j.n_pb - h, ctx->ws, ctx->fft_tab + j.tw_off_c[1], ctx->fft_tab + j.post_off_c[1],
@@ -1524,7 +1545,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     launch_sort_pack(all_d + sorted0, E.n_img - sorted0, next_pow2(E.max_T), eps, sk, ps, s, ctx->sort_kernel,
                      E.max_T);
   }
-  if (sorted0) HIPCHK(ctx, hipStreamWaitEvent(s, ctx->side_out, 0));   // every output complete on the caller's stream
+  side_join.join();   // every output complete on the caller's stream
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
   return 0;
@@ -2162,14 +2183,21 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
     Timer t(ctx, s, "dec_map");
     launch_dec_map((int64_t)n_rows * S, dd, a, map, s);
   }
+  // 32 kept tile columns on the default row kernel: U in the band layout
+  // (k_idct_cols512b); otherwise row-major U (k_idct_cols512)
+  const bool rows512 = ctx->dec_rows_kernel == 3 && D[0].qw == 32;
+  const bool band = rows512 && ctx->dec_cols_kernel == 2;
   {
     Timer t(ctx, s, "idct_cols");
-    launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
+    if (band)
+      launch_idct_cols512b(dd, n_img, ctx->ws, map, tw, pre, a, s);
+    else
+      launch_idct_cols512(dd, n_img, D[0].qw, ctx->ws, map, tw, pre, a, s);
   }
   {
     Timer t(ctx, s, "idct_rows");
-    if (ctx->dec_rows_kernel == 3 && D[0].qw == 32)
-      launch_idct_rows512(dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
+    if (rows512)
+      launch_idct_rows512(band, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
     else
       launch_idct_rows_spec(1, dd, (const int2*)(pd + rb_off), (int)rb.size(), ctx->ws, rgb, tw, pre, ctx->cm, s);
   }
@@ -2226,6 +2254,9 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
     wsf += 3ll * d.H * d.W;
     max_hw = std::max<int64_t>(max_hw, (int64_t)d.H * d.W);
   }
+  // the GEMM path's slot map (k_dec_map: the later packed slot wins at a duplicate place, FE:639-643)
+  const int64_t gmap_off = (wsf + 63) & ~63ll;
+  const int64_t gmap_n = (int64_t)n_img * 3 * cfg->max_patch_h * cfg->max_patch_w;
   // FFT path (dctae_idct.hip): every image 512 x 512 on the specialised plan, recommended LFQ
   bool fftdec = ctx->fft_decode && P == 14 && (!codes || (lfq->codebook_dim == 14 && lfq->num_codebooks == 14));
   for (int i = 0; fftdec && i < n_img; ++i)
@@ -2234,7 +2265,7 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   if (fftdec) fftdec = fft_plan_for(ctx, 512, P, &fpl) == 0 && fpl.spec == 1;
   if (fftdec) return decode_fft(ctx, cfg, D, fpl, n_rows, img_lut, lut_w, ids, key_pad, pos, ch, norm, lfq, codes,
                                 patches, rgb, s);
-  if ((rc = ensure_ws(ctx, (size_t)wsf * 4, 256))) return rc;
+  if ((rc = ensure_ws(ctx, (size_t)(gmap_off + gmap_n) * 4, 256))) return rc;
   const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
   std::vector<GemmProblem> probs;
   std::vector<TileRef> t1, t2;
@@ -2292,9 +2323,15 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   a.maxph = cfg->max_patch_h;
   a.maxpw = cfg->max_patch_w;
   a.err = ctx->err_dev;
+  int32_t* gmap = (int32_t*)(ctx->ws + gmap_off);
+  HIPCHK(ctx, hipMemsetAsync(gmap, 0xFF, (size_t)gmap_n * 4, s));
+  {
+    Timer t(ctx, s, "dec_map");
+    launch_dec_map((int64_t)n_rows * S, dd, a, gmap, s);
+  }
   {
     Timer t(ctx, s, "scatter_tokens");
-    launch_scatter_tokens((int64_t)n_rows * S, dd, ctx->ws, a, s);
+    launch_scatter_tokens((int64_t)n_rows * S, dd, ctx->ws, a, gmap, s);
   }
   {
     Timer t(ctx, s, "idct_cols");

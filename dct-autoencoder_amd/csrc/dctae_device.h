@@ -4,6 +4,15 @@
 
 namespace dctae {
 
+// Lanes of one wave handing data to each other through LDS: orders the
+// earlier phase's LDS stores before the later phase's loads for the compiler
+// (the hardware runs the wave's instructions in order).  Costs no instructions.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 

@@ -269,6 +269,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
       }
     }
   }
+  wave_lds_sync();   // the reorder stores of other lanes
   // ---- pass 1: radix 16, Ns = 1; in place, one butterfly per lane (63 of 64)
   if (lane < CR * B1) {
     const int c = lane / B1, j = lane - c * B1;
@@ -282,6 +283,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
 #pragma unroll
     for (int r = 0; r < R1; ++r) z[c][pad16(j * R1 + r)] = make_float2(v[r].x, v[r].y);
   }
+  wave_lds_sync();
   // ---- pass 2: radix 7, Ns = 16; twiddle W_M^{r j}; 144 butterflies in 3 rounds
 #pragma unroll
   for (int t = 0; t < (CR * B2 + 63) / 64; ++t) {
@@ -304,6 +306,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
       for (int r = 0; r < R2; ++r) z[c][pad16(j + r * R1)] = make_float2(v[r].x, v[r].y);
     }
   }
+  wave_lds_sync();
   // ---- Makhoul post -> T: (X[k], X[N - k]) = makhoul_pair(Z[k], Z[M - k]), k = lane + 64 i
   int oa[KI], ob[KI];
 #pragma unroll

@@ -18,6 +18,7 @@
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
 #include "dctae_launch.h"
+#include "dctae_rows512.h"
 
 namespace dctae {
 
@@ -108,20 +109,19 @@ struct IColsLds {
   };
 };
 
-// one (image, channel, tile column) of the column pass; vt[r][p] = the
-// (code bit 1, code bit 0) values of this thread's tile row r, element p
-// (inverse PatchNorm of +-scale, image-independent: loaded once per block)
-__device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c, int strip, float* __restrict__ ws,
-                                               const int32_t* __restrict__ map, const DecodeArgs& a,
-                                               const float2 (&vt)[2][14], IColsLds& L, const float4* pre_s,
-                                               const float2* tw_s) {
-#pragma clang fp contract(fast)
-  constexpr int N = 512, M = 256, KS = 14, S16 = 257, PP = KS * KS;
+// tokens of one (image, channel, tile column) -> X[ky][col] in LDS (natural
+// rows through xrow, zero rows for tiles absent from the batch): thread
+// (g16, jl) expands tile rows h = g16 + 16 r, element row jl, from the
+// token's code (LFQ bit -> +-scale -> inverse PatchNorm: vt) or its patch.
+// zero_tail: also zero rows 448 .. 511 (read by k_idct_cols512 only).
+__device__ __forceinline__ void icols_fill_x(int img, const ImgDesc& d, int c, int strip,
+                                             const int32_t* __restrict__ map, const DecodeArgs& a,
+                                             const float2 (&vt)[2][14], float* x, bool zero_tail) {
+  constexpr int N = 512, KS = 14, PP = KS * KS;
   const int tid = itid();
-  // ---- 1. tokens -> X rows 14 h + jl (tile h = g16 + 16 r)
 #if defined(DCTAE_PROFILING) && defined(DCTAE_IC_ABL)
   if (DCTAE_IC_ABL & 1) {   // profiling ablation: no token loads / expansion (wrong output)
-    for (int e = tid; e < N * KS; e += 256) L.x[e] = 0.001f * (e & 63);
+    for (int e = tid; e < N * KS; e += 256) x[e] = 0.001f * (e & 63);
   } else
 #endif
   {
@@ -150,7 +150,7 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
     for (int r = 0; r < 2; ++r) {
       const int h = g16 + 16 * r;
       if (jl < KS) {
-        f2v* xr = reinterpret_cast<f2v*>(L.x + xrow(KS * h + jl) * KS);
+        f2v* xr = reinterpret_cast<f2v*>(x + xrow(KS * h + jl) * KS);
 #pragma unroll
         for (int p = 0; p < KS / 2; ++p) {
           float v0, v1;
@@ -171,8 +171,46 @@ __device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c,
       }
     }
     // rows 448 .. 511 (beyond Kh = 448 when qh = 32): zero
-    for (int e = tid; e < (N - KS * 32) * KS; e += 256) L.x[KS * 32 * KS + e] = 0.0f;
+    if (zero_tail)
+      for (int e = tid; e < (N - KS * 32) * KS; e += 256) x[KS * 32 * KS + e] = 0.0f;
   }
+}
+
+// image-independent values of this thread's two tile rows (h = g16 + 16 r,
+// element row jl) of a (channel, strip) item: inverse PatchNorm of y = +scale
+// (code bit 1, .x) and y = -scale (bit 0, .y), lfq.py:105-134 -> patchnorm.py:167-177
+__device__ __forceinline__ void icols_vt(int c, int strip, const DecodeArgs& a, float2 (&vt)[2][14]) {
+  constexpr int KS = 14, PP = KS * KS;
+  const int tid = itid();
+  const int g16 = tid >> 4, jl = tid & 15;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int h = min(g16 + 16 * r, a.maxph - 1);
+    const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + (jl < KS ? jl : 0) * KS;
+    if (a.use_codes) {
+      const float yp = __fsub_rn(__fmul_rn(1.0f, a.scale * 2.0f), a.scale);
+      const float yn = __fsub_rn(__fmul_rn(0.0f, a.scale * 2.0f), a.scale);
+#pragma unroll
+      for (int p = 0; p < KS; ++p) {
+        const float m = a.median[tab + p], bb = a.b[tab + p];
+        vt[r][p] = make_float2(pn_inverse(yp, m, bb, a.eps), pn_inverse(yn, m, bb, a.eps));
+      }
+    }
+  }
+}
+
+// one (image, channel, tile column) of the column pass; vt[r][p] = the
+// (code bit 1, code bit 0) values of this thread's tile row r, element p
+// (inverse PatchNorm of +-scale, image-independent: loaded once per block)
+__device__ __forceinline__ void idct_col_image(int img, const ImgDesc& d, int c, int strip, float* __restrict__ ws,
+                                               const int32_t* __restrict__ map, const DecodeArgs& a,
+                                               const float2 (&vt)[2][14], IColsLds& L, const float4* pre_s,
+                                               const float2* tw_s) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14, S16 = 257;
+  const int tid = itid();
+  // ---- 1. tokens -> X rows 14 h + jl (tile h = g16 + 16 r)
+  icols_fill_x(img, d, c, strip, map, a, vt, L.x, true);
   __syncthreads();
   // lanes of columns 14 / 15 (tid >= 224) redo column 13: same reads, same
   // values, same stores (no divergent branches)
@@ -259,7 +297,7 @@ __global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict_
                                                       float* __restrict__ ws, const int32_t* __restrict__ map,
                                                       const float2* __restrict__ tw, const float4* __restrict__ pre,
                                                       DecodeArgs a) {
-  constexpr int M = 256, KS = 14, PP = KS * KS;
+  constexpr int M = 256, KS = 14;
   __shared__ IColsLds L;
   __shared__ float4 pre_s[M];
   __shared__ float2 tw_s[M];
@@ -273,27 +311,8 @@ __global__ __launch_bounds__(256) void k_idct_cols512(const ImgDesc* __restrict_
     pre_s[i] = pre[i];
     tw_s[i] = tw[i];
   }
-  // image-independent values of this thread's two tile rows: inverse
-  // PatchNorm of y = +scale (code bit 1) and y = -scale (bit 0)
   float2 vt[2][KS];
-  {
-    const int tid = itid();
-    const int g16 = tid >> 4, jl = tid & 15;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int h = min(g16 + 16 * r, a.maxph - 1);
-      const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + (jl < KS ? jl : 0) * KS;
-      if (a.use_codes) {
-        const float yp = __fsub_rn(__fmul_rn(1.0f, a.scale * 2.0f), a.scale);   // lfq.py:105-134
-        const float yn = __fsub_rn(__fmul_rn(0.0f, a.scale * 2.0f), a.scale);
-#pragma unroll
-        for (int p = 0; p < KS; ++p) {
-          const float m = a.median[tab + p], bb = a.b[tab + p];
-          vt[r][p] = make_float2(pn_inverse(yp, m, bb, a.eps), pn_inverse(yn, m, bb, a.eps));   // patchnorm.py:167-177
-        }
-      }
-    }
-  }
+  icols_vt(c, strip, a, vt);
 #pragma unroll
   for (int u = 0; u < IPB; ++u) {
     const int img = i0 + u;
@@ -442,6 +461,110 @@ __global__ __launch_bounds__(256) void k_idct_rows2(const ImgDesc* __restrict__ 
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_idct_cols512b: the column DCT-III of 512 x 512 images at 32 x 32 kept
+// tiles with the encode's register-resident FFT (fft256_group, dctae_rows512.h)
+// and U written straight from registers in the band layout U'[c][y / 4][kx][4]
+// (u4_index: band16 by default, rows 4 m .. 4 m + 3 of one column = one
+// float4, natural order), read by k_idct_rows512<448, true>.  Block = (channel,
+// tile strip) x IPB images, one 16-lane group per column (groups 14 / 15
+// repeat column 13 and store the same values), XCD-dealt like k_cols512b.
+// Per image: tokens -> X (LDS, icols_fill_x) | barrier | lane j of column col
+// builds conj Z[j + 16 r] (its pass-1 inputs) from X | barrier (X aliases the
+// transpose regions) | fft256_group with the identity butterfly order: lane j
+// holds W[j + 16 i] and the mirror lane W[255 - j - 16 i], so rows 4 m + (0,
+// 1, 2, 3) of m = j + 16 i are (Re W[m], -Im W[255 - m], -Im W[m], Re W[255 - m])
+// (dctae_idct.hip header) -- eight 16-byte stores per lane.  Three block
+// barriers per image against k_idct_cols512's six, no LDS round trip for U.
+// ---------------------------------------------------------------------------
+struct ICols512bLds {
+  union {
+    float x[448 * 14];            // Y[ky][col] of the strip, rows through xrow (25,088 B)
+    cf xch[16][kXchStridePk];     // per group transpose region (34,816 B)
+  } u;
+  float2 tw2[16][16];
+  float4 pre[256];                // (conj a_k, conj b_k)
+};                                // 40,960 B: 4 blocks per CU
+
+#ifndef DCTAE_IC5B_WPE
+#define DCTAE_IC5B_WPE 0
+#endif
+template <int IPB>
+__global__ __launch_bounds__(256)
+#if DCTAE_IC5B_WPE
+__attribute__((amdgpu_waves_per_eu(DCTAE_IC5B_WPE)))
+#endif
+void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
+                                                       float* __restrict__ ws, const int32_t* __restrict__ map,
+                                                       const float2* __restrict__ tw, const float4* __restrict__ pre,
+                                                       DecodeArgs a) {
+#pragma clang fp contract(fast)
+  constexpr int M = 256, KS = 14, KW = 448, per_x = 12;   // 96 items = 3 channels x 32 strips, 12 per XCD lane
+  constexpr int ustep = 16 * KW * 16;   // bytes between band4 = m and m + 16 (both layouts)
+  __shared__ ICols512bLds L;
+  const int b = blockIdx.x, slot = b >> 3;
+  const int t = (b & 7) * per_x + slot % per_x, i0 = (slot / per_x) * IPB;
+  if (i0 >= n_img) return;
+  const int c = t >> 5, strip = t & 31;
+  const int tid = itid();
+  L.tw2[tid >> 4][tid & 15] = tw[(tid >> 4) * (tid & 15)];
+  L.pre[tid] = pre[tid];
+  float2 vt[2][KS];
+  icols_vt(c, strip, a, vt);
+  const int G = tid >> 4, j = tid & 15;
+  const int col = min(G, KS - 1);
+  const int uo = u4_index(j, KS * strip + col) * 16;   // band4 = j + 16 i at + i * ustep
+#pragma unroll
+  for (int u = 0; u < IPB; ++u) {
+    const int img = i0 + u;
+    if (img >= n_img) break;   // block-uniform
+    const ImgDesc d = imgs[img];
+    __syncthreads();   // tables (u = 0) / the previous image's transposes (x aliases xch)
+    icols_fill_x(img, d, c, strip, map, a, vt, L.u.x, false);
+    __syncthreads();
+    // conj Z_k, k = j + 16 i (Ys[M + k] = 0 for i >= 12, Ys[N - k] = 0 for k <= 64)
+    cf v[16];
+    {
+      const float* xc = L.u.x + col;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k = j + 16 * i;
+        const float* pk = xc + xrow(k) * KS;
+        const float* pm = xc + xrow(M - k) * KS;   // k = 0: row M
+        float yk = pk[0];
+        if (i == 0) yk = j == 0 ? yk * 1.41421356237309515f : yk;
+        const float ymk2 = pm[0];
+        const float ymk = i < 12 ? pk[M * KS] : 0.0f;   // xrow(M + y) = M + xrow(y)
+        float ynk = 0.0f;
+        if (i >= 4) {
+          ynk = pm[M * KS];                              // row N - k (i = 4, j = 0: row 448, dropped)
+          if (i == 4) ynk = j == 0 ? 0.0f : ynk;
+        }
+        v[i] = pre_z(yk, ynk, ymk, ymk2, L.pre[k]);
+      }
+    }
+    __syncthreads();   // every group's X reads before the transposes
+    fft256_group(v, L.u.xch[G], j, j, L.tw2);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws + d.ws_t + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
+                                                        0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float px = mirror16(v[15 - i].x), py = mirror16(v[15 - i].y);
+      __builtin_amdgcn_raw_buffer_store_b128(
+          (v4u){__float_as_uint(v[i].x), __float_as_uint(-py), __float_as_uint(-v[i].y), __float_as_uint(px)}, rsrc,
+          uo, i * ustep, 0);
+    }
+  }
+}
+
+void launch_idct_cols512b(const ImgDesc* imgs, int n_img, float* ws, const int32_t* map, const float2* tw,
+                          const float4* pre, const DecodeArgs& a, hipStream_t s) {
+  constexpr int IPB = 2;
+  const int grid = 8 * 12 * ((n_img + IPB - 1) / IPB);
+  if (n_img > 0)
+    hipLaunchKernelGGL((k_idct_cols512b<IPB>), dim3(grid), dim3(256), 0, s, imgs, n_img, ws, map, tw, pre, a);
 }
 
 void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, const int32_t* map, const float2* tw,

@@ -20,6 +20,7 @@
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
 #include "dctae_launch.h"
+#include "dctae_rows512.h"
 
 namespace dctae {
 
@@ -42,7 +43,10 @@ struct IRows512Lds {
 
 }  // namespace
 
-template <int KW>
+// BAND: U in the band layout U'[c][y / 4][kx][4] of k_idct_cols512b (element
+// (y, kx) at u4_index(y / 4, kx) * 4 + y % 4); otherwise row-major
+// U[c][y][kx] (k_idct_cols512)
+template <int KW, bool BAND>
 __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                       const float* __restrict__ ws, float* __restrict__ rgb,
                                                       const float2* __restrict__ tw, const float4* __restrict__ pre,
@@ -65,16 +69,40 @@ __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict_
   const int H = d.H;
   const int yl = min(y, H - 1);   // rows past H compute a duplicate and store nothing
   const int64_t cstride = (int64_t)H * KW;
-  const float* src = ws + d.ws_t + (int64_t)yl * KW + j;
-
   // ---- loads: A[c][r] = Ys[j + 16 r], B[c][r] = Ys[256 + j + 16 r] (r < NB)
   float A[3][16], B[3][NB];
+  if constexpr (BAND) {
+    // the wave's four rows are one band4 of U': lane (g, j) loads the float4
+    // (rows 4 bnd .. + 3) of column kx = j + 16 (4 q + g); the 4 x 4 cross-row
+    // transpose (xpose4_rows) then leaves row g's values of the columns
+    // j + 16 (4 q + k), k = 0..3, in the lane (1 KB per wave load at layout 0)
+    static_assert(NB % 4 == 0, "B in whole transposes");
+    const int bnd = (jb.y >> 2) + wv;
+    const float* ub = ws + d.ws_t;
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < 3; ++c) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) A[c][r] = src[c * cstride + 16 * r];
+      for (int q = 0; q < 4 + NB / 4; ++q) {
+        const int kx = j + 16 * (4 * q + g);   // q >= 4: B[4 (q - 4) + k] = Ys[M + j + 16 (4 (q - 4) + k)]
+        const float4 f = *reinterpret_cast<const float4*>(ub + c * cstride + (int64_t)u4_index(bnd, kx) * 4);
+        float r4[4] = {f.x, f.y, f.z, f.w};
+        xpose4_rows(r4);
 #pragma unroll
-    for (int r = 0; r < NB; ++r) B[c][r] = src[c * cstride + M + 16 * r];
+        for (int k = 0; k < 4; ++k) {
+          if (q < 4) A[c][4 * q + k] = r4[k];
+          else B[c][4 * (q - 4) + k] = r4[k];
+        }
+      }
+    }
+  } else {
+    const float* src = ws + d.ws_t + (int64_t)yl * KW + j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) A[c][r] = src[c * cstride + 16 * r];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) B[c][r] = src[c * cstride + M + 16 * r];
+    }
   }
   __syncthreads();   // tables
 
@@ -181,10 +209,14 @@ __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict_
   }
 }
 
-void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
+void launch_idct_rows512(bool band, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
                          const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s) {
   if (n_blocks <= 0) return;
-  hipLaunchKernelGGL(k_idct_rows512<448>, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre, cm);
+  if (band)
+    hipLaunchKernelGGL((k_idct_rows512<448, true>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre, cm);
+  else
+    hipLaunchKernelGGL((k_idct_rows512<448, false>), dim3(n_blocks), dim3(256), 0, s, imgs, blocks, ws, rgb, tw, pre,
+                       cm);
 }
 
 }  // namespace dctae

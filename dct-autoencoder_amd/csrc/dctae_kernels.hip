@@ -849,8 +849,12 @@ void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float 
 // ---------------------------------------------------------------------------
 
 
+// Two tokens at one image place (c, h, w): FE:639-643 assigns them in packed
+// order, so the later slot wins.  map (k_dec_map, atomicMax) holds that slot
+// per place; only its elements are stored (plain stores of every duplicate
+// would race and make the result depend on the schedule).
 __global__ void k_scatter_tokens(int64_t n_tok, const ImgDesc* __restrict__ imgs, float* __restrict__ ws,
-                                 DecodeArgs a) {
+                                 DecodeArgs a, const int32_t* __restrict__ map) {
   const int PP = a.P * a.P;
   const int64_t total = n_tok * PP;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -866,6 +870,7 @@ __global__ void k_scatter_tokens(int64_t n_tok, const ImgDesc* __restrict__ imgs
     const ImgDesc d = imgs[im];
     const int64_t c = a.ch[t], h = a.pos[2 * t], w = a.pos[2 * t + 1];
     if (c < 0 || c >= 3 || h < 0 || h >= d.qh || w < 0 || w >= d.qw) { atomicOr(a.err, 4); continue; }
+    if (map[(((int64_t)im * 3 + c) * a.maxpw + w) * a.maxph + h] != (int32_t)t) continue;   // a later slot wins
     float v;
     if (a.use_codes) {
       const int cbi = q / a.cb_dim, dd = q % a.cb_dim;
@@ -882,11 +887,12 @@ __global__ void k_scatter_tokens(int64_t n_tok, const ImgDesc* __restrict__ imgs
   }
 }
 
-void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s) {
+void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, const int32_t* map,
+                           hipStream_t s) {
   int64_t total = n_tok * a.P * a.P;
   int gx = (int)std::min<int64_t>((total + 255) / 256, 16384);
   if (gx <= 0) return;
-  hipLaunchKernelGGL(k_scatter_tokens, dim3(gx), dim3(256), 0, s, n_tok, imgs, ws, a);
+  hipLaunchKernelGGL(k_scatter_tokens, dim3(gx), dim3(256), 0, s, n_tok, imgs, ws, a, map);
 }
 
 }  // namespace dctae

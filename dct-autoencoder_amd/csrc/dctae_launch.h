@@ -58,7 +58,8 @@ void launch_vq_codebook(const double* acc, float* bm, float* bv, int32_t* init, 
 void launch_vq_assign(const float* xp, int64_t nv, int heads, const float* et, const float* y2, int C, float* xq,
                       int64_t* ind, hipStream_t s);
 void launch_vq_codes(const int64_t* ind, int64_t nv, const float* embed, int C, float* out, int* err, hipStream_t s);
-void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, hipStream_t s);
+void launch_scatter_tokens(int64_t n_tok, const ImgDesc* imgs, float* ws, const DecodeArgs& a, const int32_t* map,
+                           hipStream_t s);
 
 // PatchNorm training statistics (dctae_stats.hip)
 void launch_stats_lists(const int64_t* ch, const int64_t* pos, const uint8_t* key_pad, int64_t n_tok, int C, int mh,
@@ -90,12 +91,14 @@ void launch_fft_cols_spec(int spec, const ImgDesc* imgs, const int4* blocks, int
 
 // decode on the FFT path (dctae_idct.hip)
 void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int32_t* map, hipStream_t s);
+void launch_idct_cols512b(const ImgDesc* imgs, int n_img, float* ws, const int32_t* map, const float2* tw,
+                          const float4* pre, const DecodeArgs& a, hipStream_t s);
 void launch_idct_cols512(const ImgDesc* imgs, int n_img, int qw, float* ws, const int32_t* map, const float2* tw,
                          const float4* pre, const DecodeArgs& a, hipStream_t s);
 void launch_idct_rows_spec(int spec, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws,
                            float* rgb, const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 
-void launch_idct_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
+void launch_idct_rows512(bool band, const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* ws, float* rgb,
                          const float2* tw, const float4* pre, const ColorMats& cm, hipStream_t s);
 void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
                     const float2* tw, const float2* post, const ColorMats& cm, hipStream_t s);

@@ -56,6 +56,21 @@ __device__ __forceinline__ int t4_index(int band4, int kx) {
 #endif
 }
 
+// The decode's band-layout U' (k_idct_cols512b -> k_idct_rows512<448, true>),
+// natural row order in the float4: the same two layouts, chosen apart
+// (DCTAE_ULAYOUT 2 = band16 [y / 16][kx][16], 0 = [y / 4][kx][4]).
+#ifndef DCTAE_ULAYOUT
+#define DCTAE_ULAYOUT 2
+#endif
+static_assert(DCTAE_ULAYOUT == 0 || DCTAE_ULAYOUT == 2, "U' layouts: 0 or 2");
+__device__ __forceinline__ int u4_index(int band4, int kx) {
+#if DCTAE_ULAYOUT == 0
+  return band4 * 448 + kx;
+#else
+  return ((band4 >> 2) * 448 + kx) * 4 + (band4 & 3);
+#endif
+}
+
 __device__ __forceinline__ float mirror16(float x) {   // lane l <- lane 15 - l of its 16-lane row
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xf, 0xf, false));
 }

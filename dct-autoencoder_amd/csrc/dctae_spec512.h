@@ -397,7 +397,8 @@ __device__ __forceinline__ void cols7_compute(const ImgDesc& d, int c, int strip
 
 // ---------------------------------------------------------------------------
 // k_cols512b (N = 512 columns of 512 x 512 images whose row pass wrote the band
-// layout T'[c][y / 4][kx][y % 4], dctae_rows512.h): the column transform runs
+// layout: band16 T'[c][y / 16][kx][16 rows] by default, t4_index in
+// dctae_rows512.h; float4 = 4 rows of one column): the column transform runs
 // exactly like the row kernel's, one 16-lane group per column.  Block = 4 waves
 // = 16 groups over the 14 columns of one tile strip (groups 14 / 15 repeat
 // column 13 and store the same values to the same slots).

@@ -417,11 +417,12 @@ def test_large_ragged_vs_oracle(fe, pn, lfq, ref_tables, sizes, bluestein):
 
 
 @pytest.mark.parametrize("B,H", [(1024, 512), (256, 224)])
-def test_batch_encoder_matches_encode_batch(pkg, fe, pn, lfq, B, H):
+def test_batch_encoder_matches_encode_batch(pkg, fe, pn, lfq, ref_tables, B, H):
     """Full bench geometry (config 3: 1024 x 512^2; config 2: 256 x 224^2):
     the pre-planned BatchEncoder equals encode_batch on a sampled subset of the
     same images, bit for bit (codes, positions, channels; one image per row
-    at 512^2, four at 224^2)."""
+    at 512^2, four at 224^2), and its codes of 3 (512^2) / 4 (224^2) images,
+    the last one included, equal the oracle's outside the guard band."""
     from importlib import import_module
     fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
     x = _ops().synth_images(B, H, H, seed=1234, first_index=0, device=DEV)
@@ -441,6 +442,23 @@ def test_batch_encoder_matches_encode_batch(pkg, fe, pn, lfq, B, H):
         assert torch.equal(pos_b[r, c0:c0 + k], dp.patch_positions[rr, cc:cc + k])
         assert torch.equal(ch_b[r, c0:c0 + k], dp.patch_channels[rr, cc:cc + k])
         assert torch.all(ids_b[r, c0:c0 + k] == pl.local_id[i])
+    # and straight against the oracle: images of the full-grid launch (the first,
+    # two inside, the LAST: XCD dealing and the last partial block included);
+    # the guard band's d is the coefficient difference of the same kernels on
+    # that image (encode_batch with raw tokens, bit-equal codes checked above)
+    pick = [0, 1, B // 2 + 3, B - 1] if B < 1024 else [0, B // 2 + 3, B - 1]
+    ((dp_r, codes_r),) = fe.encode_batch([x[i] for i in pick], pn, lfq, return_raw=True)
+    flips = n = 0
+    for m, i in enumerate(pick):
+        rr, cc = _slot_of(dp_r, m)
+        r, c0 = pl.row[i], pl.col[i]
+        assert torch.equal(codes_b[r, c0:c0 + k], codes_r[rr, cc:cc + k])
+        f, t = _check_image_vs_oracle(dp_r.patches[rr, cc:cc + k].cpu(), codes_b[r, c0:c0 + k].cpu(),
+                                      pos_b[r, c0:c0 + k].cpu(), ch_b[r, c0:c0 + k].cpu(), x[i].cpu().numpy(),
+                                      ref_tables)
+        flips, n = flips + f, n + t
+    print(f"[BatchEncoder {B} x {H}^2 vs oracle, images {pick}] mismatches inside the guard band: {flips} / {n}")
+    assert flips <= max(2, n // 10000)
 
 
 def _slot_of(dp, n):
@@ -535,6 +553,15 @@ def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
         assert d <= 2e-6 * ymax, (d, ymax)
         mism = (c_f.cpu()[r, fj] != c_g.cpu()[r, gj]).sum().item()
         assert mism <= max(2, fj.numel() * 14 // 10000), mism
+
+
+@pytest.mark.parametrize("shape", [(224, 98), (98, 224), (224, 322), (322, 224)])
+def test_224_kernels_odd_shapes_vs_oracle(fe, pn, lfq, ref_tables, shape):
+    """Config 2's kernels (k_rows224p for 224-wide rows, k_cols224 for
+    224-high columns) on shapes with an odd column-item count (224 x 98,
+    224 x 322) or a partial last row block (98 x 224, 322 x 224): tokens and
+    codes straight against the oracle (not the GEMM path)."""
+    _encode_vs_oracle(fe, pn, lfq, ref_tables, rng.synth_images(43, [shape] * 3), CFG, f"224 kernels {shape}")
 
 
 @pytest.mark.parametrize("shape", [(333, 517), (1021, 997), (97, 1000), (1000, 97), (30, 997), (997, 30)])
@@ -638,15 +665,22 @@ def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
         assert (c_s.cpu()[r, sj] != c_g.cpu()[r, gj]).sum().item() <= 4
 
 
-def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables):
+@pytest.mark.parametrize("dec_cols", [2, 1])
+def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables, dec_cols):
     """Config 3 decode (codes -> indices_to_codes -> inverse_norm -> revert ->
-    IDCT -> RGB) of 512^2 images on the FFT path (dctae_idct.hip) against the
-    oracle's decode of the same codes (<= 1e-5 x image range) and against the
-    MFMA GEMM decode (two fp32 evaluations of the same transform)."""
+    IDCT -> RGB) of 512^2 images on the FFT path (dctae_idct.hip; columns on
+    k_idct_cols512b with the band-layout U (dec_cols_kernel 2, default) or
+    k_idct_cols512 with row-major U (1)) against the oracle's decode of the
+    same codes (<= 1e-5 x image range) and against the MFMA GEMM decode (two
+    fp32 evaluations of the same transform)."""
     ops = _ops()
     x = torch.from_numpy(np.stack(rng.synth_images(71, [(512, 512)] * 3))).to(DEV)
     ((dp, codes),) = fe.encode_batch(x, pn, lfq)
-    imgs_fft = fe.decode_batch(dp, codes, pn, lfq)
+    ops.set_option("dec_cols_kernel", dec_cols)
+    try:
+        imgs_fft = fe.decode_batch(dp, codes, pn, lfq)
+    finally:
+        ops.set_option("dec_cols_kernel", 2)
     ops.set_option("fft_decode", 0)
     try:
         imgs_gemm = fe.decode_batch(dp, codes, pn, lfq)
@@ -669,6 +703,37 @@ def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables):
         assert ok, ("fft vs gemm", dmax, scale)
 
 
+@pytest.mark.parametrize("caps", [(20, 32), (32, 20)])
+def test_fft_decode_512_patch_caps_vs_oracle(pkg, lfq, ref_tables, caps):
+    """512^2 decode at max_patch_h / max_patch_w below 32: 20 kept tile rows
+    (band-layout column kernel with absent tiles zero) or 20 kept tile columns
+    (row-major U, k_idct_cols512 + k_idct_rows2) against the oracle's decode."""
+    mh, mw = caps
+    cfg = ref_cpu.FEConfig(max_patch_h=mh, max_patch_w=mw, max_seq_len=3 * mh * mw)
+    tables = ref_cpu.NormTables(ref_tables.n[:, :mh, :mw].contiguous(), ref_tables.median[:, :mh, :mw].contiguous(),
+                                ref_tables.b[:, :mh, :mw].contiguous())
+    pn = pkg.PatchNorm(mh, mw, 14, 3).to(DEV)
+    pn.median.data.copy_(tables.median)
+    pn.b.data.copy_(tables.b)
+    pn.frozen = True
+    pn.eval()
+    fe = pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, mh, mw, 3 * mh * mw)
+    x = torch.from_numpy(np.stack(rng.synth_images(73, [(512, 512)] * 2))).to(DEV)
+    ((dp, codes),) = fe.encode_batch(x, pn, lfq)
+    imgs = fe.decode_batch(dp, codes, pn, lfq)
+    _ops().check_device_errors(x.device)
+    y = ref_cpu.lfq_indices_to_codes(codes.cpu(), ref_cpu.LFQConfig())
+    pos, chs = dp.patch_positions.cpu(), dp.patch_channels.cpu()
+    xin = ref_cpu.norm_inverse(tables, y, chs, pos[..., 0], pos[..., 1])
+    batch = ref_cpu.Batch(xin, dp.key_pad_mask.cpu(), None, dp.batched_image_ids.cpu(), chs, pos, dp.patch_sizes,
+                          dp.original_sizes)
+    refs = ref_cpu.postprocess(batch, cfg)
+    for a, r in zip(imgs, refs):
+        scale = max(1.0, float(r.abs().max()))
+        ok, dmax = _rgb_close(a.cpu(), r, atol=1e-5 * scale, rtol=2e-5)
+        assert ok, (dmax, scale)
+
+
 def test_sort_overlap_bit_identical(fe, pn, lfq):
     """Option sort_overlap (the columns of a band-image batch in two halves,
     the first half's sort / pack on a side stream beside the second half's
@@ -687,26 +752,30 @@ def test_sort_overlap_bit_identical(fe, pn, lfq):
         assert torch.equal(getattr(dp0, f), getattr(dp1, f)), f
 
 
-def test_fft_decode_duplicate_tokens_last_wins(fe, pn, lfq, ref_tables):
+@pytest.mark.parametrize("shapes", [[(512, 512)] * 2, [(224, 224), (300, 262)]], ids=["fft512", "gemm"])
+def test_fft_decode_duplicate_tokens_last_wins(fe, pn, lfq, ref_tables, shapes):
     """Two tokens of one image at the same (channel, h, w): the reference's
     revert_patching assigns tokens in packed order (FE:639-643), so the later
-    one wins.  FFT decode (item-major map by atomicMax + staged codes) against
-    the oracle's per-token loop on the same edited batch."""
-    x = torch.from_numpy(np.stack(rng.synth_images(83, [(512, 512)] * 2))).to(DEV)
+    one wins.  FFT decode (512^2: item-major map by atomicMax + staged codes)
+    and the GEMM decode (other sizes: the same slot map gates
+    k_scatter_tokens' stores) against the oracle's per-token loop on the same
+    edited batch."""
+    xs = rng.synth_images(83, shapes)
+    x = torch.from_numpy(np.stack(xs)).to(DEV) if len(set(shapes)) == 1 else [torch.from_numpy(a).to(DEV) for a in xs]
     ((dp, codes),) = fe.encode_batch(x, pn, lfq)
     pos, chs, codes = dp.patch_positions.clone(), dp.patch_channels.clone(), codes.clone()
     ids, kp = dp.batched_image_ids, dp.key_pad_mask
     # image of row 0's first token: copy (c, h, w) of its slot j0 onto three later slots of the same image
     img0 = int(ids[0, 0])
     js = [j for j in range(ids.shape[1]) if int(ids[0, j]) == img0 and not bool(kp[0, j])]
-    j0, later = js[3], [js[100], js[1000], js[len(js) - 1]]
+    j0, later = js[3], [js[len(js) // 8], js[len(js) // 2], js[len(js) - 1]]
     for n, j in enumerate(later):
         pos[0, j] = pos[0, j0]
         chs[0, j] = chs[0, j0]
         codes[0, j] = (codes[0, j0] + 977 * (n + 1)) % (2 ** 14)   # distinguishable codes
     dp.patch_positions, dp.patch_channels = pos, chs
     imgs = fe.decode_batch(dp, codes, pn, lfq)
-    _ops().check_device_errors(x.device)
+    _ops().check_device_errors(codes.device)
     y = ref_cpu.lfq_indices_to_codes(codes.cpu(), ref_cpu.LFQConfig())
     xin = ref_cpu.norm_inverse(ref_tables, y, chs.cpu(), pos.cpu()[..., 0], pos.cpu()[..., 1])
     batch = ref_cpu.Batch(xin, kp.cpu(), None, ids.cpu(), chs.cpu(), pos.cpu(), dp.patch_sizes, dp.original_sizes)
