@@ -52,33 +52,57 @@ __device__ __forceinline__ cf pre_z(float yk, float ynk, float ymk, float ymk2, 
 // wins (atomicMax: deterministic, where plain stores would race; +0.03 ms per
 // 1024 images).  Same argument checks as k_scatter_tokens.
 // ---------------------------------------------------------------------------
-__global__ void k_dec_map(int64_t n_tok, const ImgDesc* __restrict__ imgs, DecodeArgs a, int32_t* __restrict__ map) {
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tok; t += (int64_t)gridDim.x * blockDim.x) {
-    if (a.key_pad[t]) continue;
-    const int64_t r = t / a.S;
-    const int64_t id = a.ids[t];
-    if (id < 0 || id >= a.lut_w) {
-      atomicOr(a.err, 2);
-      continue;
-    }
-    const int im = a.lut[r * a.lut_w + id];
-    if (im < 0) {
-      atomicOr(a.err, 2);
-      continue;
-    }
-    const ImgDesc d = imgs[im];
-    const int64_t c = a.ch[t], h = a.pos[2 * t], w = a.pos[2 * t + 1];
-    if (c < 0 || c >= 3 || h < 0 || h >= d.qh || w < 0 || w >= d.qw) {
-      atomicOr(a.err, 4);
-      continue;
-    }
-    atomicMax(map + (((int64_t)im * 3 + c) * a.maxpw + w) * a.maxph + h, (int32_t)t);
+__device__ __forceinline__ void dec_map_token(int64_t t, int64_t id, int64_t c, int64_t h, int64_t w,
+                                              const ImgDesc* __restrict__ imgs, const DecodeArgs& a,
+                                              int32_t* __restrict__ map) {
+  const int64_t r = t / a.S;
+  if (id < 0 || id >= a.lut_w) {
+    atomicOr(a.err, 2);
+    return;
   }
+  const int im = a.lut[r * a.lut_w + id];
+  if (im < 0) {
+    atomicOr(a.err, 2);
+    return;
+  }
+  const int qh = imgs[im].qh, qw = imgs[im].qw;
+  if (c < 0 || c >= 3 || h < 0 || h >= qh || w < 0 || w >= qw) {
+    atomicOr(a.err, 4);
+    return;
+  }
+  atomicMax(map + (((int64_t)im * 3 + c) * a.maxpw + w) * a.maxph + h, (int32_t)t);
+}
+
+// four consecutive tokens per thread: ids / channels as two 16-byte loads,
+// positions as four, key_pad as one 4-byte load, for the first 4 n4 tokens
+// (n4 = 0 unless the tensors are 16-byte aligned); the rest token by token
+__global__ void k_dec_map(int64_t n_tok, int64_t n4, const ImgDesc* __restrict__ imgs, DecodeArgs a,
+                          int32_t* __restrict__ map) {
+  typedef long long i64x2 __attribute__((ext_vector_type(2)));
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t0 = 4 * q;
+    const uint32_t kp = *reinterpret_cast<const uint32_t*>(a.key_pad + t0);
+    if (kp == 0x01010101u) continue;
+    const i64x2* ip = reinterpret_cast<const i64x2*>(a.ids + t0);
+    const i64x2* cp = reinterpret_cast<const i64x2*>(a.ch + t0);
+    const i64x2* pp = reinterpret_cast<const i64x2*>(a.pos + 2 * t0);
+    const i64x2 i01 = ip[0], i23 = ip[1], c01 = cp[0], c23 = cp[1];
+    const i64x2 p0 = pp[0], p1 = pp[1], p2 = pp[2], p3 = pp[3];
+    if (!(kp & 0xffu)) dec_map_token(t0, i01.x, c01.x, p0.x, p0.y, imgs, a, map);
+    if (!(kp & 0xff00u)) dec_map_token(t0 + 1, i01.y, c01.y, p1.x, p1.y, imgs, a, map);
+    if (!(kp & 0xff0000u)) dec_map_token(t0 + 2, i23.x, c23.x, p2.x, p2.y, imgs, a, map);
+    if (!(kp & 0xff000000u)) dec_map_token(t0 + 3, i23.y, c23.y, p3.x, p3.y, imgs, a, map);
+  }
+  for (int64_t t = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_tok;
+       t += (int64_t)gridDim.x * blockDim.x)
+    if (!a.key_pad[t]) dec_map_token(t, a.ids[t], a.ch[t], a.pos[2 * t], a.pos[2 * t + 1], imgs, a, map);
 }
 
 void launch_dec_map(int64_t n_tok, const ImgDesc* imgs, const DecodeArgs& a, int32_t* map, hipStream_t s) {
-  const int gx = (int)std::min<int64_t>((n_tok + 255) / 256, 8192);
-  if (gx > 0) hipLaunchKernelGGL(k_dec_map, dim3(gx), dim3(256), 0, s, n_tok, imgs, a, map);
+  const bool al = ((uintptr_t)a.ids | (uintptr_t)a.ch | (uintptr_t)a.pos) % 16 == 0 && (uintptr_t)a.key_pad % 4 == 0;
+  const int64_t n4 = al ? n_tok / 4 : 0;
+  const int gx = (int)std::min<int64_t>((std::max<int64_t>(n4, n_tok - 4 * n4) + 255) / 256, 8192);
+  if (gx > 0) hipLaunchKernelGGL(k_dec_map, dim3(gx), dim3(256), 0, s, n_tok, n4, imgs, a, map);
 }
 
 // ---------------------------------------------------------------------------
@@ -113,67 +137,93 @@ struct IColsLds {
 // rows through xrow, zero rows for tiles absent from the batch): thread
 // (g16, jl) expands tile rows h = g16 + 16 r, element row jl, from the
 // token's code (LFQ bit -> +-scale -> inverse PatchNorm: vt) or its patch.
-// zero_tail: also zero rows 448 .. 511 (read by k_idct_cols512 only).
-__device__ __forceinline__ void icols_fill_x(int img, const ImgDesc& d, int c, int strip,
-                                             const int32_t* __restrict__ map, const DecodeArgs& a,
-                                             const float2 (&vt)[2][14], float* x, bool zero_tail) {
+// Three stages, so k_idct_cols512b can keep the next image's in flight:
+// icols_map (packed slots of the two tiles, FE:639-643's winner), icols_codes
+// (the element row's code of each; a dependent load), icols_expand.
+struct IcTok {
+  int32_t sl[2];     // packed slot of tile g16 + 16 r, -1 = absent
+  int32_t code[2];   // its code for element row jl (use_codes)
+};
+
+__device__ __forceinline__ void icols_map(int img, const ImgDesc& d, int c, int strip, const int32_t* __restrict__ map,
+                                          const DecodeArgs& a, IcTok& t) {
+  const int g16 = itid() >> 4;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int h = g16 + 16 * r;
+    t.sl[r] = map[(((int64_t)img * 3 + c) * a.maxpw + strip) * a.maxph + (h < d.qh ? h : 0)];
+    if (h >= d.qh) t.sl[r] = -1;
+  }
+}
+
+__device__ __forceinline__ void icols_codes(const DecodeArgs& a, IcTok& t) {
+  constexpr int KS = 14;
+  const int jl = itid() & 15;
+  if (!a.use_codes) return;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {   // unconditional loads; the low word of the int64 code (lfq.py:117 .int())
+    const int64_t s0 = t.sl[r] >= 0 ? t.sl[r] : 0;
+    t.code[r] = reinterpret_cast<const int32_t*>(a.codes)[2 * (s0 * a.ncb + (jl < KS ? jl : 0))];
+  }
+}
+
+// zero_tail: also zero rows 448 .. 511 (read by k_idct_cols512 only)
+__device__ __forceinline__ void icols_expand(const IcTok& t, const DecodeArgs& a, const float2 (&vt)[2][14], float* x,
+                                             bool zero_tail) {
   constexpr int N = 512, KS = 14, PP = KS * KS;
   const int tid = itid();
 #if defined(DCTAE_PROFILING) && defined(DCTAE_IC_ABL)
   if (DCTAE_IC_ABL & 1) {   // profiling ablation: no token loads / expansion (wrong output)
     for (int e = tid; e < N * KS; e += 256) x[e] = 0.001f * (e & 63);
-  } else
-#endif
-  {
-    const int g16 = tid >> 4, jl = tid & 15;
-    int32_t sl[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int h = g16 + 16 * r;
-      sl[r] = map[(((int64_t)img * 3 + c) * a.maxpw + strip) * a.maxph + (h < d.qh ? h : 0)];
-      if (h >= d.qh) sl[r] = -1;
-    }
-    int32_t code[2];
-    float pv[2][KS];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int64_t s0 = sl[r] >= 0 ? sl[r] : 0;   // unconditional loads
-      if (a.use_codes) {
-        code[r] = (int32_t)a.codes[s0 * a.ncb + (jl < KS ? jl : 0)];
-      } else {
-        const float* pt = a.patches + s0 * PP + (jl < KS ? jl : 0) * KS;
-#pragma unroll
-        for (int p = 0; p < KS; ++p) pv[r][p] = pt[p];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int h = g16 + 16 * r;
-      if (jl < KS) {
-        f2v* xr = reinterpret_cast<f2v*>(x + xrow(KS * h + jl) * KS);
-#pragma unroll
-        for (int p = 0; p < KS / 2; ++p) {
-          float v0, v1;
-          if (a.use_codes) {
-            // bit select by masks: a ?: on the pair lets the compiler select
-            // the address instead and move vt to scratch
-            const uint32_t m0 = 0u - ((uint32_t)(code[r] >> (KS - 1 - 2 * p)) & 1u);
-            const uint32_t m1 = 0u - ((uint32_t)(code[r] >> (KS - 2 - 2 * p)) & 1u);
-            v0 = __uint_as_float((__float_as_uint(vt[r][2 * p].x) & m0) | (__float_as_uint(vt[r][2 * p].y) & ~m0));
-            v1 = __uint_as_float((__float_as_uint(vt[r][2 * p + 1].x) & m1) |
-                                 (__float_as_uint(vt[r][2 * p + 1].y) & ~m1));
-          } else {
-            v0 = pv[r][2 * p];
-            v1 = pv[r][2 * p + 1];
-          }
-          xr[p] = sl[r] >= 0 ? (f2v){v0, v1} : (f2v){0.0f, 0.0f};
-        }
-      }
-    }
-    // rows 448 .. 511 (beyond Kh = 448 when qh = 32): zero
-    if (zero_tail)
-      for (int e = tid; e < (N - KS * 32) * KS; e += 256) x[KS * 32 * KS + e] = 0.0f;
+    return;
   }
+#endif
+  const int g16 = tid >> 4, jl = tid & 15;
+  float pv[2][KS];
+  if (!a.use_codes) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int64_t s0 = t.sl[r] >= 0 ? t.sl[r] : 0;   // unconditional loads
+      const float* pt = a.patches + s0 * PP + (jl < KS ? jl : 0) * KS;
+#pragma unroll
+      for (int p = 0; p < KS; ++p) pv[r][p] = pt[p];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int h = g16 + 16 * r;
+    if (jl < KS) {
+      f2v* xr = reinterpret_cast<f2v*>(x + xrow(KS * h + jl) * KS);
+#pragma unroll
+      for (int p = 0; p < KS / 2; ++p) {
+        float v0, v1;
+        if (a.use_codes) {
+          // bit select by masks: a ?: on the pair lets the compiler select
+          // the address instead and move vt to scratch
+          const uint32_t m0 = 0u - ((uint32_t)(t.code[r] >> (KS - 1 - 2 * p)) & 1u);
+          const uint32_t m1 = 0u - ((uint32_t)(t.code[r] >> (KS - 2 - 2 * p)) & 1u);
+          v0 = __uint_as_float((__float_as_uint(vt[r][2 * p].x) & m0) | (__float_as_uint(vt[r][2 * p].y) & ~m0));
+          v1 = __uint_as_float((__float_as_uint(vt[r][2 * p + 1].x) & m1) | (__float_as_uint(vt[r][2 * p + 1].y) & ~m1));
+        } else {
+          v0 = pv[r][2 * p];
+          v1 = pv[r][2 * p + 1];
+        }
+        xr[p] = t.sl[r] >= 0 ? (f2v){v0, v1} : (f2v){0.0f, 0.0f};
+      }
+    }
+  }
+  // rows 448 .. 511 (beyond Kh = 448 when qh = 32): zero
+  if (zero_tail)
+    for (int e = tid; e < (N - KS * 32) * KS; e += 256) x[KS * 32 * KS + e] = 0.0f;
+}
+
+__device__ __forceinline__ void icols_fill_x(int img, const ImgDesc& d, int c, int strip,
+                                             const int32_t* __restrict__ map, const DecodeArgs& a,
+                                             const float2 (&vt)[2][14], float* x, bool zero_tail) {
+  IcTok t;
+  icols_map(img, d, c, strip, map, a, t);
+  icols_codes(a, t);
+  icols_expand(t, a, vt, x, zero_tail);
 }
 
 // image-independent values of this thread's two tile rows (h = g16 + 16 r,
@@ -516,13 +566,22 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
   const int G = tid >> 4, j = tid & 15;
   const int col = min(G, KS - 1);
   const int uo = u4_index(j, KS * strip + col) * 16;   // band4 = j + 16 i at + i * ustep
+  // the tokens of image u + 1 in flight during image u: its map entries are
+  // loaded right after image u's expansion, its codes (dependent on them)
+  // after image u's FFT, before image u's U stores
+  IcTok tk;
+  icols_map(i0, imgs[i0], c, strip, map, a, tk);
+  icols_codes(a, tk);
 #pragma unroll
   for (int u = 0; u < IPB; ++u) {
     const int img = i0 + u;
     if (img >= n_img) break;   // block-uniform
     const ImgDesc d = imgs[img];
     __syncthreads();   // tables (u = 0) / the previous image's transposes (x aliases xch)
-    icols_fill_x(img, d, c, strip, map, a, vt, L.u.x, false);
+    icols_expand(tk, a, vt, L.u.x, false);
+    IcTok tn;
+    const int img_n = min(img + 1, n_img - 1);   // unconditional (the last image reloads itself)
+    if (u + 1 < IPB) icols_map(img_n, imgs[img_n], c, strip, map, a, tn);
     __syncthreads();
     // conj Z_k, k = j + 16 i (Ys[M + k] = 0 for i >= 12, Ys[N - k] = 0 for k <= 64)
     cf v[16];
@@ -547,6 +606,7 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
     }
     __syncthreads();   // every group's X reads before the transposes
     fft256_group(v, L.u.xch[G], j, j, L.tw2);
+    if (u + 1 < IPB) icols_codes(a, tn);
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws + d.ws_t + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
                                                         0x00020000);
 #pragma unroll
@@ -556,12 +616,16 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
           (v4u){__float_as_uint(v[i].x), __float_as_uint(-py), __float_as_uint(-v[i].y), __float_as_uint(px)}, rsrc,
           uo, i * ustep, 0);
     }
+    if (u + 1 < IPB) tk = tn;
   }
 }
 
+#ifndef DCTAE_IC5B_IPB
+#define DCTAE_IC5B_IPB 8
+#endif
 void launch_idct_cols512b(const ImgDesc* imgs, int n_img, float* ws, const int32_t* map, const float2* tw,
                           const float4* pre, const DecodeArgs& a, hipStream_t s) {
-  constexpr int IPB = 2;
+  constexpr int IPB = DCTAE_IC5B_IPB;
   const int grid = 8 * 12 * ((n_img + IPB - 1) / IPB);
   if (n_img > 0)
     hipLaunchKernelGGL((k_idct_cols512b<IPB>), dim3(grid), dim3(256), 0, s, imgs, n_img, ws, map, tw, pre, a);

@@ -703,6 +703,32 @@ def test_fft_decode_512_vs_oracle_and_gemm(fe, pn, lfq, ref_tables, dec_cols):
         assert ok, ("fft vs gemm", dmax, scale)
 
 
+@pytest.mark.parametrize("shapes", [[(512, 512)] * 2, [(224, 224), (100, 140), (300, 262)]], ids=["fft512", "gemm"])
+def test_decode_odd_seq_len_vs_oracle(pkg, pn, lfq, ref_tables, shapes):
+    """max_seq_len 3073 (odd): every packed row ends in pads and the token count
+    is not a multiple of 4, so k_dec_map runs its 4-token vector loop and the
+    token-by-token tail; decode (FFT path at 512^2, GEMM otherwise) against
+    the oracle's decode of the same codes."""
+    cfg = ref_cpu.FEConfig(max_seq_len=3073)
+    fe = pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, 32, 32, 3073)
+    xs = rng.synth_images(91, shapes)
+    ((dp, codes),) = fe.encode_batch([torch.from_numpy(a).to(DEV) for a in xs], pn, lfq)
+    assert (dp.key_pad_mask.numel() % 4) != 0
+    imgs = fe.decode_batch(dp, codes, pn, lfq)
+    _ops().check_device_errors(codes.device)
+    y = ref_cpu.lfq_indices_to_codes(codes.cpu(), ref_cpu.LFQConfig())
+    pos, chs = dp.patch_positions.cpu(), dp.patch_channels.cpu()
+    xin = ref_cpu.norm_inverse(ref_tables, y, chs, pos[..., 0], pos[..., 1])
+    batch = ref_cpu.Batch(xin, dp.key_pad_mask.cpu(), None, dp.batched_image_ids.cpu(), chs, pos, dp.patch_sizes,
+                          dp.original_sizes)
+    refs = ref_cpu.postprocess(batch, cfg)
+    assert len(refs) == len(imgs) == len(xs)
+    for a, r in zip(imgs, refs):
+        scale = max(1.0, float(r.abs().max()))
+        ok, dmax = _rgb_close(a.cpu(), r, atol=1e-5 * scale, rtol=2e-5)
+        assert ok, (dmax, scale)
+
+
 @pytest.mark.parametrize("caps", [(20, 32), (32, 20)])
 def test_fft_decode_512_patch_caps_vs_oracle(pkg, lfq, ref_tables, caps):
     """512^2 decode at max_patch_h / max_patch_w below 32: 20 kept tile rows

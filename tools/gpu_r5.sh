@@ -17,6 +17,14 @@ fi
 if [ -n "${AB:-}" ]; then
   eval "bash tools/gpu_try.sh $AB" || exit 1
 fi
+if [ -n "${PROBE:-}" ]; then   # DFT16 on VALU vs MFMA (tools/probe/dft16_mfma.hip) + its counters
+  timeout -k 10 120 ./tools/probe/dft16_mfma > gpurun_out/dft16_probe.json 2> gpurun_out/dft16_probe.err || { cat gpurun_out/dft16_probe.err; exit 1; }
+  cat gpurun_out/dft16_probe.json
+  rm -rf gpurun_out/dft16_pmc
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES \
+      SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/dft16_pmc -o pmc -- ./tools/probe/dft16_mfma \
+      > gpurun_out/dft16_pmc.log 2>&1 || { tail -20 gpurun_out/dft16_pmc.log; exit 1; }
+fi
 if [ -n "${CFG2TRACE:-}" ]; then
   rm -rf gpurun_out/cfg2trace
   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/cfg2trace -o run --output-format csv -- \
