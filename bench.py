@@ -141,7 +141,7 @@ def cpu_config1(threads, reps=10, size=224):
             "reps": reps, "cores": threads, "kind": "port", "roundtrip_max_abs_err": err}
 
 
-def cpu_config_legs(threads, tables, seed=3):
+def cpu_config_legs(threads, tables, seed=3, min_s=2.0):
     """BASELINE.md §3's capped CPU subsets of configs 2-4 on the oracle port
     (the reference's op sequence: FFT DCT, per-image sort, greedy packing with
     attn_mask, PatchNorm, LFQ; decode through the reference's per-token revert
@@ -149,7 +149,8 @@ def cpu_config_legs(threads, tables, seed=3):
       config 2: 256 x 224^2 encode;
       config 3: 8 x 512^2 round trip (encode, then indices_to_codes ->
                 inverse_norm -> postprocess), encode and decode timed apart;
-      config 4: the first 32 images of the GPU leg's ragged sizes (seed 7)."""
+      config 4: the first 32 images of the GPU leg's ragged sizes (seed 7).
+    Each leg runs once untimed, then repeats until min_s of host time."""
     from oracle import ref_cpu
     torch.set_num_threads(threads)
     cfg, lcfg = ref_cpu.FEConfig(), ref_cpu.LFQConfig()
@@ -157,35 +158,49 @@ def cpu_config_legs(threads, tables, seed=3):
     out = {}
 
     def enc(imgs):
-        t0 = time.perf_counter()
-        res = ref_cpu.encode(imgs, cfg, tables, lcfg, batch_size=None, build_attn_mask=True)
-        return res, time.perf_counter() - t0
+        return ref_cpu.encode(imgs, cfg, tables, lcfg, batch_size=None, build_attn_mask=True)
+
+    def timed(fn, min_s):
+        """fn repeated until min_s of host time (after one untimed run): mean seconds per run"""
+        fn()
+        n, t0 = 0, time.perf_counter()
+        while True:
+            fn()
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= min_s:
+                return el / n, n
 
     imgs = [torch.rand(3, 224, 224, generator=g) for _ in range(256)]
-    _, el = enc(imgs)
+    el, n = timed(lambda: enc(imgs), min_s)
     out["config2"] = {"workload": "256 x 224x224 encode", "value": round(256 * 224 * 224 / el / 1e6, 3),
-                      "unit": "Mpix/s", "seconds": round(el, 3)}
+                      "unit": "Mpix/s", "seconds_per_run": round(el, 4), "runs": n}
     imgs = [torch.rand(3, 512, 512, generator=g) for _ in range(8)]
-    res, el_e = enc(imgs)
-    t0 = time.perf_counter()
-    n_out = 0
-    for batch, idx in res:
-        y = ref_cpu.lfq_indices_to_codes(idx, lcfg)
-        batch.patches = ref_cpu.norm_inverse(tables, y, batch.patch_channels, batch.h_indices, batch.w_indices)
-        n_out += len(ref_cpu.postprocess(batch, cfg, per_token_loop=True))
-    el_d = time.perf_counter() - t0
-    assert n_out == 8
+    el_e, n_e = timed(lambda: enc(imgs), min_s)
+    res = enc(imgs)
+
+    def dec():
+        n_out = 0
+        for batch, idx in res:
+            b = ref_cpu.Batch(None, batch.key_pad_mask, None, batch.batched_image_ids, batch.patch_channels,
+                              batch.patch_positions, batch.patch_sizes, batch.original_sizes)
+            y = ref_cpu.lfq_indices_to_codes(idx, lcfg)
+            b.patches = ref_cpu.norm_inverse(tables, y, batch.patch_channels, batch.h_indices, batch.w_indices)
+            n_out += len(ref_cpu.postprocess(b, cfg, per_token_loop=True))
+        assert n_out == 8
+
+    el_d, n_d = timed(dec, min_s)
     pix = 8 * 512 * 512
     out["config3"] = {"workload": "8 x 512x512 round trip (encode + decode through the per-token revert loop)",
                       "value": round(pix / (el_e + el_d) / 1e6, 3), "unit": "Mpix/s (round trip)",
                       "encode_mpix_s": round(pix / el_e / 1e6, 3), "decode_mpix_s": round(pix / el_d / 1e6, 3),
-                      "seconds": round(el_e + el_d, 3)}
+                      "seconds_per_run": round(el_e + el_d, 4), "runs": [n_e, n_d]}
     hw = np.random.default_rng(7).integers(14, 1025, size=(1024, 2))[:32]
     imgs = [torch.rand(3, int(h), int(w), generator=g) for h, w in hw]
-    _, el = enc(imgs)
+    el, n = timed(lambda: enc(imgs), min_s)
     out["config4"] = {"workload": "32 ragged images, the GPU leg's first 32 sizes (H, W) ~ U{14..1024}^2 seed 7, "
                                   "encode", "value": round(int((hw[:, 0] * hw[:, 1]).sum()) / el / 1e6, 3),
-                      "unit": "Mpix/s", "seconds": round(el, 3)}
+                      "unit": "Mpix/s", "seconds_per_run": round(el, 4), "runs": n}
     return out
 
 

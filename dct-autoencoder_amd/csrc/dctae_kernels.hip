@@ -54,56 +54,80 @@ void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_
 // column GEMM.  One thread per group of up to 4 mirrored pixels.
 // Blocks from a host list of (image, first group): kRgbGroups groups per
 // block (a grid over every image x the largest image's groups spent most of its
-// blocks exiting on the ragged config 4).
-constexpr int kRgbGroups = 256;
+// blocks exiting on the ragged config 4), kRgbGpt groups per thread (thread t
+// takes groups t + 256 k): every group's 12 loads are issued before any
+// colour math, so a thread keeps up to 48 loads in flight (one group per
+// thread, 256 groups per block, measured 1.55 ms on config 4).
+constexpr int kRgbGpt = 4;
+constexpr int kRgbGroups = 256 * kRgbGpt;
 
-__global__ void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
-                             const float* __restrict__ rgb, float* __restrict__ ws, ColorMats cm) {
+__global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
+                                                    const float* __restrict__ rgb, float* __restrict__ ws,
+                                                    ColorMats cm) {
   const int2 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
-  const int64_t hw = (int64_t)d.H * d.W;
-  const int Wh = (d.W + 1) / 2;
+  const int W = d.W, H = d.H;
+  const int64_t hw = (int64_t)H * W;
+  const int Wh = (W + 1) / 2;
   const bool yfold = d.plan_h < 0;
-  const int Hh = yfold ? (d.H + 1) / 2 : d.H;
-  const int64_t n_groups = (int64_t)Hh * Wh;
+  const int Hh = yfold ? (H + 1) / 2 : H;
+  const int n_groups = Hh * Wh;   // < 2^31: the ABI's int32 image sides
   const float* src = rgb + d.rgb_off;
   float* dst = ws + d.ws_p;
-  auto ipt = [&](int64_t e, float out[3]) {
-    float r = src[e], g = src[hw + e], b = src[2 * hw + e];
-    float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), 0.430000007152557373046875f);
-    float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), 0.430000007152557373046875f);
-    float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), 0.430000007152557373046875f);
-    for (int c = 0; c < 3; ++c) out[c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
-  };
-  // x-fold of one row's pair (p[x], p[x2]) into row `row`
-  auto put_row = [&](int64_t row, int x, bool pair, const float* a, const float* b) {
-    for (int c = 0; c < 3; ++c) {
-      dst[c * hw + row + x] = pair ? a[c] + b[c] : a[c];
-      if (pair) dst[c * hw + row + Wh + x] = a[c] - b[c];
-    }
-  };
-  const int64_t e_end = min(n_groups, (int64_t)jb.y + kRgbGroups);
-  for (int64_t e = (int64_t)jb.y + threadIdx.x; e < e_end; e += blockDim.x) {
-    const int y = (int)(e / Wh);
-    const int x = (int)(e - (int64_t)y * Wh), x2 = d.W - 1 - x, y2 = d.H - 1 - y;
+  const float gam = 0.430000007152557373046875f;
+  // pixel q of group k: 0 = (y, x), 1 = (y, x2), 2 = (y2, x), 3 = (y2, x2); absent
+  // mirrors (middle column / row, no y-fold) re-read pixel 0 and are not stored
+  float px[kRgbGpt][4][3];
+  int yk[kRgbGpt], xk[kRgbGpt];
+#pragma unroll
+  for (int k = 0; k < kRgbGpt; ++k) {
+    const int e = min(jb.y + (int)threadIdx.x + 256 * k, n_groups - 1);
+    const int y = e / Wh, x = e - y * Wh;
+    yk[k] = y;
+    xk[k] = x;
+    const int x2 = W - 1 - x, y2 = yfold ? H - 1 - y : y;
+    const int64_t o[4] = {(int64_t)y * W + x, (int64_t)y * W + x2, (int64_t)y2 * W + x, (int64_t)y2 * W + x2};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) px[k][q][c] = src[c * hw + o[q]];
+  }
+#pragma unroll
+  for (int k = 0; k < kRgbGpt; ++k) {
+    const int e = jb.y + (int)threadIdx.x + 256 * k;
+    if (e >= n_groups || e >= jb.y + kRgbGroups) break;
+    const int y = yk[k], x = xk[k], x2 = W - 1 - x, y2 = H - 1 - y;
     const bool xp = x2 != x, yp = yfold && y2 != y;
-    float a[3], b[3] = {0.f, 0.f, 0.f};
-    ipt((int64_t)y * d.W + x, a);
-    if (xp) ipt((int64_t)y * d.W + x2, b);
-    if (yp) {
-      float c2[3], d2[3] = {0.f, 0.f, 0.f}, s0[3], s1[3], t0[3], t1[3];
-      ipt((int64_t)y2 * d.W + x, c2);
-      if (xp) ipt((int64_t)y2 * d.W + x2, d2);
-      for (int c = 0; c < 3; ++c) {
-        s0[c] = a[c] + c2[c];
-        s1[c] = b[c] + d2[c];
-        t0[c] = a[c] - c2[c];
-        t1[c] = b[c] - d2[c];
+    float p[4][3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // util.py:70-82
+      const float r = px[k][q][0], g = px[k][q][1], b = px[k][q][2];
+      const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), gam);
+      const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), gam);
+      const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), gam);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) p[q][c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
+    }
+    // y-fold (rows y / y2: sum / difference), then the x-fold of each row's pair
+    float a[3], b[3], c2[3], d2[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float pb = xp ? p[1][c] : 0.0f, pd = xp ? p[3][c] : 0.0f;
+      a[c] = yp ? p[0][c] + p[2][c] : p[0][c];
+      b[c] = yp ? pb + pd : pb;
+      c2[c] = p[0][c] - p[2][c];
+      d2[c] = pb - pd;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float* ro = dst + c * hw + (int64_t)y * W;
+      ro[x] = xp ? a[c] + b[c] : a[c];
+      if (xp) ro[Wh + x] = a[c] - b[c];
+      if (yp) {
+        float* r2 = dst + c * hw + (int64_t)y2 * W;
+        r2[x] = xp ? c2[c] + d2[c] : c2[c];
+        if (xp) r2[Wh + x] = c2[c] - d2[c];
       }
-      put_row((int64_t)y * d.W, x, xp, s0, s1);
-      put_row((int64_t)y2 * d.W, x, xp, t0, t1);
-    } else {
-      put_row((int64_t)y * d.W, x, xp, a, b);
     }
   }
 }

@@ -2,7 +2,7 @@
 # Iteration: parity tests selected by TESTS (pytest -k), then a same-box A/B of
 # the encode bench over option sets ("opt=v opt=v" per argument; a leading
 # "lib=<path>" selects another libdctae.so build).  DEC=1 adds the config-3
-# decode leg; CFG2=1 times config 2 only (tools/cfg2_try.py).  Each GPU step time-limited; stop at the first failure.
+# decode leg; CFG2=1 / CFG4=1 time config 2 / 4 only (tools/cfg2_try.py, cfg4_try.py).  Each GPU step time-limited; stop at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -19,6 +19,12 @@ for opts in "$@"; do
   for o in $opts; do
     case $o in lib=*) export DCTAE_LIBRARY="${o#lib=}";; *) args="$args --opt $o";; esac
   done
+  if [ -n "${CFG4:-}" ]; then   # config 4 only (tools/cfg4_try.py)
+    timeout -k 10 300 python tools/cfg4_try.py $args > gpurun_out/try_cfg4.log 2>&1
+    rc=$?; echo "=== cfg4 [$opts] rc=$rc"; tail -1 gpurun_out/try_cfg4.log
+    [ $rc -ne 0 ] && exit $rc
+    continue
+  fi
   if [ -n "${CFG2:-}" ]; then   # config 2 only (tools/cfg2_try.py)
     timeout -k 10 200 python tools/cfg2_try.py $args > gpurun_out/try_cfg2.log 2>&1
     rc=$?; echo "=== cfg2 [$opts] rc=$rc"; tail -1 gpurun_out/try_cfg2.log
