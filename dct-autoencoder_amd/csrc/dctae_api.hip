@@ -39,6 +39,8 @@ struct dctae_ctx {
   struct X3Mat {
     uint16_t* d;
     int R, K, Rp, Kp;
+    uint16_t* dh;   // k_gemm_h2: two fp16 planes [2][Rp][Kp] of the matrix scaled by 2^hexp
+    int hexp;
   };
   std::map<const float*, X3Mat> dct_x3;
   // workspace (floats) and token staging (bytes), grow-only
@@ -104,6 +106,10 @@ struct dctae_ctx {
   // split-bf16 MFMA kernel k_gemm_x3 (fp32 accuracy, 0.375 of the MFMA time),
   // 0 = the fp32 MFMA kernel k_gemm_f32
   int gemm_x3 = 1;
+  // the encode's DCT GEMMs (with gemm_x3): 1 = k_gemm_h2 (fp16 MFMA, two-piece
+  // operands scaled into the fp16 range, three products: half k_gemm_x3's
+  // MFMAs), 0 = k_gemm_x3
+  int gemm_h2 = 1;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
@@ -325,10 +331,14 @@ int dct_matrix(dctae_ctx* ctx, int N, int rows, const float** out, int parity = 
   ctx->dct[key] = d;
   {
     std::vector<uint16_t> x;
-    dctae_ctx::X3Mat xm{nullptr, R, Nc, 0, 0};
+    dctae_ctx::X3Mat xm{nullptr, R, Nc, 0, 0, nullptr, 0};
     split_matrix_x3(h.data(), R, Nc, x, &xm.Rp, &xm.Kp);
     HIPCHK(ctx, hipMalloc((void**)&xm.d, x.size() * sizeof(uint16_t)));
     HIPCHK(ctx, hipMemcpy(xm.d, x.data(), x.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    int rp, kp;
+    split_matrix_h2(h.data(), R, Nc, x, &rp, &kp, &xm.hexp);
+    HIPCHK(ctx, hipMalloc((void**)&xm.dh, x.size() * sizeof(uint16_t)));
+    HIPCHK(ctx, hipMemcpy(xm.dh, x.data(), x.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     ctx->dct_x3[d] = xm;
   }
   *out = d;
@@ -371,6 +381,8 @@ void attach_x3(const dctae_ctx* ctx, GemmProblem& g) {
   g.Xs = x.d;
   g.xs_ld = x.Kp;
   g.xs_plane = (int64_t)x.Rp * x.Kp;
+  g.Xh = x.dh;
+  g.xh_exp = x.hexp;
 }
 
 int check_cfg(dctae_ctx* ctx, const dctae_fe_cfg* cfg) {
@@ -729,6 +741,8 @@ struct ChunkJob {
   int n_br[4], n_bc[4];
   int64_t max_hw;
   size_t lds_rows, lds_cols;
+  int64_t amax_off;   // k_gemm_h2: |max| bits per image (IPT, T) in the workspace, floats
+  int h2;             // the job's GEMMs on k_gemm_h2
 };
 
 struct EncPlan {
@@ -800,7 +814,10 @@ int dctae_ctx_destroy(dctae_ctx* ctx) {
   hipSetDevice(ctx->device);
   hipDeviceSynchronize();
   for (auto& kv : ctx->dct) hipFree(kv.second);
-  for (auto& kv : ctx->dct_x3) hipFree(kv.second.d);
+  for (auto& kv : ctx->dct_x3) {
+    hipFree(kv.second.d);
+    hipFree(kv.second.dh);
+  }
   if (ctx->ws) hipFree(ctx->ws);
   if (ctx->stage) hipFree(ctx->stage);
   if (ctx->plan_host) hipHostFree(ctx->plan_host);
@@ -885,6 +902,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "dec_cols_kernel" && (value == 1 || value == 2)) ctx->dec_cols_kernel = (int)value;
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
+  else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1083,6 +1101,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.max_T = std::max(j.max_T, d.T);
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
+    j.amax_off = wsf;
+    wsf += up(2ll * (j.i1 - j.i0));
     E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
     E.max_T = std::max(E.max_T, j.max_T);
   }
@@ -1127,6 +1147,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           GemmProblem g = gemm(ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1, CW, 0, K, 1,
                                ws + d.ws_t + par, (int64_t)d.Kw * d.H, d.Kw, 2, d.H, M, K, 3);
           attach_x3(ctx, g);
+          uint32_t* am = reinterpret_cast<uint32_t*>(ws + j.amax_off) + 2 * li;
+          g.amax = am;                               // k_rgb_to_ipt's |max| of the folded IPT
+          g.omax = d.plan_h < 0 ? am + 1 : nullptr;  // T's |max| for the column GEMM
           add_tiles(rt, (int)(probs.size() - p0), g);
           probs.push_back(g);
         }
@@ -1163,6 +1186,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
                                ws + d.ws_y + (int64_t)par * d.Kw, (int64_t)d.Kh * d.Kw, 2 * (int64_t)d.Kw, 1, M,
                                d.Kw, K, 3);
           attach_x3(ctx, g);
+          g.amax = reinterpret_cast<uint32_t*>(ws + j.amax_off) + 2 * li + 1;   // T's |max| (row GEMM / k_fold_t)
           add_tiles(ct, (int)(probs.size() - p0), g);
           probs.push_back(g);
         }
@@ -1201,6 +1225,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
         }
       }
     }
+    // k_gemm_h2 when every GEMM of the job has its shared matrix pre-split
+    j.h2 = ctx->gemm_x3 && ctx->gemm_h2 && probs.size() > p0;
+    for (size_t q = p0; q < probs.size(); ++q) j.h2 = j.h2 && probs[q].Xh != nullptr;
     j.gp_off = E.pb.add(probs.data() + p0, probs.size() - p0);
     if (ctx->xcd_order) {
       xcd_deal_tiles(rt, probs.data() + p0, 1);
@@ -1314,7 +1341,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
                              64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3 +
-                             4096 * ctx->cols512b + 8192 * ctx->rows_kernel,
+                             4096 * ctx->cols512b + 8192 * ctx->rows_kernel + 65536 * ctx->gemm_h2,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1399,15 +1426,24 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   TokenSinks skc = sk;   // the column kernels' sinks (codes come from the projection kernel)
   if (proj_w) skc.codes = nullptr;
   // row half / column half of a chunk job on a stream
+  auto gemm = [&](const ChunkJob& j, size_t tiles_off, int n_tiles, hipStream_t st, int share) {
+    if (j.h2)
+      launch_gemm_h2((const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share);
+    else
+      ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share);
+  };
   auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
+    uint32_t* amax = reinterpret_cast<uint32_t*>(ctx->ws + j.amax_off);
+    if (j.h2) hipMemsetAsync(amax, 0, 8 * (size_t)(j.i1 - j.i0), st);   // errors surface at hipGetLastError
     if (j.any_gemm_rows) {
       {
         Timer t(ctx, st, "rgb_to_ipt");
-        launch_rgb_to_ipt(dd, (const int2*)(pd + j.ipt_off), j.n_ipt, imgs->rgb_dev, ctx->ws, ctx->cm, st);
+        launch_rgb_to_ipt(dd, (const int2*)(pd + j.ipt_off), j.n_ipt, imgs->rgb_dev, ctx->ws, ctx->cm,
+                          j.h2 ? amax : nullptr, st);
       }
       Timer t(ctx, st, "gemm_rows");
-      ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.rows_t_off), j.n_rows_tiles, st, 1);
+      gemm(j, j.rows_t_off, j.n_rows_tiles, st, 1);
     }
     for (int l = 0; l < 4; ++l)
       if (j.n_br[l]) {
@@ -1437,10 +1473,11 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     if (j.any_gemm_cols) {
       if (j.fold_t) {
         Timer t(ctx, st, "fold_t");
-        launch_fold_t(dd, (const int32_t*)(pd + j.fold_off), j.n_fold, j.fold_max_hw, ctx->ws, st);
+        launch_fold_t(dd, (const int32_t*)(pd + j.fold_off), j.n_fold, j.fold_max_hw, ctx->ws,
+                      j.h2 ? reinterpret_cast<uint32_t*>(ctx->ws + j.amax_off) : nullptr, st);
       }
       Timer t(ctx, st, "gemm_cols");
-      ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.cols_t_off), j.n_cols_tiles, st, 2);
+      gemm(j, j.cols_t_off, j.n_cols_tiles, st, 2);
     }
     for (int l = 0; l < 4; ++l)
       if (j.n_bc[l]) {
@@ -1537,8 +1574,11 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   if (proj_w && E.n_tok > 0) {
     Timer t(ctx, s, "lfq_project_in");
     if ((rc = proj_scratch(ctx, lfq->codebook_dim * lfq->num_codebooks, PP))) return rc;
+    // the staged tokens are PatchNorm outputs, clamped to [min_val, max_val]
+    // (patchnorm.py:163): the fp16 projection's operand bound
+    const float xb = ctx->gemm_h2 ? std::max(std::fabs(norm->min_val), std::fabs(norm->max_val)) : 0.0f;
     launch_lfq_project_in16(sk.norm, E.n_tok, PP, proj_w, proj_b, lfq->codebook_dim, lfq->num_codebooks, sk.codes,
-                            ctx->proj_ws, s);
+                            ctx->proj_ws, s, xb);
   }
   if (full && E.n_img > sorted0) {
     Timer t(ctx, s, "sort_pack");
@@ -1934,7 +1974,7 @@ int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* i
   {
     Timer t(ctx, s, "lfq_project_out");
     launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
-                           ctx->proj_ws, s);
+                           ctx->proj_ws, s, nullptr, nullptr, nullptr, nullptr, 0.f, 0, 0, nullptr, ctx->gemm_h2 != 0);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
@@ -1962,7 +2002,7 @@ int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, con
     Timer t(ctx, s, "lfq_project_out");
     launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
                            ctx->proj_ws, s, channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h,
-                           max_patch_w, ctx->err_dev);
+                           max_patch_w, ctx->err_dev, ctx->gemm_h2 != 0);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);

@@ -30,6 +30,8 @@
 #include "dctae_launch.h"
 #include "dctae_device.h"
 
+#include <cmath>
+
 namespace dctae {
 
 namespace {
@@ -42,6 +44,7 @@ typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 hv8 __attribute__((ext_vector_type(8)));
 
 // LDS image of one operand tile: three bf16 pieces of ROWS x 32 k, rows of
 // 64 bytes, the 16-byte k group kq of row r at slot kq ^ swz(r).  With this
@@ -52,9 +55,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int swz(int r) { return ((r >> 1) ^ (r >> 2)) & 3; }
 __device__ __forceinline__ int lds_off(int r, int kq) { return r * XK + 8 * (kq ^ swz(r)); }
 
-template <int ROWS>
+template <int ROWS, int NP = 3>
 struct Pieces {
-  uint16_t p[3][ROWS * XK];
+  uint16_t p[NP][ROWS * XK];
 };
 
 // one fp32 operand (64 rows x depth k) of one channel, as this thread stages it
@@ -105,7 +108,7 @@ __device__ __forceinline__ f32x8 load_src(const Src& s, int k0, int K) {
 }
 
 template <int ROWS>
-__device__ __forceinline__ void split_store(Pieces<ROWS>& L, const Src& s, int rbase, f32x8 v) {
+__device__ __forceinline__ void split_store(Pieces<ROWS, 3>& L, const Src& s, int rbase, f32x8 v, float) {
   const bfv8 h0 = __builtin_convertvector(v, bfv8);
   const f32x8 r1 = v - __builtin_convertvector(h0, f32x8);
   const bfv8 h1 = __builtin_convertvector(r1, bfv8);
@@ -117,48 +120,71 @@ __device__ __forceinline__ void split_store(Pieces<ROWS>& L, const Src& s, int r
   *reinterpret_cast<bfv8*>(&L.p[2][o]) = h2;
 }
 
-// pre-split planes, ROWS rows: thread slot i = tid + 256 j -> (row i / 4, k group i % 4)
+// k_gemm_h2: v scaled by the exact power of two `scale` (so its largest
+// magnitude is below 2^14), then two fp16 pieces h0 = fp16(v), h1 = fp16(v - h0)
 template <int ROWS>
+__device__ __forceinline__ void split_store(Pieces<ROWS, 2>& L, const Src& s, int rbase, f32x8 v, float scale) {
+  const f32x8 vs = v * scale;
+  const hv8 h0 = __builtin_convertvector(vs, hv8);
+  const f32x8 r1 = vs - __builtin_convertvector(h0, f32x8);
+  const hv8 h1 = __builtin_convertvector(r1, hv8);
+  const int o = lds_off(rbase + s.row, s.kq);
+  *reinterpret_cast<hv8*>(&L.p[0][o]) = h0;
+  *reinterpret_cast<hv8*>(&L.p[1][o]) = h1;
+}
+
+// pre-split planes, ROWS rows: thread slot i = tid + 256 j -> (row i / 4, k group i % 4)
+template <int ROWS, int NP = 3>
 struct PreSplit {
-  u32x4 v[ROWS / 64][3];
+  u32x4 v[ROWS / 64][NP];
 };
 
 // buffer loads (a plain load through the pointer read from the problem struct
 // compiles to flat_load, which also counts in lgkmcnt: the first LDS wait of
 // the chunk's MFMAs then waited for these global loads too)
-template <int ROWS>
-__device__ __forceinline__ void load_pre(PreSplit<ROWS>& q, const GemmProblem& p, int r0, int k0) {
+template <int ROWS, int NP>
+__device__ __forceinline__ void load_pre(PreSplit<ROWS, NP>& q, const GemmProblem& p, int r0, int k0) {
   const int tid = threadIdx.x;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.Xs), 0, (int)(3 * p.xs_plane * 2), 0x00020000);
+  const uint16_t* planes = NP == 3 ? p.Xs : p.Xh;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(planes), 0, (int)(NP * p.xs_plane * 2), 0x00020000);
 #pragma unroll
   for (int j = 0; j < ROWS / 64; ++j) {
     const int o = ((r0 + 64 * j + (tid >> 2)) * p.xs_ld + k0 + 8 * (tid & 3)) * 2;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < NP; ++i)
       q.v[j][i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + (int)(i * p.xs_plane * 2), 0, 0));
   }
 }
 
-template <int ROWS>
-__device__ __forceinline__ void store_pre(Pieces<ROWS>& L, const PreSplit<ROWS>& q) {
+template <int ROWS, int NP>
+__device__ __forceinline__ void store_pre(Pieces<ROWS, NP>& L, const PreSplit<ROWS, NP>& q) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int j = 0; j < ROWS / 64; ++j) {
     const int o = lds_off(64 * j + (tid >> 2), tid & 3);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) *reinterpret_cast<u32x4*>(&L.p[i][o]) = q.v[j][i];
+    for (int i = 0; i < NP; ++i) *reinterpret_cast<u32x4*>(&L.p[i][o]) = q.v[j][i];
   }
 }
 
-template <int ROWS>
-__device__ __forceinline__ void read_frag(bf16x8 (&f)[3], const Pieces<ROWS>& L, int r, int kq) {
+template <int ROWS, int NP>
+__device__ __forceinline__ void read_frag(bf16x8 (&f)[NP], const Pieces<ROWS, NP>& L, int r, int kq) {
   const int o = lds_off(r, kq);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8*>(&L.p[q][o]);
+  for (int q = 0; q < NP; ++q) f[q] = *reinterpret_cast<const bf16x8*>(&L.p[q][o]);
+}
+
+// k_gemm_h2: the three fp16 products of piece order <= 1, small terms first
+__device__ __forceinline__ void mfma_pieces(floatx16& acc, const bf16x8 (&a)[2], const bf16x8 (&b)[2]) {
+  const hv8 a0 = __builtin_bit_cast(hv8, a[0]), a1 = __builtin_bit_cast(hv8, a[1]);
+  const hv8 b0 = __builtin_bit_cast(hv8, b[0]), b1 = __builtin_bit_cast(hv8, b[1]);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
 }
 
 // six split products, small terms first
-__device__ __forceinline__ void mfma6(floatx16& acc, const bf16x8 (&a)[3], const bf16x8 (&b)[3]) {
+__device__ __forceinline__ void mfma_pieces(floatx16& acc, const bf16x8 (&a)[3], const bf16x8 (&b)[3]) {
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
@@ -181,11 +207,27 @@ struct X3Shape {
   static constexpr int TM = SH == 2 ? 128 : 64, TN = SH == 1 ? 128 : 64;
 };
 
-template <int NC, int SH, bool PRE>
+template <int NC, int SH, bool PRE, int NP = 3>
 __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int tn,
-                                             Pieces<X3Shape<NC, SH>::TM> (&As)[X3Shape<NC, SH>::NA],
-                                             Pieces<X3Shape<NC, SH>::TN> (&Bs)[X3Shape<NC, SH>::NB]) {
+                                             Pieces<X3Shape<NC, SH>::TM, NP> (&As)[X3Shape<NC, SH>::NA],
+                                             Pieces<X3Shape<NC, SH>::TN, NP> (&Bs)[X3Shape<NC, SH>::NB]) {
   using S = X3Shape<NC, SH>;
+  static_assert(NP == 3 || (PRE && SH != 0), "k_gemm_h2: the shared operand comes pre-split");
+  // k_gemm_h2: the per-channel operand scaled by 2^ea so its |max| < 2^14 (fp16
+  // range with headroom; |max| from p.amax, a non-finite or zero max leaves it
+  // unscaled), the output unscaled by 2^-(ea + xh_exp): exact powers of two
+  float scale = 1.0f, unscale = 1.0f;
+  if constexpr (NP == 2) {
+    const uint32_t mb = *p.amax;
+    int ea = 0;
+    if (mb != 0u && mb < 0x7f800000u) {
+      int e;
+      frexpf(__uint_as_float(mb), &e);   // max in [2^(e-1), 2^e)
+      ea = min(max(14 - e, -100), 100);
+    }
+    scale = ldexpf(1.0f, ea);
+    unscale = ldexpf(1.0f, -(ea + p.xh_exp));
+  }
   constexpr int NA = S::NA, NB = S::NB, TM = S::TM, TN = S::TN;
   constexpr int BM = TM / 64, BN = TN / 64;   // 32 x 32 MFMA blocks per wave, per dimension
   constexpr bool preA = PRE && SH == 2, preB = PRE && SH == 1;
@@ -216,8 +258,8 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
         for (int r = 0; r < 16; ++r) acc[c][i][j][r] = 0.0f;
 
   f32x8 va[NA][SAM > 0 ? SAM : 1], vb[NB][SBN > 0 ? SBN : 1];
-  PreSplit<TM> qa;
-  PreSplit<TN> qb;
+  PreSplit<TM, NP> qa;
+  PreSplit<TN, NP> qb;
   auto load = [&](int k0) {
     if constexpr (preA) load_pre(qa, p, m0, k0);
 #pragma unroll
@@ -235,12 +277,12 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
 #pragma unroll
     for (int c = 0; c < NA; ++c)
 #pragma unroll
-      for (int j = 0; j < SAM; ++j) split_store(As[c], sa[c][j], 64 * j, va[c][j]);
+      for (int j = 0; j < SAM; ++j) split_store(As[c], sa[c][j], 64 * j, va[c][j], scale);
     if constexpr (preB) store_pre(Bs[0], qb);
 #pragma unroll
     for (int c = 0; c < NB; ++c)
 #pragma unroll
-      for (int j = 0; j < SBN; ++j) split_store(Bs[c], sb[c][j], 64 * j, vb[c][j]);
+      for (int j = 0; j < SBN; ++j) split_store(Bs[c], sb[c][j], 64 * j, vb[c][j], scale);
   };
   load(0);
   store();
@@ -257,7 +299,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
       // before the MFMAs that consume them capped the kernel at ~40 % of the
       // MFMA peak; with the reads removed it ran 1.54x faster.)
       constexpr int X = NB == 1 ? BN : BM;   // shared-side 32-blocks per wave
-      auto rd_shared = [&](bf16x8 (&f)[X][3], int st) {
+      auto rd_shared = [&](bf16x8 (&f)[X][NP], int st) {
         const int kq = 2 * st + half;
 #pragma unroll
         for (int x = 0; x < X; ++x) {
@@ -265,19 +307,19 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
           else read_frag(f[x], As[0], wm * (TM / 2) + 32 * x + l32, kq);
         }
       };
-      auto rd_own = [&](bf16x8 (&f)[3], int st, int c) {
+      auto rd_own = [&](bf16x8 (&f)[NP], int st, int c) {
         const int kq = 2 * st + half;
         if constexpr (NB == 1) read_frag(f, As[c], wm * (TM / 2) + l32, kq);
         else read_frag(f, Bs[c], wn * (TN / 2) + l32, kq);
       };
-      auto mm = [&](const bf16x8 (&sh)[X][3], const bf16x8 (&ow)[3], int c) {
+      auto mm = [&](const bf16x8 (&sh)[X][NP], const bf16x8 (&ow)[NP], int c) {
 #pragma unroll
         for (int x = 0; x < X; ++x) {
-          if constexpr (NB == 1) mfma6(acc[c][0][x], ow, sh[x]);
-          else mfma6(acc[c][x][0], sh[x], ow);
+          if constexpr (NB == 1) mfma_pieces(acc[c][0][x], ow, sh[x]);
+          else mfma_pieces(acc[c][x][0], sh[x], ow);
         }
       };
-      bf16x8 sh0[X][3], sh1[X][3], ow[2][3];
+      bf16x8 sh0[X][NP], sh1[X][NP], ow[2][NP];
       rd_shared(sh0, 0);
       rd_own(ow[0], 0, 0);
       __builtin_amdgcn_sched_barrier(0);
@@ -304,10 +346,10 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
         const int kq = 2 * s + half;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-          bf16x8 a[3], b[3];
+          bf16x8 a[NP], b[NP];
           read_frag(a, As[c], wm * 32 + l32, kq);
           read_frag(b, Bs[c], wn * 32 + l32, kq);
-          mfma6(acc[c][0][0], a, b);
+          mfma_pieces(acc[c][0][0], a, b);
         }
       }
     }
@@ -315,6 +357,28 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
     if (more) {
       store();
       __syncthreads();
+    }
+  }
+  if constexpr (NP == 2) {
+    uint32_t mx = 0;   // |max| of the outputs in uint order (NaN above Inf above finite)
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < BM; ++i)
+#pragma unroll
+        for (int j = 0; j < BN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            acc[c][i][j][r] *= unscale;
+            mx = max(mx, __float_as_uint(acc[c][i][j][r]) & 0x7fffffffu);
+          }
+    if (p.omax) {   // padded rows / columns accumulate zeros: no mask needed; one atomic per block
+      __shared__ uint32_t part[4];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+      if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mx;
+      __syncthreads();
+      if (threadIdx.x == 0) atomicMax(p.omax, max(max(part[0], part[1]), max(part[2], part[3])));
     }
   }
   // C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
@@ -374,6 +438,32 @@ __global__ __launch_bounds__(256, (SH == 0 && NC == 3) ? 1 : 2) void k_gemm_x3(c
     gemm_x3_body<NC, SH, false>(p, tm, tn, As, Bs);
 }
 
+// k_gemm_h2: the encode's DCT GEMMs on fp16 MFMAs with two-piece operands and
+// three products (a1 b0 + a0 b1 + a0 b0): each operand scaled by a power of
+// two into the fp16 range, so a piece pair carries 22 significant bits and
+// the dropped terms (a1 b1, the pieces' residuals) are <= 3 x 2^-22 |a b|
+// (~0.1 of the fp32 rounding of k_gemm_f32's sums; half the MFMAs of k_gemm_x3)
+template <int NC, int SH>
+__global__ __launch_bounds__(256, 2) void k_gemm_h2(const GemmProblem* __restrict__ probs,
+                                                  const TileRef* __restrict__ tiles) {
+  using S = X3Shape<NC, SH>;
+  __shared__ Pieces<S::TM, 2> As[S::NA];
+  __shared__ Pieces<S::TN, 2> Bs[S::NB];
+  const TileRef tr = tiles[blockIdx.x];
+  if (tr.problem < 0) return;   // padding of an XCD-dealt list
+  const GemmProblem p = probs[tr.problem];
+  const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
+  gemm_x3_body<NC, SH, true, 2>(p, tm, tn, As, Bs);
+}
+
+void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
+  if (n_tiles <= 0) return;
+  if (share == 1)
+    hipLaunchKernelGGL((k_gemm_h2<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else
+    hipLaunchKernelGGL((k_gemm_h2<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+}
+
 void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
   if (n_tiles <= 0) return;
   if (nc == 3 && share == 1)
@@ -418,6 +508,33 @@ void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, i
       out[o] = h0;
       out[plane + o] = h1;
       out[2 * plane + o] = host_bf16(r2);
+    }
+}
+
+// host: two fp16 planes [2][Rp][Kp] of the matrix scaled by 2^e, e chosen so
+// the largest |value| * 2^e lies in [2^13, 2^14) (k_gemm_h2's operand range)
+void split_matrix_h2(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp, int* e_out) {
+  *Rp = (R + 127) / 128 * 128;
+  *Kp = (K + XK - 1) / XK * XK;
+  const size_t plane = (size_t)*Rp * *Kp;
+  out.assign(2 * plane, 0);
+  float mx = 0.0f;
+  for (size_t i = 0; i < (size_t)R * K; ++i) mx = std::max(mx, std::fabs(m[i]));
+  int e = 0;
+  if (mx > 0.0f && std::isfinite(mx)) {
+    int ex;
+    std::frexp(mx, &ex);
+    e = 14 - ex;
+  }
+  *e_out = e;
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < K; ++k) {
+      const float v = std::ldexp(m[(size_t)r * K + k], e);
+      const _Float16 h0 = (_Float16)v;
+      const _Float16 h1 = (_Float16)(v - (float)h0);
+      const size_t o = (size_t)r * *Kp + k;
+      out[o] = __builtin_bit_cast(uint16_t, h0);
+      out[plane + o] = __builtin_bit_cast(uint16_t, h1);
     }
 }
 

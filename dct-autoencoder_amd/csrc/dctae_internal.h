@@ -66,6 +66,16 @@ struct GemmProblem {
   int32_t pad2;
   const uint16_t* Xs;
   int64_t xs_plane;  // Rp * xs_ld
+  // k_gemm_h2 (encode DCT GEMMs, option gemm_h2): the shared operand as two
+  // fp16 planes of the matrix scaled by 2^xh_exp [2][Rp][xs_ld]; amax = the
+  // |max| bits (uint order of |x|) of the per-channel operand, written by the
+  // kernel that produced it (k_rgb_to_ipt, k_fold_t, the row GEMM's omax);
+  // omax (nullable) receives the |max| bits of this GEMM's outputs
+  const uint16_t* Xh;
+  const uint32_t* amax;
+  uint32_t* omax;
+  int32_t xh_exp;
+  int32_t pad3;
 };
 
 // FFT-DCT plan for one length N (M = N/2 point complex FFT), dctae_fft.hip

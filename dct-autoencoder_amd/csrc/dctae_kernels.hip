@@ -61,9 +61,25 @@ void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_
 constexpr int kRgbGpt = 4;
 constexpr int kRgbGroups = 256 * kRgbGpt;
 
+// |max| of a 256-thread block's values in uint order (|x| bits: NaN above Inf
+// above finite) into *dst: one atomic per block (one per wave serialised
+// thousands of atomics on one address per image: +0.25 ms on config 4).
+// Every thread of the block must call it.
+__device__ __forceinline__ void block_amax(uint32_t m, uint32_t* dst) {
+  __shared__ uint32_t part[4];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = max(max(part[0], part[1]), max(part[2], part[3]));
+    if (m != 0u) atomicMax(dst, m);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                     const float* __restrict__ rgb, float* __restrict__ ws,
-                                                    ColorMats cm) {
+                                                    ColorMats cm, uint32_t* __restrict__ amax) {
   const int2 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
   const int W = d.W, H = d.H;
@@ -92,6 +108,7 @@ __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ 
 #pragma unroll
       for (int c = 0; c < 3; ++c) px[k][q][c] = src[c * hw + o[q]];
   }
+  uint32_t mx = 0;   // |max| of the values written (k_gemm_h2's operand scale)
 #pragma unroll
   for (int k = 0; k < kRgbGpt; ++k) {
     const int e = jb.y + (int)threadIdx.x + 256 * k;
@@ -121,15 +138,22 @@ __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ 
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       float* ro = dst + c * hw + (int64_t)y * W;
-      ro[x] = xp ? a[c] + b[c] : a[c];
-      if (xp) ro[Wh + x] = a[c] - b[c];
+      const float u0 = xp ? a[c] + b[c] : a[c], v0 = a[c] - b[c];
+      const float u1 = xp ? c2[c] + d2[c] : c2[c], v1 = c2[c] - d2[c];
+      ro[x] = u0;
+      if (xp) ro[Wh + x] = v0;
       if (yp) {
         float* r2 = dst + c * hw + (int64_t)y2 * W;
-        r2[x] = xp ? c2[c] + d2[c] : c2[c];
-        if (xp) r2[Wh + x] = c2[c] - d2[c];
+        r2[x] = u1;
+        if (xp) r2[Wh + x] = v1;
       }
+      mx = max(mx, __float_as_uint(u0) & 0x7fffffffu);
+      if (xp) mx = max(mx, __float_as_uint(v0) & 0x7fffffffu);
+      if (yp) mx = max(mx, __float_as_uint(u1) & 0x7fffffffu);
+      if (yp && xp) mx = max(mx, __float_as_uint(v1) & 0x7fffffffu);
     }
   }
+  if (amax) block_amax(mx, amax + 2 * jb.x);
 }
 
 // T (3, H, Kw) of the images whose columns run through the GEMM DCT but rows
@@ -137,34 +161,46 @@ __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ 
 // T[H-1-m] <- T[m] - T[H-1-m] for m < floor(H/2) (middle row of an odd H kept).
 // Launched over the listed images only (grid.y = list entries): on the
 // ragged config 4 a grid over every image spent 0.23 ms exiting blocks.
-__global__ void k_fold_t(const ImgDesc* __restrict__ imgs, const int32_t* __restrict__ list, float* __restrict__ ws) {
+__global__ void k_fold_t(const ImgDesc* __restrict__ imgs, const int32_t* __restrict__ list, float* __restrict__ ws,
+                         uint32_t* __restrict__ amax) {
   const ImgDesc d = imgs[list[blockIdx.y]];
   if (d.plan_h >= 0 || d.plan_w < 0) return;  // GEMM rows: folded by k_rgb_to_ipt
-  const int64_t n = (int64_t)(d.H / 2) * d.Kw;
+  const int Hh = (d.H + 1) / 2;                // the middle row of an odd H is kept (its |max| counts)
+  const int64_t n = (int64_t)Hh * d.Kw;
   float* t = ws + d.ws_t;
+  uint32_t mx = 0;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < 3 * n; e += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(e / n);
     const int64_t r = e - c * n;
     const int64_t m = r / d.Kw, kx = r - m * d.Kw;
     float* p0 = t + (int64_t)c * d.H * d.Kw + m * d.Kw + kx;
     float* p1 = t + (int64_t)c * d.H * d.Kw + (d.H - 1 - m) * d.Kw + kx;
-    const float a = *p0, b = *p1;
+    const float a = *p0;
+    if (p1 == p0) {
+      mx = max(mx, __float_as_uint(a) & 0x7fffffffu);
+      continue;
+    }
+    const float b = *p1;
     *p0 = a + b;
     *p1 = a - b;
+    mx = max(mx, max(__float_as_uint(a + b), __float_as_uint(a - b)) & 0x7fffffffu);
   }
+  if (amax) block_amax(mx, amax + 2 * list[blockIdx.y] + 1);
 }
 
-void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, hipStream_t s) {
+void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, uint32_t* amax,
+                   hipStream_t s) {
   if (n_list <= 0) return;
-  int gx = (int)std::min<int64_t>((3 * max_hw / 2 + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_fold_t, dim3(std::max(gx, 1), n_list), dim3(256), 0, s, imgs, list, ws);
+  // up to 64 blocks per image (grid-stride): each block ends in one atomic on its image's |max|
+  int gx = (int)std::min<int64_t>((3 * max_hw / 2 + 255) / 256, 64);
+  hipLaunchKernelGGL(k_fold_t, dim3(std::max(gx, 1), n_list), dim3(256), 0, s, imgs, list, ws, amax);
 }
 
 int rgb_to_ipt_groups_per_block() { return kRgbGroups; }
 
 void launch_rgb_to_ipt(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                       const ColorMats& cm, hipStream_t s) {
-  if (n_blocks > 0) hipLaunchKernelGGL(k_rgb_to_ipt, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, cm);
+                       const ColorMats& cm, uint32_t* amax, hipStream_t s) {
+  if (n_blocks > 0) hipLaunchKernelGGL(k_rgb_to_ipt, dim3(n_blocks), dim3(256), 0, s, imgs, blocks, rgb, ws, cm, amax);
 }
 
 // ipt (3,H,W) in place -> rgb written to out (3,H,W)

@@ -10,12 +10,15 @@ namespace dctae {
 
 void launch_synth(uint64_t seed, int64_t first, int32_t n_img, int32_t H, int32_t W, float* out, hipStream_t s);
 int rgb_to_ipt_groups_per_block();
+// amax (nullable): per job-local image, [2 i] receives the |max| bits of the folded IPT (k_gemm_h2)
 void launch_rgb_to_ipt(const ImgDesc* imgs, const int2* blocks, int n_blocks, const float* rgb, float* ws,
-                       const ColorMats& cm, hipStream_t s);
+                       const ColorMats& cm, uint32_t* amax, hipStream_t s);
 void launch_ipt_to_rgb(const ImgDesc* imgs, int n_img, int64_t max_hw, const float* ws, float* out,
                        const ColorMats& cm, hipStream_t s);
 void launch_color(const float* x, float* y, int64_t hw, int n_img, int dir, const ColorMats& cm, hipStream_t s);
-void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, hipStream_t s);
+// amax (nullable): [2 i + 1] receives the |max| bits of the folded T (k_gemm_h2)
+void launch_fold_t(const ImgDesc* imgs, const int32_t* list, int n_list, int64_t max_hw, float* ws, uint32_t* amax,
+                   hipStream_t s);
 // share: 1 = B shared by the channels (row transforms), 2 = A shared (column
 // transforms), 0 = from each problem's strides; must hold for every problem the
 // tiles reference (gemm_share of one of them)
@@ -25,6 +28,9 @@ void launch_gemm(int nc, const GemmProblem* probs, const TileRef* tiles, int n_t
 void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share = 0);
 // three bf16 planes [3][Rp][Kp] of a row-major fp32 matrix (GemmProblem::Xs)
 void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp);
+// the encode's DCT GEMMs on fp16 MFMAs, two-piece scaled operands (k_gemm_h2; 3 channels, share 1 or 2)
+void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share);
+void split_matrix_h2(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp, int* e_out);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
@@ -43,11 +49,12 @@ size_t lfq_proj_scratch_bytes(int N, int K);
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                            float scale, int64_t* idx, uint16_t* wsp, hipStream_t s);
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                             uint16_t* idx, uint16_t* wsp, hipStream_t s);
+                             uint16_t* idx, uint16_t* wsp, hipStream_t s,
+                             float x_bound = 0.f);
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                             float scale, float* out, uint16_t* wsp, hipStream_t s, const int64_t* ch = nullptr,
                             const int64_t* pos = nullptr, const float* med = nullptr, const float* nb = nullptr,
-                            float eps = 0.f, int maxph = 0, int maxpw = 0, int* err = nullptr);
+                            float eps = 0.f, int maxph = 0, int maxpw = 0, int* err = nullptr, bool h2 = true);
 // VectorQuantize inference (dctae_vq.hip)
 void launch_vq_bias(float* y, const float* bias, int64_t n, int cols, const uint8_t* mask, const float* orig,
                     hipStream_t s);

@@ -22,6 +22,8 @@
 #include "dctae_device.h"
 #include "dctae_launch.h"
 
+#include <cmath>
+
 namespace dctae {
 
 namespace {
@@ -47,6 +49,7 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bfv8 __attribute__((ext_vector_type(8)));
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 hv8 __attribute__((ext_vector_type(8)));
 
 // LDS image of a 32-k chunk: bf16 pieces of R rows, 64-byte rows, 16-byte k
 // group kq of row r at slot kq ^ swz(r) (conflict-free for the fragment reads
@@ -69,28 +72,47 @@ __device__ __forceinline__ void split8(uint16_t* planes, int plane, int o, f32x8
   }
 }
 
+// the fp16 form (H2): v scaled by the power of two `sc` into [2^13, 2^14) at
+// most, NPC pieces (2: v = p0 + p1 to 22 bits; 1: exact, e.g. +-scale codes)
+template <int NPC>
+__device__ __forceinline__ void split8h(uint16_t* planes, int plane, int o, f32x8 v, float sc) {
+  const f32x8 vs = v * sc;
+  const hv8 h0 = __builtin_convertvector(vs, hv8);
+  *reinterpret_cast<hv8*>(planes + o) = h0;
+  if constexpr (NPC > 1)
+    *reinterpret_cast<hv8*>(planes + plane + o) = __builtin_convertvector(vs - __builtin_convertvector(h0, f32x8), hv8);
+}
+
 // Split-precision GEMM on the bf16 MFMA: A (tokens or +-scale codes) and W are
 // split into three bf16 pieces each and the product keeps the six terms of
 // piece order <= 2 (a0 b0 + a0 b1 + a1 b0 + a1 b1 + a0 b2 + a2 b0, fp32
 // accumulation; the dropped terms are ~2^-24 |a b|: fp32-level accuracy, as
 // k_gemm_x3).  A1: A is exact in bf16 (mode 1 with a bf16-exact scale: +-scale
 // codes), one piece, three products.
-template <int NT, int MODE, int WB, bool A1>
-__global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
+// H2: the fp16 form -- A and W scaled by powers of two into the fp16 range
+// (A by a_scale from the caller's bound on |A|, W by 2^w_exp[0] from
+// k_split_w_h2), two pieces each (A1: one), three products (A1: two) on
+// v_mfma_f32_16x16x32_f16; the dropped terms are <= 3 x 2^-22 |a w|, the
+// accumulator is unscaled exactly before the bias
+template <int NT, int MODE, int WB, bool A1, bool H2>
+__device__ __forceinline__ void lfq_proj_body(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ w,
                                                  const float* __restrict__ bias, int cd, int ncb, float scale,
                                                  int64_t* __restrict__ idx_out, float* __restrict__ out,
                                                  uint16_t* __restrict__ idx16, InvNorm inv,
-                                                 const uint16_t* __restrict__ wsp, int Kp) {
+                                                 const uint16_t* __restrict__ wsp, int Kp, float a_scale,
+                                                 const int* __restrict__ w_exp) {
   constexpr int MT = 1;                            // 16-token M tiles per wave
   constexpr int kThr = 64 * WB;                    // WB waves per block
   constexpr int kTok = kTokW * WB * MT;            // tokens per block
   constexpr int NP = NT * 16;                      // padded output features
-  constexpr int NPA = A1 ? 1 : 3;                  // A pieces
-  constexpr int kPA = kTok * kKc, kPW = NP * kKc;  // plane sizes (bf16)
+  constexpr int NPA = A1 ? 1 : (H2 ? 2 : 3);       // A pieces
+  constexpr int NPW = H2 ? 2 : 3;                  // W pieces
+  constexpr int kPA = kTok * kKc, kPW = NP * kKc;  // plane sizes (16-bit elements)
   static_assert(kThr == 4 * kTok, "A staging: one 8-k group per thread");
   __shared__ __attribute__((aligned(16))) uint16_t As[NPA * kPA];
-  __shared__ __attribute__((aligned(16))) uint16_t Ws[3 * kPW];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[NPW * kPW];
+  const float unscale = H2 ? ldexpf(1.0f / a_scale, -w_exp[0]) : 1.0f;
   __shared__ int64_t Tb[MODE == 1 ? 32 : 1];   // mode 1 + inverse: table rows of a round's 32 tokens
   __shared__ int32_t Ix[MODE == 1 ? kTok * 32 : 1];   // mode 1: the block's indices (ncb <= 32)
   __shared__ uint32_t Msk[MODE == 0 ? WB * 16 * MT * (NT + 3) : 1];  // mode 0: sign pieces [wave][token][tile]
@@ -118,9 +140,9 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
   const int at = tid >> 2, aq = tid & 3;
   // W: the three pre-split bf16 planes [3][NP][Kp] (k_split_w), 16-byte pieces
   constexpr int WG = (NP * 4 + kThr - 1) / kThr;   // W 8-k groups per thread and chunk
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wsp), 0, 3 * NP * Kp * 2, 0x00020000);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wsp), 0, NPW * NP * Kp * 2, 0x00020000);
   f32x8 ra;
-  u32x4 rw[WG][3];
+  u32x4 rw[WG][NPW];
   auto load = [&](int k0) {
     const int k = k0 + 8 * aq;
     if (MODE == 0) {
@@ -143,18 +165,21 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
       const int g = tid + kThr * i;
       const int o = g < NP * 4 ? ((g >> 2) * Kp + k0 + 8 * (g & 3)) * 2 : 0x7ffffff0;
 #pragma unroll
-      for (int pc = 0; pc < 3; ++pc)
+      for (int pc = 0; pc < NPW; ++pc)
         rw[i][pc] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, o + pc * NP * Kp * 2, 0, 0));
     }
   };
   auto store = [&]() {
-    split8<NPA>(As, kPA, poff(at, aq), ra);
+    if constexpr (H2)
+      split8h<NPA>(As, kPA, poff(at, aq), ra, a_scale);
+    else
+      split8<NPA>(As, kPA, poff(at, aq), ra);
 #pragma unroll
     for (int i = 0; i < WG; ++i) {
       const int g = tid + kThr * i;
       if (g < NP * 4) {
 #pragma unroll
-        for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<u32x4*>(&Ws[pc * kPW + poff(g >> 2, g & 3)]) = rw[i][pc];
+        for (int pc = 0; pc < NPW; ++pc) *reinterpret_cast<u32x4*>(&Ws[pc * kPW + poff(g >> 2, g & 3)]) = rw[i][pc];
       }
     }
   };
@@ -171,18 +196,25 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
     for (int pc = 0; pc < NPA; ++pc) a[pc] = *reinterpret_cast<const bf16x8*>(&As[pc * kPA + poff(wave * kTokW + r, q)]);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      bf16x8 b[3];
+      bf16x8 b[NPW];
 #pragma unroll
-      for (int pc = 0; pc < 3; ++pc) b[pc] = *reinterpret_cast<const bf16x8*>(&Ws[pc * kPW + poff(16 * t + r, q)]);
+      for (int pc = 0; pc < NPW; ++pc) b[pc] = *reinterpret_cast<const bf16x8*>(&Ws[pc * kPW + poff(16 * t + r, q)]);
       floatx4& c = acc[0][t];
-      if constexpr (!A1) {
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+      if constexpr (H2) {
+        const hv8 a0 = __builtin_bit_cast(hv8, a[0]), b0 = __builtin_bit_cast(hv8, b[0]), b1 = __builtin_bit_cast(hv8, b[1]);
+        if constexpr (!A1) c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(hv8, a[NPA - 1]), b0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0, c, 0, 0, 0);
+      } else {
+        if constexpr (!A1) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[NPA - 1], b[0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+        }
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[NPW - 1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
       }
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
     }
     __syncthreads();
     if (more) {
@@ -203,7 +235,7 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
         const float bb = (bias && col < N) ? bias[col] : 0.f;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float h = acc[m][t][v] + bb;
+          const float h = acc[m][t][v] * unscale + bb;
           const uint64_t mk = __ballot(col < N && h > 0.0f);   // lfq.py:175 (NaN -> False)
           if (lane < 4) msk[(4 * lane + v) * (NT + 3) + t] = (uint32_t)(mk >> (16 * lane)) & 0xffffu;
         }
@@ -248,7 +280,7 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
               if (col >= N) continue;
               const float bb = bias ? bias[col] : 0.f;
 #pragma unroll
-              for (int v = 0; v < 4; ++v) tl[(4 * q + v) * N + col] = acc[m][t][v] + bb;
+              for (int v = 0; v < 4; ++v) tl[(4 * q + v) * N + col] = acc[m][t][v] * unscale + bb;
             }
           }
           const int64_t rt0 = tok0 + (int64_t)rd * WPR * kTokW;   // first token of the round
@@ -290,12 +322,31 @@ __global__ __launch_bounds__(64 * WB) void k_lfq_proj(const float* __restrict__ 
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int64_t row = wt0 + 4 * q + v;
-            if (row < n) out[row * N + col] = acc[m][t][v] + bb;
+            if (row < n) out[row * N + col] = acc[m][t][v] * unscale + bb;
           }
         }
       }
     }
   }
+}
+
+#define DCTAE_LFQP_PARAMS                                                                                         \
+  const float *__restrict__ x, const int64_t *__restrict__ idx_in, int64_t n, int K, int N, const float *__restrict__ w, \
+      const float *__restrict__ bias, int cd, int ncb, float scale, int64_t *__restrict__ idx_out,                    \
+      float *__restrict__ out, uint16_t *__restrict__ idx16, InvNorm inv, const uint16_t *__restrict__ wsp, int Kp,     \
+      float a_scale, const int *__restrict__ w_exp
+#define DCTAE_LFQP_ARGS x, idx_in, n, K, N, w, bias, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp, a_scale, w_exp
+
+template <int NT, int MODE, int WB, bool A1>
+__global__ __launch_bounds__(64 * WB) void k_lfq_proj(DCTAE_LFQP_PARAMS) {
+  lfq_proj_body<NT, MODE, WB, A1, false>(DCTAE_LFQP_ARGS);
+}
+
+// the fp16 form at 4 waves per SIMD (two 512-thread blocks per CU): its
+// projection-out body compiled to 130 VGPRs, one block per CU, 1.5x slower
+template <int NT, int MODE, int WB, bool A1>
+__global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(4))) void k_lfq_proj_h2(DCTAE_LFQP_PARAMS) {
+  lfq_proj_body<NT, MODE, WB, A1, true>(DCTAE_LFQP_ARGS);
 }
 
 // W (N x K fp32, row-major) -> three bf16 planes [3][NP][Kp], zero padded
@@ -315,12 +366,48 @@ __global__ void k_split_w(const float* __restrict__ w, int N, int K, int NP, int
   }
 }
 
-template <int MODE, int WB, bool A1>
+// W (N x K fp32) -> two fp16 planes [2][NP][Kp] of W 2^e, e from |max W| so
+// the largest piece lies in [2^13, 2^14) (0 for an all-zero or non-finite W),
+// e stored after the planes: one 1024-thread block (N x K <= 256 x 256)
+__global__ __launch_bounds__(1024) void k_split_w_h2(const float* __restrict__ w, int N, int K, int NP, int Kp,
+                                                     uint16_t* __restrict__ ws) {
+  __shared__ uint32_t part[16];
+  __shared__ int ex;
+  uint32_t m = 0;
+  for (int e = threadIdx.x; e < N * K; e += 1024) m = max(m, __float_as_uint(w[e]) & 0x7fffffffu);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; ++i) m = max(m, part[i]);
+    int e = 0;
+    if (m != 0u && m < 0x7f800000u) {
+      frexpf(__uint_as_float(m), &e);
+      e = 14 - e;
+    }
+    ex = e;
+  }
+  __syncthreads();
+  const float sc = ldexpf(1.0f, ex);
+  const int64_t plane = (int64_t)NP * Kp;
+  for (int64_t e = threadIdx.x; e < plane; e += 1024) {
+    const int row = (int)(e / Kp), k = (int)(e - (int64_t)row * Kp);
+    const float v = (row < N && k < K ? w[(int64_t)row * K + k] : 0.f) * sc;
+    const _Float16 h0 = (_Float16)v;
+    ws[e] = __builtin_bit_cast(uint16_t, h0);
+    ws[plane + e] = __builtin_bit_cast(uint16_t, (_Float16)(v - (float)h0));
+  }
+  if (threadIdx.x == 0) *reinterpret_cast<int*>(ws + 2 * plane) = ex;
+}
+
+template <int MODE, int WB, bool A1, bool H2>
 void launch_nt(int nt, dim3 g, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-               uint16_t* idx16, InvNorm inv, const uint16_t* wsp, int Kp) {
+               uint16_t* idx16, InvNorm inv, const uint16_t* wsp, int Kp, float a_scale, const int* w_exp) {
 #define DCTAE_LFQP(T) \
-  case T: hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB, A1>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp); break;
+  case T: if (H2) hipLaunchKernelGGL((k_lfq_proj_h2<T, MODE, WB, A1>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp, a_scale, w_exp); \
+          else hipLaunchKernelGGL((k_lfq_proj<T, MODE, WB, A1>), g, dim3(64 * WB), 0, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp, a_scale, w_exp); break;
   switch (nt) {
     DCTAE_LFQP(1) DCTAE_LFQP(2) DCTAE_LFQP(3) DCTAE_LFQP(4) DCTAE_LFQP(5) DCTAE_LFQP(6) DCTAE_LFQP(7)
     DCTAE_LFQP(8) DCTAE_LFQP(9) DCTAE_LFQP(10) DCTAE_LFQP(11) DCTAE_LFQP(12) DCTAE_LFQP(13)
@@ -337,12 +424,39 @@ size_t lfq_proj_scratch_bytes(int N, int K) {
   return 3 * NP * Kp * sizeof(uint16_t);
 }
 
+// fp16 form (H2) for mode 0 when the caller bounds |x| (a_bound > 0, e.g.
+// the PatchNorm clamp of the fused encode), for mode 1 when +-scale is exact
+// in fp16; otherwise the split-bf16 form
 template <int MODE>
 static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                         const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-                        uint16_t* wsp, uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}) {
-  // W pre-split once per call (a few microseconds: N x K <= 256 x 256)
+                        uint16_t* wsp, uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}, float a_bound = 0.f) {
   const int NP = nt * 16, Kp = (K + 31) / 32 * 32;
+  const dim3 g((unsigned)((n + 127) / 128));
+  bool h2 = false;
+  float a_scale = 1.0f;
+  if (MODE == 0 && a_bound > 0.0f && std::isfinite(a_bound)) {
+    int e;
+    std::frexp(a_bound, &e);
+    a_scale = std::ldexp(1.0f, 14 - e);
+    h2 = true;
+  }
+  if (MODE == 1 && a_bound > 0.0f) {   // a_bound: the caller allows the fp16 form
+    const float sh = (float)(_Float16)scale;
+    h2 = sh == scale && std::fabs(scale) >= 6.103515625e-05f && std::fabs(scale) <= 16384.0f;
+  }
+  if (h2) {
+    const int* w_exp = reinterpret_cast<const int*>(wsp + 2 * (size_t)NP * Kp);
+    hipLaunchKernelGGL(k_split_w_h2, dim3(1), dim3(1024), 0, s, w, N, K, NP, Kp, wsp);
+    if constexpr (MODE == 1)
+      launch_nt<MODE, 8, true, true>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp,
+                                     Kp, 1.0f, w_exp);
+    else
+      launch_nt<MODE, 8, false, true>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv,
+                                      wsp, Kp, a_scale, w_exp);
+    return;
+  }
+  // W pre-split once per call (a few microseconds: N x K <= 256 x 256)
   hipLaunchKernelGGL(k_split_w, dim3((NP * Kp + 255) / 256), dim3(256), 0, s, w, N, K, NP, Kp, wsp);
   // 8 waves x 16 tokens per block (the W chunk in LDS shared by 128 tokens).
   // Measured with the fp32 MFMA (v_mfma_f32_16x16x4_f32) on 3,145,728 tokens
@@ -352,14 +466,15 @@ static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* id
   // Mode 1's A (+-scale) is exact in bf16 when scale is: one A piece
   uint32_t sb;
   memcpy(&sb, &scale, 4);
-  const dim3 g((unsigned)((n + 127) / 128));
   if constexpr (MODE == 1) {
     if ((sb & 0xffffu) == 0) {
-      launch_nt<MODE, 8, true>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp);
+      launch_nt<MODE, 8, true, false>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp,
+                                      Kp, 1.0f, nullptr);
       return;
     }
   }
-  launch_nt<MODE, 8, false>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp, Kp);
+  launch_nt<MODE, 8, false, false>(nt, g, s, x, idx_in, n, K, N, w, b, cd, ncb, scale, idx_out, out, idx16, inv, wsp,
+                                   Kp, 1.0f, nullptr);
 }
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
@@ -370,19 +485,21 @@ void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, con
 }
 
 // the same into the encode's u16 token staging (cd <= 16)
+// x_bound > 0: |x| <= x_bound (NaN aside), the fp16 form
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                             uint16_t* idx, uint16_t* wsp, hipStream_t s) {
+                             uint16_t* idx, uint16_t* wsp, hipStream_t s, float x_bound) {
   if (n <= 0) return;
-  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, nullptr, nullptr, wsp, idx);
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, nullptr, nullptr, wsp, idx,
+                 InvNorm{}, x_bound);
 }
 
 // indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                             float scale, float* out, uint16_t* wsp, hipStream_t s, const int64_t* ch, const int64_t* pos,
-                            const float* med, const float* nb, float eps, int maxph, int maxpw, int* err) {
+                            const float* med, const float* nb, float eps, int maxph, int maxpw, int* err, bool h2) {
   if (n <= 0) return;
   launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out, wsp, nullptr,
-                 InvNorm{ch, pos, med, nb, eps, maxph, maxpw, err});
+                 InvNorm{ch, pos, med, nb, eps, maxph, maxpw, err}, h2 ? 1.0f : 0.0f);
 }
 
 }  // namespace dctae

@@ -564,6 +564,37 @@ def test_224_kernels_odd_shapes_vs_oracle(fe, pn, lfq, ref_tables, shape):
     _encode_vs_oracle(fe, pn, lfq, ref_tables, rng.synth_images(43, [shape] * 3), CFG, f"224 kernels {shape}")
 
 
+def test_gemm_h2_accuracy_vs_oracle_and_x3(fe):
+    """The encode's DCT GEMMs on k_gemm_h2 (fp16 MFMA, two-piece operands
+    scaled into the fp16 range, three products; default) against the oracle's
+    tokens and against k_gemm_x3 (split-bf16, six products; gemm_h2=0) on
+    sides without an FFT plan (GEMM rows and columns, odd and even folds, FFT
+    rows + GEMM columns through k_fold_t, sides below 32): tokens within
+    5e-7 x max|Y| of the oracle (the global tolerance is 2e-6)."""
+    ops = _ops()
+    xs = rng.synth_images(47, [(333, 517), (1021, 997), (512, 511), (448, 449), (15, 17), (256, 1000), (1000, 97)])
+    outs = {}
+    for h2 in (1, 0):
+        ops.set_option("gemm_h2", h2)
+        try:
+            outs[h2] = [fe.preprocess(torch.from_numpy(x).to(DEV)) for x in xs]
+        finally:
+            ops.set_option("gemm_h2", 1)
+    worst = {0: 0.0, 1: 0.0}
+    for n, x_np in enumerate(xs):
+        toks, pos, ch, _ = _oracle_tokens(x_np)
+        omap = {_key(c, p): i for i, (p, c) in enumerate(zip(pos.tolist(), ch.tolist()))}
+        ymax = float(toks.abs().max())
+        for h2 in (1, 0):
+            out = outs[h2][n]
+            idx = torch.tensor([omap[_key(c, p)] for p, c in zip(out["positions"].cpu().tolist(),
+                                                                 out["channels"].cpu().tolist())])
+            err = float((out["patches"].cpu() - toks[idx]).abs().max()) / ymax
+            worst[h2] = max(worst[h2], err)
+    print(f"[gemm tokens vs oracle, / max|Y|] h2 {worst[1]:.3g}  x3 {worst[0]:.3g}")
+    assert worst[1] <= 5e-7, worst
+
+
 @pytest.mark.parametrize("shape", [(333, 517), (1021, 997), (97, 1000), (1000, 97), (30, 997), (997, 30)])
 def test_bluestein_matches_gemm_path(fe, pn, lfq, shape):
     """Sides without a Makhoul plan: the Bluestein FFT (option bluestein=1)

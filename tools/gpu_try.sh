@@ -19,6 +19,12 @@ for opts in "$@"; do
   for o in $opts; do
     case $o in lib=*) export DCTAE_LIBRARY="${o#lib=}";; *) args="$args --opt $o";; esac
   done
+  if [ -n "${LFQP:-}" ]; then   # the LFQ-projection leg only (tools/lfqp_try.py)
+    timeout -k 10 300 python tools/lfqp_try.py $args > gpurun_out/try_lfqp.log 2>&1
+    rc=$?; echo "=== lfqp [$opts] rc=$rc"; tail -1 gpurun_out/try_lfqp.log
+    [ $rc -ne 0 ] && exit $rc
+    continue
+  fi
   if [ -n "${CFG4:-}" ]; then   # config 4 only (tools/cfg4_try.py)
     timeout -k 10 300 python tools/cfg4_try.py $args > gpurun_out/try_cfg4.log 2>&1
     rc=$?; echo "=== cfg4 [$opts] rc=$rc"; tail -1 gpurun_out/try_cfg4.log
