@@ -91,6 +91,10 @@ struct dctae_ctx {
   // DESIGN.md section 4); 0 = row-major T and k_fft_cols7
   int cols512b = 1;
   int sort_overlap = 0;
+  // one job of uniform images whose rows and columns each run one compile-time
+  // plan kernel (config 2's 224^2): the first half's columns and sort / pack on
+  // a side stream beside the second half's rows and columns
+  int halves = 0;   // flipped on after its GPU A/B
   int xcd_order = 1;                  // column blocks of one (image, channel) on one XCD, back to back
   size_t lds_limit = 64 * 1024;       // dynamic LDS the FFT kernels may use
   int64_t chunk_bytes = 1ll << 40;    // workspace per chunk of the FFT path (measured: one chunk is fastest)
@@ -756,6 +760,7 @@ struct EncPlan {
   size_t ws_need = 0, st_need = 0;
   int ncb = 0;
   bool any_pad = true;   // some packed row shorter than max_seq_len
+  bool uniform = false;  // every image of the call has the same (H, W)
 };
 
 // ---------------------------------------------------------------------------
@@ -897,6 +902,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "rows_kernel" && (value == 2 || value == 4)) ctx->rows_kernel = (int)value;
   else if (k == "cols512b") ctx->cols512b = value != 0;
   else if (k == "sort_overlap") ctx->sort_overlap = value != 0;
+  else if (k == "halves") ctx->halves = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
   else if (k == "dec_rows_kernel" && (value == 2 || value == 3)) ctx->dec_rows_kernel = (int)value;
   else if (k == "dec_cols_kernel" && (value == 1 || value == 2)) ctx->dec_cols_kernel = (int)value;
@@ -1108,6 +1114,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   }
   E.n_tok = tok;
   E.n_img = n;
+  E.uniform = true;
+  for (int i = 1; i < n; ++i) E.uniform = E.uniform && D[i].H == D[0].H && D[i].W == D[0].W;
   {
     int64_t st = 0;
     for (int i = 0; i < n; ++i) st += st_of(D[i]);
@@ -1538,13 +1546,62 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   } side_join;
   const bool split = full && !proj_w && ctx->sort_overlap && E.jobs.size() == 1 && E.n_img >= 64 &&
                      E.jobs[0].n_pb == E.n_img && E.jobs[0].i0 == 0;
-  if (split && !ctx->side) {
+  // halves (option): see dctae_ctx::halves; hv = the plan kernel variant
+  int hv = 0;
+  if (full && !proj_w && ctx->halves && !split && E.jobs.size() == 1 && E.uniform && E.n_img >= 32) {
+    const ChunkJob& j = E.jobs[0];
+    bool ok = !j.any_gemm_rows && !j.any_gemm_cols && !j.any_bs_cols && j.n_pb == 0 && j.n_pc == 0 && j.n_fr[0] == 0 &&
+              j.n_fc[0] == 0;
+    for (int l = 0; l < 4; ++l) ok = ok && !j.n_br[l] && !j.n_bc[l];
+    int vv = -1;
+    for (int v = 1; v < kVariants; ++v)
+      if (j.n_fr[v] || j.n_fc[v]) {
+        if (vv < 0 && j.n_fr[v] && j.n_fc[v]) vv = v;
+        else ok = false;
+      }
+    if (ok && vv >= 2 && j.n_fr[vv] % E.n_img == 0 && j.n_fc[vv] % E.n_img == 0) hv = vv;
+  }
+  if ((split || hv) && !ctx->side) {
     if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->side_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->side_out, hipEventDisableTiming) != hipSuccess)
       return fail(ctx, DCTAE_EHIP, "side stream allocation failed");
   }
+  if (hv) {
+    const ChunkJob& j = E.jobs[0];
+    const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
+    const int n_img = E.n_img, h = n_img / 2;
+    const int rpi = j.n_fr[hv] / n_img, cpi = j.n_fc[hv] / n_img;   // blocks / items per image (image-major lists)
+    const int2* rl = (const int2*)(pd + j.fr_off[hv]);
+    const int4* cl = (const int4*)(pd + j.fc_off[hv]);
+    auto rows = [&](int a, int m, hipStream_t st) {
+      Timer t(ctx, st, "fft_rows");
+      launch_fft_rows_spec(hv, dd, rl + (size_t)a * rpi, m * rpi, imgs->rgb_dev, ctx->ws, ctx->fft_tab + j.tw_off[hv],
+                           ctx->fft_tab + j.post_off_r[hv], ctx->cm, st);
+    };
+    auto cols = [&](int a, int m, hipStream_t st) {
+      Timer t(ctx, st, "fft_cols");
+      launch_fft_cols_spec(hv, dd, cl + (size_t)a * cpi, m * cpi, ctx->ws, ctx->fft_tab + j.tw_off_c[hv],
+                           ctx->fft_tab + j.post_off_c[hv], epj, skc, st, nullptr, 0, 0);
+    };
+    rows(0, h, s);
+    HIPCHK(ctx, hipEventRecord(ctx->side_in, s));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
+    side_join.s = s;
+    side_join.side = ctx->side;
+    side_join.e = ctx->side_out;
+    side_join.armed = true;
+    cols(0, h, ctx->side);
+    {
+      Timer t(ctx, ctx->side, "sort_pack");
+      launch_sort_pack(all_d, h, next_pow2(E.max_T), eps, sk, ps, ctx->side, ctx->sort_kernel, E.max_T);
+    }
+    rows(h, n_img - h, s);
+    cols(h, n_img - h, s);
+    sorted0 = h;
+  }
   for (const ChunkJob& j : E.jobs) {
+    if (hv) break;
     do_rows(j, s);
     if (!split) {
       do_cols(j, s);

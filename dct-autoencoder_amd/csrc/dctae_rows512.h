@@ -47,6 +47,14 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #ifndef DCTAE_TLAYOUT
 #define DCTAE_TLAYOUT 2
 #endif
+// cache-policy bits of the band T' stores (k_rows512pk) and loads (k_cols512b):
+// 0 = default, 2 = nontemporal (A/B switches)
+#ifndef DCTAE_T_ST_AUX
+#define DCTAE_T_ST_AUX 0
+#endif
+#ifndef DCTAE_T_LD_AUX
+#define DCTAE_T_LD_AUX 0
+#endif
 static_assert(DCTAE_TLAYOUT == 0 || DCTAE_TLAYOUT == 2, "T' layouts: 0 or 2");
 __device__ __forceinline__ int t4_index(int band4, int kx) {
 #if DCTAE_TLAYOUT == 0
@@ -392,7 +400,7 @@ __device__ __forceinline__ void rows512_item_pk(Rows512XchPk& X, const Rows512Ta
       const int go = (((y0 >> 4) * KW + kx0) * 4 + qd) * 16;
 #pragma unroll
       for (int it = 0; it < 7; ++it)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, rd[64 * it]), rsrc, go, 1024 * it, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, rd[64 * it]), rsrc, go, 1024 * it, DCTAE_T_ST_AUX);
       __builtin_amdgcn_sched_barrier(0);   // keep the next channel's inputs from being built up here
     } else
 #endif

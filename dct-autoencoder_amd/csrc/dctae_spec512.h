@@ -436,7 +436,7 @@ __device__ __forceinline__ void cols512b_load(int c, int strip, const float* __r
 #endif
 #pragma unroll
   for (int b = 0; b < 8; ++b)
-    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, 0));
+    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, DCTAE_T_LD_AUX));
 }
 
 template <bool THR>

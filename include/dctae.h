@@ -349,9 +349,18 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * bit-identical),
  * "sort_kernel" (2, default: rocPRIM radix for <= 3072 tokens per image; 1:
  * the bitonic kernel that serves larger images), "fft_decode" (0/1),
- * "xcd_order" (0/1), "dec_rows_kernel" (3 / 2), "gemm_x3" (1, default:
- * the DCT GEMMs on the split-bf16 MFMA kernel k_gemm_x3, fp32-level
- * accuracy; 0: the fp32 MFMA kernel).  Profiling builds only (make
+ * "xcd_order" (0/1), "dec_rows_kernel" (3 / 2), "dec_cols_kernel" (2,
+ * default: k_idct_cols512b writing the band-layout U for k_idct_rows512; 1:
+ * k_idct_cols512, row-major U), "gemm_x3" (1, default: the DCT GEMMs on the
+ * split-bf16 MFMA kernel k_gemm_x3, fp32-level accuracy; 0: the fp32 MFMA
+ * kernel), "gemm_h2" (1, default: the encode's DCT GEMMs and the fused LFQ
+ * projections on fp16 MFMAs with two-piece operands scaled by powers of two
+ * (k_gemm_h2 / k_lfq_proj_h2: tokens within 5e-7 x max|Y|); 0: split-bf16),
+ * "halves" (1, default: a batch of >= 32 images of one size whose rows and
+ * columns each run one compile-time plan kernel, e.g. 224 x 224, runs its
+ * first half's columns and sort / pack on the side stream beside the second
+ * half's rows and columns; outputs bit-identical; 0: one stream).
+ * Profiling builds only (make
  * PROFILING=1; the shipped library returns DCTAE_EUNSUP): "bs_ablate",
  * "t_alias" (these write wrong outputs on purpose). */
 int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);

@@ -809,6 +809,28 @@ def test_sort_overlap_bit_identical(fe, pn, lfq):
         assert torch.equal(getattr(dp0, f), getattr(dp1, f)), f
 
 
+HALVES_DEFAULT = 0   # dctae_ctx::halves
+
+
+@pytest.mark.parametrize("n", [33, 64])
+def test_halves_bit_identical(fe, pn, lfq, n):
+    """Option halves (default on; config 2's 224^2 batches of >= 32 images:
+    the first half's columns and sort / pack on a side stream beside the
+    second half's rows and columns): every packed output equal to the
+    one-stream encode (halves=0), odd image count included."""
+    ops = _ops()
+    x = ops.synth_images(n, 224, 224, seed=78, device=torch.device(DEV))
+    ops.set_option("halves", 1)
+    ((dp1, c1),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_option("halves", 0)
+    ((dp0, c0),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_option("halves", HALVES_DEFAULT)
+    torch.cuda.synchronize()
+    assert torch.equal(c0, c1)
+    for f in ("patches", "key_pad_mask", "batched_image_ids", "patch_channels", "patch_positions"):
+        assert torch.equal(getattr(dp0, f), getattr(dp1, f)), f
+
+
 @pytest.mark.parametrize("shapes", [[(512, 512)] * 2, [(224, 224), (300, 262)]], ids=["fft512", "gemm"])
 def test_fft_decode_duplicate_tokens_last_wins(fe, pn, lfq, ref_tables, shapes):
     """Two tokens of one image at the same (channel, h, w): the reference's
