@@ -31,12 +31,14 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--per-call", type=int, required=True, help="kernels per call")
     ap.add_argument("--calls", type=int, default=20)
-    ap.add_argument("--match", default="", help="only kernels whose name contains this")
+    ap.add_argument("--match", action="append", default=[], help="only kernels whose name contains one of these")
+    ap.add_argument("--first", type=int, default=None,
+                    help="take the calls starting at this call index (default: the last --calls calls)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
-    rows = [r for r in load(args.csv) if args.match in r[2]]
+    rows = [r for r in load(args.csv) if not args.match or any(m in r[2] for m in args.match)]
     n = args.per_call * args.calls
-    rows = rows[-n:]
+    rows = rows[-n:] if args.first is None else rows[args.per_call * args.first:args.per_call * args.first + n]
     per_kernel, gaps_in, gaps_between, spans = {}, [], [], []
     for c in range(args.calls):
         call = rows[c * args.per_call:(c + 1) * args.per_call]
