@@ -90,6 +90,8 @@ struct dctae_ctx {
   // the columns run k_cols512b (16-byte loads,
   // DESIGN.md section 4); 0 = row-major T and k_fft_cols7
   int cols512b = 1;
+  // k_cols512b's codes-only encodes on k_cols512w (two strips per 7-wave block, no repeated column lanes)
+  int cols_wide = 0;   // measured slower
   int sort_overlap = 0;
   // one job of uniform images whose rows and columns each run one compile-time
   // plan kernel (config 2's 224^2): the first half's columns and sort / pack on
@@ -901,6 +903,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
 #endif
   else if (k == "rows_kernel" && (value == 2 || value == 4)) ctx->rows_kernel = (int)value;
   else if (k == "cols512b") ctx->cols512b = value != 0;
+  else if (k == "cols_wide") ctx->cols_wide = value != 0;
   else if (k == "sort_overlap") ctx->sort_overlap = value != 0;
   else if (k == "halves") ctx->halves = value != 0;
   else if (k == "fft_decode") ctx->fft_decode = value != 0;
@@ -1505,7 +1508,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     if (j.n_pb) {
       Timer t(ctx, st, "fft_cols");
       launch_cols512b(dd, (const int*)(pd + j.pb_off), j.n_pb, ctx->ws, ctx->fft_tab + j.tw_off_c[1],
-                      ctx->fft_tab + j.post_off_c[1], epj, skc, st);
+                      ctx->fft_tab + j.post_off_c[1], epj, skc, st, ctx->cols_wide != 0);
     }
     for (int v = 1; v < kVariants; ++v)
       if (j.n_fc[v]) {
@@ -1612,7 +1615,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     const int h = j.n_pb / 2;
     {
       Timer t(ctx, s, "fft_cols");
-      launch_cols512b(dd, list, h, ctx->ws, ctx->fft_tab + j.tw_off_c[1], ctx->fft_tab + j.post_off_c[1], epj, skc, s);
+      launch_cols512b(dd, list, h, ctx->ws, ctx->fft_tab + j.tw_off_c[1], ctx->fft_tab + j.post_off_c[1], epj, skc, s,
+                      ctx->cols_wide != 0);
     }
     HIPCHK(ctx, hipEventRecord(ctx->side_in, s));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->side_in, 0));
@@ -1624,7 +1628,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     {
       Timer t(ctx, s, "fft_cols");
       launch_cols512b(dd, list + h, j.n_pb - h, ctx->ws, ctx->fft_tab + j.tw_off_c[1], ctx->fft_tab + j.post_off_c[1],
-                      epj, skc, s);
+                      epj, skc, s, ctx->cols_wide != 0);
     }
     sorted0 = h;
   }

@@ -701,12 +701,194 @@ __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ im
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_cols512w: k_cols512b's codes-only (THR) path with no idle lanes.  A block
+// of 7 waves = 28 16-lane groups covers TWO tile strips (28 columns) of one
+// channel, so every group transforms a distinct column (k_cols512b's 16
+// groups over one 14-column strip repeat column 13 twice: 1/8 of its FFT and
+// epilogue work).  The epilogue maps thread t to tile row (h, jl) = (t / 14,
+// t % 14) of both strips (448 = 32 x 14 threads, two rows each, no repeated
+// lanes); the row maxima go through LDS (rmax) and the 64 tile scores are
+// finished by wave 0 after the block barrier that ends the image.
+// ---------------------------------------------------------------------------
+struct Cols512wLds {
+  union {
+    cf xch[28][kXchStridePk];   // per group transpose region (60,928 B)
+    float X[2][449 * 14];       // the two strips' 448 x 14 coefficients (+ the spare row of the k = 64 store)
+  } u;
+  uint32_t rmax[2][32][14];     // row |max| bits (uint order: +NaN above Inf above finite)
+  float2 tw2[16][16];
+  float4 pc[256];
+};                              // 70,656 B: 2 blocks per CU
+
+__device__ __forceinline__ void cols512w_load(int c, int kx, const float* __restrict__ T, float4 (&q)[8]) {
+  const int j = opaque_tid() & 15;
+  constexpr int KW = 448;
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
+                                                      0x00020000);
+  const int o = t4_index(j, kx) * 16;   // band4 = 16 b + j
+  constexpr int bstep = 16 * KW * 16;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, DCTAE_T_LD_AUX));
+}
+
+// the transform of group G = column col of strip 2 sp + sg, image k: band T'
+// in qa -> X[sg] (lane indices from a fresh opaque_tid: the compiler rebuilds
+// the addresses per phase instead of holding them across the image loop)
+__device__ __forceinline__ void cols512w_transform(Cols512wLds& L, const float4 (&qa)[8], float4 pcM) {
+#pragma clang fp contract(fast)
+  constexpr int N = 512, M = 256, KS = 14;
+  const int tid = opaque_tid();
+  const int G = tid >> 4, j = tid & 15;
+  const int sg = G >= KS ? 1 : 0, col = G - KS * sg;
+  const int s = sigma16(j);
+  const bool self0 = (j == 0), self8 = (j == 15);
+  cf v[16];
+#pragma unroll
+  for (int bb = 0; bb < 8; ++bb) {   // qa[bb] = rows 64 bb + 4 j + (0, 2, 3, 1)
+    v[bb] = (cf){qa[bb].x, qa[bb].y};
+    v[15 - bb] = (cf){mirror16(qa[bb].z), mirror16(qa[bb].w)};
+  }
+  fft256_group(v, L.u.xch[G], j, s, L.tw2);
+  __syncthreads();   // X aliases the transpose regions
+  float* xs = L.u.X[sg];
+  float* xa = xs + s * KS + col;         // X[s + 16 i] at + 224 i
+  float* xb = xs + (N - s) * KS + col;   // X[N - s - 16 i] at - 224 i
+  float4 cn0 = L.pc[s], cn1 = L.pc[s + 16];
+#pragma unroll
+  for (int i = 0; i < 16; i += 2) {
+    const float4 c0 = cn0, c1 = cn1;
+    if (i + 2 < 16) {
+      cn0 = L.pc[s + 16 * (i + 2)];
+      cn1 = L.pc[s + 16 * (i + 3)];
+    }
+    cf x0, x1;
+    makhoul_step2(v, i, self0, self8, c0, c1, x0, x1);
+    xa[224 * i] = x0.x;
+    xa[224 * (i + 1)] = x1.x;
+    if (i >= 4) xb[-224 * i] = x0.y;
+    if (i + 1 >= 4) xb[-224 * (i + 1)] = x1.y;
+  }
+  if (self0) xs[M * KS + col] = (pcM.x + pcM.y) * v[0].x + (pcM.w - pcM.z) * v[0].y;
+}
+
+// codes of tile row (h, jl) = (t / 14, t % 14) in both strips, the rows' |max| into rmax
+__device__ __forceinline__ void cols512w_epilogue(Cols512wLds& L, const ImgDesc& dk, int c, int sp,
+                                                  const float2 (&thr_r)[2][7], const EncParams& ep,
+                                                  const TokenSinks& sk) {
+  constexpr int KS = 14;
+  const int tid = opaque_tid();
+  const int eh = tid / KS, ejl = tid - KS * eh;
+  const f2v* row0 = reinterpret_cast<const f2v*>(L.u.X[0]) + (KS * eh + ejl) * (KS / 2);
+  const f2v* row1 = reinterpret_cast<const f2v*>(L.u.X[1]) + (KS * eh + ejl) * (KS / 2);
+  uint32_t code0 = 0, code1 = 0;
+  float am0 = 0.0f, am1 = 0.0f;
+#pragma unroll
+  for (int p = 0; p < KS / 2; ++p) code_bits4(code0, code1, am0, am1, row0[p], row1[p], thr_r[0][p], thr_r[1][p]);
+  L.rmax[0][eh][ejl] = __float_as_uint(am0);
+  L.rmax[1][eh][ejl] = __float_as_uint(am1);
+  if (sk.codes) {
+    sk.codes[cols_tok(dk, c, 2 * sp, eh, ep.C) * KS + ejl] = (uint16_t)code0;
+    sk.codes[cols_tok(dk, c, 2 * sp + 1, eh, ep.C) * KS + ejl] = (uint16_t)code1;
+  }
+  if (sk.raw) {   // both strips' tokens as 16-byte pieces (cols_store_tokens over 448 threads)
+    for (int e = tid; e < 2 * 32 * 49; e += 448) {
+      const int r = e / (32 * 49), e2 = e - r * 32 * 49, h = e2 / 49, q = e2 - h * 49;
+      reinterpret_cast<float4*>(sk.raw + cols_tok(dk, c, 2 * sp + r, h, ep.C) * (KS * KS))[q] =
+          reinterpret_cast<const float4*>(L.u.X[r] + KS * KS * h)[q];
+    }
+  }
+}
+
+// wave 0: the 64 tile scores of image dk from rmax (FE:409-416)
+__device__ __forceinline__ void cols512w_scores(const Cols512wLds& L, const ImgDesc& dk, int c, int sp,
+                                                const EncParams& ep, const TokenSinks& sk) {
+  constexpr int KS = 14;
+  const int tid = opaque_tid();
+  if (tid < 64) {
+    const int r = tid >> 5, h = tid & 31;
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) m = max(m, L.rmax[r][h][q]);
+    const float sb = __fdiv_rn(-(float)(h + 2 * sp + r), ep.ci[c]);
+    sk.scores[cols_tok(dk, c, 2 * sp + r, h, ep.C)] = __fadd_rn(__fmul_rn(__uint_as_float(m), ep.mw), sb);
+  }
+}
+
+template <int IPB>
+__global__ __launch_bounds__(448) __attribute__((amdgpu_waves_per_eu(4))) void k_cols512w(
+    const ImgDesc* __restrict__ imgs, const int* __restrict__ list, int n_list, const float* __restrict__ ws,
+    const float2* __restrict__ tw, const float2* __restrict__ post, EncParams ep, TokenSinks sk) {
+  constexpr int M = 256, KS = 14, per_x = 6;   // 48 items = 3 channels x 16 strip pairs, 6 per XCD lane
+  __shared__ Cols512wLds L;
+  const int b = blockIdx.x;
+  const int slot = b >> 3;
+  const int t = (b & 7) * per_x + slot % per_x, k0 = (slot / per_x) * IPB;
+  if (k0 >= n_list) return;
+  const int c = t >> 4, sp = t & 15;
+  {
+    const int tid = threadIdx.x;
+    if (tid < 256) {
+      L.tw2[tid >> 4][tid & 15] = tw[(tid >> 4) * (tid & 15)];
+      const float4 ab = reinterpret_cast<const float4*>(post)[tid];   // (al.x, al.y, be.x, be.y) -> c1..c4
+      L.pc[tid] = make_float4(ab.x + ab.z, ab.x - ab.z, ab.y + ab.w, ab.y - ab.w);
+    }
+  }
+  const float4 abM = reinterpret_cast<const float4*>(post)[M];
+  const float4 pcM = make_float4(abM.x + abM.z, abM.x - abM.z, abM.y + abM.w, abM.y - abM.w);
+  float2 thr_r[2][7];   // the thread's epilogue rows' thresholds (image-independent; band images: qh = qw = 32)
+  {
+    const int tid = opaque_tid();
+    const int eh = tid / KS, ejl = tid - KS * eh;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const float2* t2 = reinterpret_cast<const float2*>(
+          ep.thr + ((((int64_t)c * ep.maxph + eh) * ep.maxpw) + 2 * sp + r) * (KS * KS) + (int64_t)ejl * KS);
+#pragma unroll
+      for (int p = 0; p < KS / 2; ++p) thr_r[r][p] = t2[p];
+    }
+  }
+  const int kx = [&] {
+    const int G = opaque_tid() >> 4, sg = G >= KS ? 1 : 0;
+    return KS * (2 * sp + sg) + G - KS * sg;
+  }();
+  float4 qa[8];
+  cols512w_load(c, kx, ws + imgs[list[k0]].ws_t, qa);
+  __syncthreads();   // tables
+#pragma unroll
+  for (int u = 0; u < IPB; ++u) {
+    const int k = k0 + u;
+    if (k >= n_list) break;   // block-uniform
+#pragma unroll
+    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(qa[r].x), "+v"(qa[r].y), "+v"(qa[r].z), "+v"(qa[r].w));
+    float4 qn[8];
+    if (u + 1 < IPB) cols512w_load(c, kx, ws + imgs[list[min(k + 1, n_list - 1)]].ws_t, qn);
+    // the previous image's scores (its rmax was written before the barrier that ended it)
+    if (u > 0) cols512w_scores(L, imgs[list[k - 1]], c, sp, ep, sk);
+    cols512w_transform(L, qa, pcM);
+    __syncthreads();
+    cols512w_epilogue(L, imgs[list[k]], c, sp, thr_r, ep, sk);
+    __syncthreads();   // X / rmax reads before the next image's transposes and the score reads
+    if (u + 1 < IPB) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) qa[r] = qn[r];
+    }
+  }
+  cols512w_scores(L, imgs[list[min(k0 + IPB, n_list) - 1]], c, sp, ep, sk);
+}
+
 void launch_cols512b(const ImgDesc* imgs, const int* list, int n_list, const float* ws, const float2* tw,
-                     const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
+                     const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s, bool wide) {
   if (n_list <= 0) return;
   const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
   const int ipb = thr ? DCTAE_C5B_IPB : 2;
   const int grid = 96 * ((n_list + ipb - 1) / ipb);
+  if (thr && wide) {   // two strips per 7-wave block: 48 items
+    hipLaunchKernelGGL((k_cols512w<DCTAE_C5B_IPB>), dim3(48 * ((n_list + DCTAE_C5B_IPB - 1) / DCTAE_C5B_IPB)), dim3(448),
+                       0, s, imgs, list, n_list, ws, tw, post, ep, sk);
+    return;
+  }
   if (thr)
     hipLaunchKernelGGL((k_cols512b<true, DCTAE_C5B_IPB>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, ws, tw,
                        post, ep, sk);

@@ -443,8 +443,11 @@ __global__ __launch_bounds__(256, (SH == 0 && NC == 3) ? 1 : 2) void k_gemm_x3(c
 // two into the fp16 range, so a piece pair carries 22 significant bits and
 // the dropped terms (a1 b1, the pieces' residuals) are <= 3 x 2^-22 |a b|
 // (~0.1 of the fp32 rounding of k_gemm_f32's sums; half the MFMAs of k_gemm_x3)
+#ifndef DCTAE_H2_WPE
+#define DCTAE_H2_WPE 2
+#endif
 template <int NC, int SH>
-__global__ __launch_bounds__(256, 2) void k_gemm_h2(const GemmProblem* __restrict__ probs,
+__global__ __launch_bounds__(256, DCTAE_H2_WPE) void k_gemm_h2(const GemmProblem* __restrict__ probs,
                                                   const TileRef* __restrict__ tiles) {
   using S = X3Shape<NC, SH>;
   __shared__ Pieces<S::TM, 2> As[S::NA];

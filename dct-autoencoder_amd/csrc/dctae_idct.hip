@@ -614,7 +614,7 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
       const float px = mirror16(v[15 - i].x), py = mirror16(v[15 - i].y);
       __builtin_amdgcn_raw_buffer_store_b128(
           (v4u){__float_as_uint(v[i].x), __float_as_uint(-py), __float_as_uint(-v[i].y), __float_as_uint(px)}, rsrc,
-          uo, i * ustep, 0);
+          uo, i * ustep, DCTAE_U_ST_AUX);
     }
     if (u + 1 < IPB) tk = tn;
   }

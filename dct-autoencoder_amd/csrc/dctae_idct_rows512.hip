@@ -84,7 +84,13 @@ __global__ __launch_bounds__(256) void k_idct_rows512(const ImgDesc* __restrict_
 #pragma unroll
       for (int q = 0; q < 4 + NB / 4; ++q) {
         const int kx = j + 16 * (4 * q + g);   // q >= 4: B[4 (q - 4) + k] = Ys[M + j + 16 (4 (q - 4) + k)]
+#if DCTAE_U_LD_NT
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f fv = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(ub + c * cstride + (int64_t)u4_index(bnd, kx) * 4));
+        const float4 f = make_float4(fv.x, fv.y, fv.z, fv.w);
+#else
         const float4 f = *reinterpret_cast<const float4*>(ub + c * cstride + (int64_t)u4_index(bnd, kx) * 4);
+#endif
         float r4[4] = {f.x, f.y, f.z, f.w};
         xpose4_rows(r4);
 #pragma unroll

@@ -113,7 +113,8 @@ void launch_rows512(const ImgDesc* imgs, const int2* blocks, int n_blocks, const
 int cols7_grid(int n_list, int qw, int ipb);
 // band-layout column pass of 512 x 512 images (k_cols512b; the rows wrote T' with band = 1)
 void launch_cols512b(const ImgDesc* imgs, const int* list, int n_list, const float* ws, const float2* tw,
-                     const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s);
+                     const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s,
+                     bool wide = false);
 
 // Bluestein DCT for lengths without a Makhoul plan (dctae_bluestein.hip)
 int bs_rows_per_block(int L);

@@ -47,13 +47,23 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #ifndef DCTAE_TLAYOUT
 #define DCTAE_TLAYOUT 2
 #endif
-// cache-policy bits of the band T' stores (k_rows512pk) and loads (k_cols512b):
-// 0 = default, 2 = nontemporal (A/B switches)
+// cache-policy bits of the band T' stores (k_rows512pk) and loads (k_cols512b /
+// k_cols512w): 2 = nontemporal (default: T' is written once, read once; its
+// 2.8 GB per 1024 images otherwise churn the L2 / MALL -- same-box A/B, rows
+// 1.089-1.092 -> 1.053-1.054 ms with NT stores, the following sort / pack
+// 0.128 -> 0.108 ms with NT loads), 0 = the default policy
 #ifndef DCTAE_T_ST_AUX
-#define DCTAE_T_ST_AUX 0
+#define DCTAE_T_ST_AUX 2
 #endif
 #ifndef DCTAE_T_LD_AUX
-#define DCTAE_T_LD_AUX 0
+#define DCTAE_T_LD_AUX 2
+#endif
+// the decode's band U' (k_idct_cols512b stores, k_idct_rows512 loads): A/B switches
+#ifndef DCTAE_U_ST_AUX
+#define DCTAE_U_ST_AUX 0
+#endif
+#ifndef DCTAE_U_LD_NT
+#define DCTAE_U_LD_NT 0
 #endif
 static_assert(DCTAE_TLAYOUT == 0 || DCTAE_TLAYOUT == 2, "T' layouts: 0 or 2");
 __device__ __forceinline__ int t4_index(int band4, int kx) {

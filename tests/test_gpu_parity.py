@@ -809,6 +809,28 @@ def test_sort_overlap_bit_identical(fe, pn, lfq):
         assert torch.equal(getattr(dp0, f), getattr(dp1, f)), f
 
 
+def test_cols_wide_bit_identical(fe, pn, lfq):
+    """Option cols_wide (default on: the codes-only column pass of 512^2 band
+    images on k_cols512w, two tile strips per 7-wave block) against
+    k_cols512b (cols_wide=0): codes, raw tokens, scores and packing equal bit
+    for bit, odd image count included."""
+    ops = _ops()
+    x = ops.synth_images(7, 512, 512, seed=79, device=torch.device(DEV))
+    outs = {}
+    for w in (1, 0):
+        ops.set_option("cols_wide", w)
+        try:
+            outs[w] = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)[0]
+        finally:
+            ops.set_option("cols_wide", 0)
+    (dp1, c1), (dp0, c0) = outs[1], outs[0]
+    torch.cuda.synchronize()
+    assert torch.equal(c0, c1)
+    assert torch.equal(dp0._data["scores"], dp1._data["scores"])
+    for f in ("patches", "key_pad_mask", "batched_image_ids", "patch_channels", "patch_positions"):
+        assert torch.equal(getattr(dp0, f), getattr(dp1, f)), f
+
+
 HALVES_DEFAULT = 0   # dctae_ctx::halves
 
 

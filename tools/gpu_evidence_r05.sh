@@ -23,3 +23,9 @@ python3 tools/trace_gaps.py "$tr" --per-call 3 --calls 10 --first 3 --match k_ro
     --match k_sort_pack2 --json $OUT/encode_trace_gaps_$TAG.json || true
 PMC_OUT=$OUT/pmc DECODE=1 bash tools/gpu_pmc_enc.sh > $OUT/pmc_$TAG.log 2>&1 || { tail -20 $OUT/pmc_$TAG.log; exit 1; }
 python3 tools/pmc_enc_summary.py $OUT/pmc --profile $OUT/pmc_$TAG.json --tag $TAG | tail -12
+# multi-rank rehearsal at HEAD (two ranks sharing the card, gloo collectives; tools/gpu_multirank.sh)
+if [ -n "${MULTIRANK:-}" ]; then
+  bash tools/gpu_multirank.sh > $OUT/multirank_$TAG.log 2>&1 || { tail -30 $OUT/multirank_$TAG.log; exit 1; }
+  tail -3 $OUT/multirank_$TAG.log
+  cp gpurun_out/multirank.log $OUT/multirank_bench_$TAG.log
+fi
