@@ -116,6 +116,10 @@ struct dctae_ctx {
   // operands scaled into the fp16 range, three products: half k_gemm_x3's
   // MFMAs), 0 = k_gemm_x3
   int gemm_h2 = 1;
+  // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
+  // (192 < in, out <= 208 / 224): 1 = the W-stationary kernel k_lfq_ws
+  // (dctae_lfq_ws.hip), 0 = k_lfq_proj_h2
+  int lfq_ws = 0;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only
@@ -912,6 +916,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
+  else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1639,7 +1644,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
     // (patchnorm.py:163): the fp16 projection's operand bound
     const float xb = ctx->gemm_h2 ? std::max(std::fabs(norm->min_val), std::fabs(norm->max_val)) : 0.0f;
     launch_lfq_project_in16(sk.norm, E.n_tok, PP, proj_w, proj_b, lfq->codebook_dim, lfq->num_codebooks, sk.codes,
-                            ctx->proj_ws, s, xb);
+                            ctx->proj_ws, s, xb, ctx->lfq_ws != 0);
   }
   if (full && E.n_img > sorted0) {
     Timer t(ctx, s, "sort_pack");
@@ -2035,7 +2040,8 @@ int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* i
   {
     Timer t(ctx, s, "lfq_project_out");
     launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
-                           ctx->proj_ws, s, nullptr, nullptr, nullptr, nullptr, 0.f, 0, 0, nullptr, ctx->gemm_h2 != 0);
+                           ctx->proj_ws, s, nullptr, nullptr, nullptr, nullptr, 0.f, 0, 0, nullptr, ctx->gemm_h2 != 0,
+                           ctx->lfq_ws != 0);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
@@ -2063,7 +2069,7 @@ int dctae_lfq_project_out_inverse_norm(dctae_ctx* ctx, const dctae_lfq* lfq, con
     Timer t(ctx, s, "lfq_project_out");
     launch_lfq_project_out(idx, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, out,
                            ctx->proj_ws, s, channels, positions, norm->median_dev, norm->b_dev, norm->eps, max_patch_h,
-                           max_patch_w, ctx->err_dev, ctx->gemm_h2 != 0);
+                           max_patch_w, ctx->err_dev, ctx->gemm_h2 != 0, ctx->lfq_ws != 0);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);

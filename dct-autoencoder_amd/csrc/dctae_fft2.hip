@@ -9,6 +9,16 @@
 #include "dctae_launch.h"
 #include "dctae_spec512.h"
 
+// config 2's T with the nontemporal hint: on for k_rows224p's stores (rows
+// 0.060 -> 0.057 ms), off for k_cols224's loads (their strided 8-byte reads
+// share lines through L2: cols 0.052 -> 0.069 ms with it), same-box A/B r05.
+#ifndef DCTAE_T224_ST_NT
+#define DCTAE_T224_ST_NT 1
+#endif
+#ifndef DCTAE_T224_LD_NT
+#define DCTAE_T224_LD_NT 0
+#endif
+
 
 namespace dctae {
 
@@ -330,8 +340,13 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
         const float4 cc = pc[k];
         const float2 A = z[cr][pad16(k)], P = z[cr][pad16(k == 0 ? 0 : M - k)];
         const cf t = makhoul_pair((cf){A.x, A.y}, (cf){P.x, P.y}, (cf){cc.x, cc.y}, (cf){cc.z, cc.w});
+#if DCTAE_T224_ST_NT
+        if (oa[i] >= 0) __builtin_nontemporal_store(t.x, tb + oa[i]);
+        if (ob[i] >= 0) __builtin_nontemporal_store(t.y, tb + ob[i]);
+#else
         if (oa[i] >= 0) tb[oa[i]] = t.x;
         if (ob[i] >= 0) tb[ob[i]] = t.y;
+#endif
       }
     }
     if (lane == 0 && M < Kw) {   // k = M: Z[0] with itself
@@ -992,7 +1007,13 @@ __global__ __launch_bounds__(256) void k_cols224(const ImgDesc* __restrict__ img
     const int64_t rstep = (int64_t)8 * Kw;   // 16 rows, in float2
     c4f2 tv[N / 16];
 #pragma unroll
-    for (int k = 0; k < N / 16; ++k) tv[k] = src[k * rstep];
+    for (int k = 0; k < N / 16; ++k) {
+#if DCTAE_T224_LD_NT
+      tv[k] = __builtin_nontemporal_load(src + k * rstep);
+#else
+      tv[k] = src[k * rstep];
+#endif
+    }
     float* dst = zs + y0 * KSP + KS * u + 2 * p;
 #pragma unroll
     for (int k = 0; k < N / 16; ++k) {

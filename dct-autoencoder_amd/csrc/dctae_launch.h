@@ -50,11 +50,18 @@ void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, con
                            float scale, int64_t* idx, uint16_t* wsp, hipStream_t s);
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                              uint16_t* idx, uint16_t* wsp, hipStream_t s,
-                             float x_bound = 0.f);
+                             float x_bound = 0.f, bool ws = false);
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                             float scale, float* out, uint16_t* wsp, hipStream_t s, const int64_t* ch = nullptr,
                             const int64_t* pos = nullptr, const float* med = nullptr, const float* nb = nullptr,
-                            float eps = 0.f, int maxph = 0, int maxpw = 0, int* err = nullptr, bool h2 = true);
+                            float eps = 0.f, int maxph = 0, int maxpw = 0, int* err = nullptr, bool h2 = true,
+                            bool ws = false);
+// dctae_lfq_ws.hip: the W-stationary form of the two (fp16 pieces; 192 < K <= 208, 192 < N <= 224)
+bool lfq_ws_fits(int mode, int K, int N, int cd, int ncb);
+void launch_lfq_ws(int mode, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
+                   const float* bias, int cd, int ncb, float scale, int64_t* idx_out, float* out, uint16_t* idx16,
+                   const int64_t* ch, const int64_t* pos, const float* med, const float* nb, float eps, int maxph,
+                   int maxpw, int* err, const uint16_t* wsp, int NPw, int Kp, float a_scale);
 // VectorQuantize inference (dctae_vq.hip)
 void launch_vq_bias(float* y, const float* bias, int64_t n, int cols, const uint8_t* mask, const float* orig,
                     hipStream_t s);

@@ -430,7 +430,8 @@ size_t lfq_proj_scratch_bytes(int N, int K) {
 template <int MODE>
 static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
                         const float* w, const float* b, int cd, int ncb, float scale, int64_t* idx_out, float* out,
-                        uint16_t* wsp, uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}, float a_bound = 0.f) {
+                        uint16_t* wsp, uint16_t* idx16 = nullptr, InvNorm inv = InvNorm{}, float a_bound = 0.f,
+                        bool ws = false) {
   const int NP = nt * 16, Kp = (K + 31) / 32 * 32;
   const dim3 g((unsigned)((n + 127) / 128));
   bool h2 = false;
@@ -444,6 +445,13 @@ static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* id
   if (MODE == 1 && a_bound > 0.0f) {   // a_bound: the caller allows the fp16 form
     const float sh = (float)(_Float16)scale;
     h2 = sh == scale && std::fabs(scale) >= 6.103515625e-05f && std::fabs(scale) <= 16384.0f;
+  }
+  if (h2 && ws && lfq_ws_fits(MODE, K, N, cd, ncb)) {   // the W-stationary kernel (dctae_lfq_ws.hip)
+    const int NPw = (N + 31) / 32 * 32;
+    hipLaunchKernelGGL(k_split_w_h2, dim3(1), dim3(1024), 0, s, w, N, K, NPw, Kp, wsp);
+    launch_lfq_ws(MODE, s, x, idx_in, n, K, N, b, cd, ncb, scale, idx_out, out, idx16, inv.ch, inv.pos, inv.med, inv.b,
+                  inv.eps, inv.maxph, inv.maxpw, inv.err, wsp, NPw, Kp, MODE == 0 ? a_scale : 1.0f);
+    return;
   }
   if (h2) {
     const int* w_exp = reinterpret_cast<const int*>(wsp + 2 * (size_t)NP * Kp);
@@ -487,19 +495,20 @@ void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, con
 // the same into the encode's u16 token staging (cd <= 16)
 // x_bound > 0: |x| <= x_bound (NaN aside), the fp16 form
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                             uint16_t* idx, uint16_t* wsp, hipStream_t s, float x_bound) {
+                             uint16_t* idx, uint16_t* wsp, hipStream_t s, float x_bound, bool ws) {
   if (n <= 0) return;
   launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, 0.f, nullptr, nullptr, wsp, idx,
-                 InvNorm{}, x_bound);
+                 InvNorm{}, x_bound, ws);
 }
 
 // indices (n, ncb) -> codes (+-scale, n x ncb cd) -> out (n, D) = codes w_out^T + b_out; w_out (D, ncb cd)
 void launch_lfq_project_out(const int64_t* idx, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                             float scale, float* out, uint16_t* wsp, hipStream_t s, const int64_t* ch, const int64_t* pos,
-                            const float* med, const float* nb, float eps, int maxph, int maxpw, int* err, bool h2) {
+                            const float* med, const float* nb, float eps, int maxph, int maxpw, int* err, bool h2,
+                            bool ws) {
   if (n <= 0) return;
   launch_mode<1>((D + 15) / 16, s, nullptr, idx, n, cd * ncb, D, w, b, cd, ncb, scale, nullptr, out, wsp, nullptr,
-                 InvNorm{ch, pos, med, nb, eps, maxph, maxpw, err}, h2 ? 1.0f : 0.0f);
+                 InvNorm{ch, pos, med, nb, eps, maxph, maxpw, err}, h2 ? 1.0f : 0.0f, ws);
 }
 
 }  // namespace dctae

@@ -1,0 +1,345 @@
+// W-stationary LFQ projections for the conf/patch14-l.json shapes (lfq.py:54-62:
+// project_in 196 -> 16 x 13 = 208 fused with sign + index packing, lfq.py:164,
+// :175-187; indices -> +-scale codes -> project_out 208 -> 196, lfq.py:105-127,
+// optionally followed by the inverse PatchNorm, patchnorm.py:167-177).
+//
+// k_lfq_proj (dctae_lfq_proj.hip) stages a 32-k chunk of W in LDS for 128
+// tokens and every wave reads all of it: per chunk 8 waves x 26 KB of W
+// fragments out of LDS for 39 MFMAs each, the LDS port, not the MFMA pipe,
+// sets its pace (1.38 ms for 3.1 M tokens).  Here each of the 7 waves of a
+// block owns one 32-feature output tile and keeps that tile's W fragments in
+// registers for the block's whole life (13 k steps x 2 fp16 planes x 8 halves
+// = 104 VGPRs); only the tokens go through LDS (32 per tile, split once into
+// fp16 planes and shared by the 7 waves).  One block per CU (the W registers
+// allow no second), persistent over a contiguous run of 32-token tiles, the
+// next tile's global loads in flight during the current tile's MFMAs, one
+// barrier per tile.
+//
+// Arithmetic as k_lfq_proj_h2: A scaled by a power of two into the fp16
+// range (mode 0: a_scale from the caller's bound |x| <= x_bound, two pieces;
+// mode 1: +-scale exact in fp16, one piece), W scaled by 2^w_exp (k_split_w_h2,
+// two pieces), the products of piece order <= 1 on v_mfma_f32_32x32x16_f16
+// with fp32 accumulation, unscaled exactly before the bias.
+#include "dctae_device.h"
+#include "dctae_launch.h"
+
+#include <type_traits>
+
+namespace dctae {
+
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 hv8 __attribute__((ext_vector_type(8)));
+typedef _Float16 hv4 __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int kKS = 13;              // 16-k MFMA steps: 192 < K <= 208
+constexpr int kNW = 7;               // waves = 32-feature output tiles: 192 < N <= 224
+constexpr int kThr = 64 * kNW;
+constexpr int kTok = 32;             // tokens per tile (the MFMA's M)
+constexpr int kKp = 16 * kKS;        // k per LDS row
+constexpr int kRow = kKp + 8;        // LDS row stride in halves (108 dwords: the 16 rows of a
+                                     // b128 fragment read phase start on 16 distinct bank quads)
+constexpr int kMw = 8;               // mask words per token (256 features)
+constexpr int kYs = 32 * kNW + 8;    // mode 1's output tile row stride in floats (4 x 232 = 32 mod 64 banks)
+constexpr int kSU0 = (kTok * kKp / 4 + kThr - 1) / kThr;   // mode 0: float4 units per thread
+constexpr int kSU1 = (kTok * kKp / 8 + kThr - 1) / kThr;   // mode 1: 8-k units per thread
+
+struct WsInv {
+  const int64_t* ch;    // (n) channels of the tokens, or null: no inverse
+  const int64_t* pos;   // (n, 2)
+  const float* med;     // (3, maxph, maxpw, N)
+  const float* b;
+  float eps;
+  int maxph, maxpw;
+  int* err;             // bit 1: a table index out of range (the reference raises IndexError)
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
+                                                 int64_t n, int K, int N, const float* __restrict__ bias, int cd,
+                                                 int ncb, float scale, int64_t* __restrict__ idx_out,
+                                                 float* __restrict__ out, uint16_t* __restrict__ idx16, WsInv inv,
+                                                 const uint16_t* __restrict__ wsp, int NPw, int Kp, float a_scale,
+                                                 int64_t tiles_per_block) {
+  constexpr int NPA = MODE == 0 ? 2 : 1;   // A pieces
+  __shared__ __attribute__((aligned(16))) _Float16 As[2][NPA][kTok * kRow];
+  __shared__ uint32_t Msk[MODE == 0 ? 2 * kTok * kMw : 1];   // sign bits [buf][token][32-feature word]
+  __shared__ int64_t Tb[MODE == 1 ? 2 * kTok : 1];           // inverse PatchNorm table rows [buf][token]
+  // mode 1: the tile's outputs [buf][token][kYs], re-read as float4 along each token's N floats
+  __shared__ __attribute__((aligned(16))) float Ys[MODE == 1 ? 2 * kTok * kYs : 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, half = lane >> 5;
+  const int64_t ntiles = (n + kTok - 1) / kTok;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
+  const int64_t t1 = t0 + tiles_per_block < ntiles ? t0 + tiles_per_block : ntiles;
+  if (t0 >= t1) return;   // whole block
+
+  // zero both A buffers (the k >= K tail stays zero) and the mask words
+  for (int e = tid; e < 2 * NPA * kTok * kRow / 8; e += kThr)
+    reinterpret_cast<f32x4v*>(&As[0][0][0])[e] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE == 0)
+    for (int e = tid; e < 2 * kTok * kMw; e += kThr) Msk[e] = 0u;
+
+  // this wave's W fragments: row 32 wave + l32 of the [2][NPw][Kp] fp16 planes,
+  // k 16 s + 8 half .. + 7 (the B operand layout of v_mfma_f32_32x32x16_f16)
+  const int* w_exp = reinterpret_cast<const int*>(wsp + 2 * (size_t)NPw * Kp);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wsp), 0, 2 * NPw * Kp * 2, 0x00020000);
+  hv8 wb[2][kKS];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int s = 0; s < kKS; ++s)
+      wb[p][s] = __builtin_bit_cast(
+          hv8, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((32 * wave + l32) * Kp + 16 * s + 8 * half) * 2 + p * NPw * Kp * 2,
+                                                     0, 0));
+  const float unscale = ldexpf(1.0f / a_scale, -w_exp[0]);
+  const int col = 32 * wave + l32;   // this lane's output feature
+  const float bb = (bias && col < N) ? bias[col] : 0.f;
+
+  // staging: mode 0 loads 32 token rows of fp32 (one contiguous 32 K floats run)
+  // as float4 units two tiles ahead (two register sets), mode 1 the int64
+  // indices of the codebooks an 8-k unit touches, one tile ahead
+  const int K4 = K >> 2;
+  f32x4v ra[MODE == 0 ? 2 : 1][MODE == 0 ? kSU0 : 1];
+  int32_t ri[MODE == 1 ? kSU1 : 1][2];
+  auto load0 = [&](auto SET, int64_t t) {
+    constexpr int S = decltype(SET)::value;
+    const int64_t tok0 = t * kTok;
+#pragma unroll
+    for (int i = 0; i < kSU0; ++i) {
+      const int u = tid + kThr * i;
+      const int row = u / K4;
+      ra[S][i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (u < kTok * K4 && tok0 + row < n)
+        ra[S][i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(x + tok0 * K) + u);
+    }
+  };
+  auto store0 = [&](auto SET, int buf) {
+    constexpr int S = decltype(SET)::value;
+#pragma unroll
+    for (int i = 0; i < kSU0; ++i) {
+      const int u = tid + kThr * i;
+      if (u < kTok * K4) {
+        const int row = u / K4, k4 = u - row * K4;
+        const f32x4v v = ra[S][i] * a_scale;
+        const hv4 h = __builtin_convertvector(v, hv4);
+        const hv4 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x4v), hv4);
+        *reinterpret_cast<hv4*>(&As[buf][0][row * kRow + 4 * k4]) = h;
+        *reinterpret_cast<hv4*>(&As[buf][NPA - 1][row * kRow + 4 * k4]) = l;
+      }
+    }
+  };
+  auto load1 = [&](int64_t t) {
+    const int64_t tok0 = t * kTok;
+#pragma unroll
+    for (int i = 0; i < kSU1; ++i) {
+      const int u = tid + kThr * i;
+      const int row = u / (kKp / 8), k0 = 8 * (u - row * (kKp / 8));
+      ri[i][0] = ri[i][1] = 0;
+      if (u < kTok * (kKp / 8) && tok0 + row < n && k0 < K) {
+        const int c0 = k0 / cd, c1 = min((k0 + 7) / cd, ncb - 1);
+        const int64_t* ip = idx_in + (tok0 + row) * ncb;
+        ri[i][0] = (int32_t)ip[c0];   // lfq.py:117 indices.int()
+        ri[i][1] = (int32_t)ip[c1];
+      }
+    }
+  };
+  auto store1 = [&](int64_t t, int buf) {
+    const int64_t tok0 = t * kTok;
+#pragma unroll
+    for (int i = 0; i < kSU1; ++i) {
+      const int u = tid + kThr * i;
+      if (u < kTok * (kKp / 8)) {
+        const int row = u / (kKp / 8), k0 = 8 * (u - row * (kKp / 8));
+        const int c0 = k0 / cd;
+        hv8 a;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int k = k0 + e, c = k / cd, b = k - c * cd;
+          const int id = c == c0 ? ri[i][0] : ri[i][1];
+          const bool bit = (id >> (cd - 1 - b)) & 1;
+          a[e] = (_Float16)(k < K ? (bit ? scale : -scale) : 0.f);   // lfq.py:117-124
+        }
+        *reinterpret_cast<hv8*>(&As[buf][0][row * kRow + k0]) = a;
+      }
+    }
+    if (inv.ch && tid < kTok) {
+      const int64_t row = tok0 + tid;
+      int64_t tb = -2;   // -2: past n, -1: out-of-range table index
+      if (row < n) {
+        const int64_t c = inv.ch[row], h = inv.pos[2 * row], w = inv.pos[2 * row + 1];
+        const bool ok = c >= 0 && c < 3 && h >= 0 && h < inv.maxph && w >= 0 && w < inv.maxpw;
+        if (!ok) atomicOr(inv.err, 1);
+        tb = ok ? ((c * inv.maxph + h) * inv.maxpw + w) * N : -1;
+      }
+      Tb[buf * kTok + tid] = tb;
+    }
+  };
+
+  // one tile: `set` holds the loads of tile t + 1 (mode 0), the other set is
+  // refilled with tile t + 2's; LDS buffer buf holds tile t's A pieces
+  auto tile = [&](auto SET, int64_t t) {
+    constexpr int S = decltype(SET)::value;
+    const int buf = MODE == 0 ? S ^ 1 : (int)((t - t0) & 1);   // (t - t0) & 1
+    const int64_t tok0 = t * kTok;
+    if constexpr (MODE == 0) {
+      if (t + 2 < t1) load0(std::integral_constant<int, S ^ 1>{}, t + 2);
+    } else {
+      if (t + 1 < t1) load1(t + 1);
+    }
+    constexpr int kU1 = (kTok * 32 * kNW / 4 + kThr - 1) / kThr;   // float4 output units per thread
+    f32x4v tm[MODE == 1 ? kU1 : 1], tbv[MODE == 1 ? kU1 : 1];
+    const int N4 = N >> 2;
+    floatx16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    const _Float16* ap = &As[buf][0][l32 * kRow + 8 * half];
+#pragma unroll
+    for (int s = 0; s < kKS; ++s) {
+      const hv8 a0 = *reinterpret_cast<const hv8*>(ap + 16 * s);
+      if constexpr (MODE == 0) {
+        const hv8 a1 = *reinterpret_cast<const hv8*>(ap + kTok * kRow + 16 * s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, wb[0][s], acc, 0, 0, 0);
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[1][s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[0][s], acc, 0, 0, 0);
+    }
+    // C/D map: feature = col (lane & 31), token row = (v & 3) + 8 (v >> 2) + 4 half
+    if constexpr (MODE == 0) {
+      uint32_t* msk = Msk + buf * kTok * kMw;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const float h = acc[v] * unscale + bb;
+        const uint64_t mk = __ballot(col < N && h > 0.0f);   // lfq.py:175 (NaN -> False)
+        const int row = (v & 3) + 8 * (v >> 2);
+        if (lane == 0) {
+          msk[row * kMw + wave] = (uint32_t)mk;
+          msk[(row + 4) * kMw + wave] = (uint32_t)(mk >> 32);
+        }
+      }
+      if (t + 1 < t1) store0(std::integral_constant<int, S>{}, buf ^ 1);
+    } else {
+      float* ys = Ys + buf * kTok * kYs;
+      if (col < N) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) ys[((v & 3) + 8 * (v >> 2) + 4 * half) * kYs + col] = acc[v] * unscale + bb;
+      }
+      // this tile's table pieces, in flight during the next tile's staging and the barrier
+      if (inv.ch) {
+#pragma unroll
+        for (int i = 0; i < kU1; ++i) {
+          const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
+          const int64_t tb = u < kTok * N4 ? Tb[buf * kTok + row] : -2;
+          tm[i] = tbv[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+          if (tb >= 0) {
+            tm[i] = *reinterpret_cast<const f32x4v*>(inv.med + tb + 4 * c4);
+            tbv[i] = *reinterpret_cast<const f32x4v*>(inv.b + tb + 4 * c4);
+          }
+        }
+      }
+      if (t + 1 < t1) store1(t + 1, buf ^ 1);
+    }
+    __syncthreads();
+    if constexpr (MODE == 0) {
+      // (token i, codebook c) pairs of the tile, token-major: contiguous stores
+      const uint32_t* msk = Msk + buf * kTok * kMw;
+      for (int p = tid; p < kTok * ncb; p += kThr) {
+        const int i = p / ncb, c = p - i * ncb;
+        if (tok0 + i >= n) break;
+        const int o0 = c * cd, wd = o0 >> 5, sh = o0 & 31;
+        const uint64_t win = (uint64_t)msk[i * kMw + wd] | ((uint64_t)msk[i * kMw + wd + 1] << 32);
+        const uint32_t bits = (uint32_t)(win >> sh) & ((1u << cd) - 1u);   // bit b = feature o0 + b
+        const uint32_t code = __builtin_bitreverse32(bits) >> (32 - cd);
+        if (idx16)
+          idx16[tok0 * ncb + p] = (uint16_t)code;   // encode staging (cd <= 16), gathered by k_sort_pack2
+        else   // lfq.py:187: the bit of the quantized value
+          idx_out[tok0 * ncb + p] = (int64_t)lfq_index_bits(code, scale > 0.0f ? ~0ull : 0ull,
+                                                            -scale > 0.0f ? ~0ull : 0ull) & ((1ll << cd) - 1);
+      }
+    } else {
+      // outputs as float4 pieces along each token's N floats, the inverse
+      // PatchNorm on the prefetched table pieces (same fp32 ops as dctae_norm_inverse)
+      const float* ys = Ys + buf * kTok * kYs;
+#pragma unroll
+      for (int i = 0; i < kU1; ++i) {
+        const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
+        if (u >= kTok * N4 || tok0 + row >= n) continue;
+        f32x4v y = *reinterpret_cast<const f32x4v*>(ys + row * kYs + 4 * c4);
+        if (inv.ch) {
+          const int64_t tb = Tb[buf * kTok + row];
+          if (tb >= 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = pn_inverse(y[e], tm[i][e], tbv[i][e], inv.eps);
+          } else {
+            y = f32x4v{1.f, 1.f, 1.f, 1.f} * __int_as_float(0x7fc00000);
+          }
+        }
+        __builtin_nontemporal_store(y, reinterpret_cast<f32x4v*>(out + (tok0 + row) * N) + c4);
+      }
+    }
+  };
+
+  __syncthreads();   // the zero fill before the first tile's stores
+  if constexpr (MODE == 0) {
+    load0(std::integral_constant<int, 0>{}, t0);
+    store0(std::integral_constant<int, 0>{}, 0);
+    if (t0 + 1 < t1) load0(std::integral_constant<int, 1>{}, t0 + 1);
+  } else {
+    load1(t0);
+    store1(t0, 0);
+  }
+  __syncthreads();
+  if constexpr (MODE == 0) {
+    for (int64_t t = t0; t < t1; t += 2) {
+      tile(std::integral_constant<int, 1>{}, t);
+      if (t + 1 < t1) tile(std::integral_constant<int, 0>{}, t + 1);
+    }
+  } else {
+    for (int64_t t = t0; t < t1; ++t) tile(std::integral_constant<int, 0>{}, t);
+  }
+}
+
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
+}  // namespace
+
+bool lfq_ws_fits(int mode, int K, int N, int cd, int ncb) {
+  const bool k_ok = K > 16 * (kKS - 1) && K <= kKp && (mode == 1 || K % 4 == 0);
+  const bool n_ok = N > 32 * (kNW - 1) && N <= 32 * kNW;
+  // mode 1: an 8-k unit touches at most two codebooks; mode 0: u16 / 31-bit codes
+  const bool cd_ok = mode == 1 ? cd >= 8 : (cd >= 1 && cd <= 16);
+  return k_ok && n_ok && cd_ok && ncb >= 1 && (int64_t)cd * ncb == (mode == 0 ? N : K);
+}
+
+void launch_lfq_ws(int mode, hipStream_t s, const float* x, const int64_t* idx_in, int64_t n, int K, int N,
+                   const float* bias, int cd, int ncb, float scale, int64_t* idx_out, float* out, uint16_t* idx16,
+                   const int64_t* ch, const int64_t* pos, const float* med, const float* nb, float eps, int maxph,
+                   int maxpw, int* err, const uint16_t* wsp, int NPw, int Kp, float a_scale) {
+  const int64_t ntiles = (n + kTok - 1) / kTok;
+  if (ntiles <= 0) return;
+  const int64_t nb_ = ntiles < cu_count() ? ntiles : cu_count();
+  const int64_t per = (ntiles + nb_ - 1) / nb_;
+  const WsInv inv{ch, pos, med, nb, eps, maxph, maxpw, err};
+  const dim3 g((unsigned)((ntiles + per - 1) / per));
+  if (mode == 0)
+    hipLaunchKernelGGL(k_lfq_ws<0>, g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
+                       idx16, inv, wsp, NPw, Kp, a_scale, per);
+  else
+    hipLaunchKernelGGL(k_lfq_ws<1>, g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
+                       idx16, inv, wsp, NPw, Kp, a_scale, per);
+}
+
+}  // namespace dctae

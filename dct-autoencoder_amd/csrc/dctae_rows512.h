@@ -58,9 +58,12 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #ifndef DCTAE_T_LD_AUX
 #define DCTAE_T_LD_AUX 2
 #endif
-// the decode's band U' (k_idct_cols512b stores, k_idct_rows512 loads): A/B switches
+// the decode's band U' (k_idct_cols512b stores, k_idct_rows512 loads): the
+// stores nontemporal (default; same-box A/B r05: decode 2.07-2.12 -> 2.01-2.05
+// ms, cols 0.88-0.90 -> 0.84-0.87, rows 1.10-1.12 -> 1.05-1.08), the loads at
+// the default policy (nontemporal loads: rows 1.10 -> 1.29-1.33 ms)
 #ifndef DCTAE_U_ST_AUX
-#define DCTAE_U_ST_AUX 0
+#define DCTAE_U_ST_AUX 2
 #endif
 #ifndef DCTAE_U_LD_NT
 #define DCTAE_U_LD_NT 0

@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 CFG = ref_cpu.FEConfig()
 LCFG = ref_cpu.LFQConfig(dim=196, codebook_size=2 ** 13, num_codebooks=16)
+LFQ_WS_DEFAULT = 0   # dctae_api.hip: ctx->lfq_ws
 
 
 @pytest.fixture(scope="module")
@@ -199,3 +200,38 @@ def test_project_out_inverse_norm_fused(pkg, fe, pn, lfq_p):
     assert torch.isnan(out[0, 0]).all() and torch.equal(out[0, 1:], fused[0, 1:])
     with pytest.raises(Exception):
         ops.check_device_errors(codes.device)
+
+
+@pytest.mark.parametrize("sizes", [[(512, 512), (512, 512)], [(224, 224), (97, 1000), (300, 500)]])
+def test_w_stationary_kernel_vs_lfq_proj_h2(pkg, fe, pn, lfq_p, sizes):
+    """k_lfq_ws (option lfq_ws=1) against k_lfq_proj_h2 (lfq_ws=0):
+    the same fp16 pieces and products summed in another order, so the codes
+    agree except inside the rounding band (<= 1 in 1000 bits) and the decode
+    within 2e-5 (|W| |codes| + |b|) of each other; both directions, fused
+    inverse PatchNorm included, ragged tails (n not a multiple of 32)."""
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    dev = torch.device(DEV, 0)
+    imgs = _images(82, sizes)
+    try:
+        ops.set_option("lfq_ws", 0, dev)
+        ((dp0, c0),) = fe.encode_batch(imgs, pn, lfq_p, return_patches=True)
+        q0 = lfq_p.indices_to_codes(c0)
+        o0 = fe.decode_batch(dp0, c0, pn, lfq_p)
+        ops.set_option("lfq_ws", 1, dev)
+        ((dp1, c1),) = fe.encode_batch(imgs, pn, lfq_p, return_patches=True)
+        q1 = lfq_p.indices_to_codes(c0)
+        o1 = fe.decode_batch(dp0, c0, pn, lfq_p)
+    finally:
+        ops.set_option("lfq_ws", LFQ_WS_DEFAULT, dev)
+    assert torch.equal(dp1.patches, dp0.patches)
+    diff = int((c1 != c0).sum())
+    print(f"[{sizes}] codes differing between the two kernels: {diff} / {c1.numel()}")
+    assert diff <= max(2, c1.numel() // 1000)
+    Wo, bo = _w(lfq_p.project_out)
+    codes = ref_cpu.lfq_indices_to_codes(c0.cpu(), LCFG)
+    tol = 2e-5 * F.linear(codes.abs(), Wo.abs(), bo.abs())
+    assert torch.all((q1.cpu() - q0.cpu()).abs() <= tol)
+    for a, r in zip(o1, o0):
+        scale = max(1.0, float(r.abs().max()))
+        assert torch.all((a - r).abs() <= 1e-5 * scale + 2e-5 * r.abs())
