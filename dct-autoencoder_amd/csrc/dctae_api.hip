@@ -119,7 +119,7 @@ struct dctae_ctx {
   // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
   // (192 < in, out <= 208 / 224): 1 = the W-stationary kernel k_lfq_ws
   // (dctae_lfq_ws.hip), 0 = k_lfq_proj_h2
-  int lfq_ws = 0;
+  int lfq_ws = 1;
   // PatchNorm training scratch (token cell ids, per-cell lists, batch tables), grow-only
   uint8_t* st_ws = nullptr;
   // VectorQuantize scratch (projected vectors, codes, transformed codebook), grow-only

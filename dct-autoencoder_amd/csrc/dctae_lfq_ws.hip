@@ -23,7 +23,8 @@
 #include "dctae_device.h"
 #include "dctae_launch.h"
 
-#include <type_traits>
+#include <utility>
+
 
 namespace dctae {
 
@@ -37,14 +38,23 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int kKS = 13;              // 16-k MFMA steps: 192 < K <= 208
 constexpr int kNW = 7;               // waves = 32-feature output tiles: 192 < N <= 224
 constexpr int kThr = 64 * kNW;
-constexpr int kTok = 32;             // tokens per tile (the MFMA's M)
 constexpr int kKp = 16 * kKS;        // k per LDS row
 constexpr int kRow = kKp + 8;        // LDS row stride in halves (108 dwords: the 16 rows of a
                                      // b128 fragment read phase start on 16 distinct bank quads)
 constexpr int kMw = 8;               // mask words per token (256 features)
+constexpr int kK4 = 49;              // mode 0: float4 per token row (K = 196, conf/patch14-l.json's dim)
 constexpr int kYs = 32 * kNW + 8;    // mode 1's output tile row stride in floats (4 x 232 = 32 mod 64 banks)
-constexpr int kSU0 = (kTok * kKp / 4 + kThr - 1) / kThr;   // mode 0: float4 units per thread
-constexpr int kSU1 = (kTok * kKp / 8 + kThr - 1) / kThr;   // mode 1: 8-k units per thread
+
+// lane L of the VGPR w = the wave-uniform x (v_writelane_b32; no builtin in this hipcc)
+template <int L>
+__device__ __forceinline__ void writelane(int& w, uint32_t x) {
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(x), "n"(L));
+}
+
+template <typename F, int... Vs>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, Vs...>, F&& f) {
+  (f(std::integral_constant<int, Vs>{}), ...);
+}
 
 struct WsInv {
   const int64_t* ch;    // (n) channels of the tokens, or null: no inverse
@@ -56,32 +66,37 @@ struct WsInv {
   int* err;             // bit 1: a table index out of range (the reference raises IndexError)
 };
 
-template <int MODE>
+template <int MODE, int MT>
 __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ bias, int cd,
                                                  int ncb, float scale, int64_t* __restrict__ idx_out,
                                                  float* __restrict__ out, uint16_t* __restrict__ idx16, WsInv inv,
                                                  const uint16_t* __restrict__ wsp, int NPw, int Kp, float a_scale,
                                                  int64_t tiles_per_block) {
+  constexpr int TOK = 32 * MT;             // tokens per tile: MT 32-row M blocks
   constexpr int NPA = MODE == 0 ? 2 : 1;   // A pieces
-  __shared__ __attribute__((aligned(16))) _Float16 As[2][NPA][kTok * kRow];
-  __shared__ uint32_t Msk[MODE == 0 ? 2 * kTok * kMw : 1];   // sign bits [buf][token][32-feature word]
-  __shared__ int64_t Tb[MODE == 1 ? 2 * kTok : 1];           // inverse PatchNorm table rows [buf][token]
+  constexpr int SU0 = TOK * kK4 / kThr;                    // mode 0: float4 units per thread
+  static_assert(MODE == 1 || TOK * kK4 % kThr == 0, "mode 0: whole float4 units per thread");
+  constexpr int SU1 = (TOK * kKp / 8 + kThr - 1) / kThr;   // mode 1: 8-k units per thread
+  constexpr int U1 = (TOK * 32 * kNW / 4 + kThr - 1) / kThr;   // mode 1: float4 output units per thread
+  __shared__ __attribute__((aligned(16))) _Float16 As[2][NPA][TOK * kRow];
+  __shared__ uint32_t Msk[MODE == 0 ? 2 * TOK * kMw : 1];   // sign bits [buf][token][32-feature word]
+  __shared__ int64_t Tb[MODE == 1 ? 2 * TOK : 1];           // inverse PatchNorm table rows [buf][token]
   // mode 1: the tile's outputs [buf][token][kYs], re-read as float4 along each token's N floats
-  __shared__ __attribute__((aligned(16))) float Ys[MODE == 1 ? 2 * kTok * kYs : 1];
+  __shared__ __attribute__((aligned(16))) float Ys[MODE == 1 ? 2 * TOK * kYs : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5;
-  const int64_t ntiles = (n + kTok - 1) / kTok;
+  const int64_t ntiles = (n + TOK - 1) / TOK;
   const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
   const int64_t t1 = t0 + tiles_per_block < ntiles ? t0 + tiles_per_block : ntiles;
   if (t0 >= t1) return;   // whole block
 
   // zero both A buffers (the k >= K tail stays zero) and the mask words
-  for (int e = tid; e < 2 * NPA * kTok * kRow / 8; e += kThr)
+  for (int e = tid; e < 2 * NPA * TOK * kRow / 8; e += kThr)
     reinterpret_cast<f32x4v*>(&As[0][0][0])[e] = f32x4v{0.f, 0.f, 0.f, 0.f};
   if constexpr (MODE == 0)
-    for (int e = tid; e < 2 * kTok * kMw; e += kThr) Msk[e] = 0u;
+    for (int e = tid; e < 2 * TOK * kMw; e += kThr) Msk[e] = 0u;
 
   // this wave's W fragments: row 32 wave + l32 of the [2][NPw][Kp] fp16 planes,
   // k 16 s + 8 half .. + 7 (the B operand layout of v_mfma_f32_32x32x16_f16)
@@ -98,141 +113,172 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
   const float unscale = ldexpf(1.0f / a_scale, -w_exp[0]);
   const int col = 32 * wave + l32;   // this lane's output feature
   const float bb = (bias && col < N) ? bias[col] : 0.f;
-
-  // staging: mode 0 loads 32 token rows of fp32 (one contiguous 32 K floats run)
-  // as float4 units two tiles ahead (two register sets), mode 1 the int64
-  // indices of the codebooks an 8-k unit touches, one tile ahead
-  const int K4 = K >> 2;
-  f32x4v ra[MODE == 0 ? 2 : 1][MODE == 0 ? kSU0 : 1];
-  int32_t ri[MODE == 1 ? kSU1 : 1][2];
-  auto load0 = [&](auto SET, int64_t t) {
-    constexpr int S = decltype(SET)::value;
-    const int64_t tok0 = t * kTok;
+  // mode 0: h = acc unscale + bb > 0  <=>  acc > -bb / unscale (unscale a power
+  // of two: the product and the quotient are exact); +inf past N: never set
+  const float thr = col < N ? -bb / unscale : __int_as_float(0x7f800000);
+  // mode 0: the (token, codebook) pairs p = tid + kThr j this thread assembles
+  // each tile: token, mask word offset and shift are tile-invariant
+  constexpr int NPJ = MODE == 0 ? (TOK * 32 + kThr - 1) / kThr : 1;   // ncb <= 32
+  int pi[NPJ], pw[NPJ], psh[NPJ];
+  const uint32_t cmask = cd >= 32 ? ~0u : (1u << cd) - 1u;
+  if constexpr (MODE == 0) {
 #pragma unroll
-    for (int i = 0; i < kSU0; ++i) {
-      const int u = tid + kThr * i;
-      const int row = u / K4;
-      ra[S][i] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      if (u < kTok * K4 && tok0 + row < n)
-        ra[S][i] = __builtin_nontemporal_load(reinterpret_cast<const f32x4v*>(x + tok0 * K) + u);
+    for (int j = 0; j < NPJ; ++j) {
+      const int p = tid + kThr * j, i = p / ncb, o0 = (p - i * ncb) * cd;
+      pi[j] = i;
+      pw[j] = i * kMw + (o0 >> 5);
+      psh[j] = o0 & 31;
+    }
+  }
+
+  // staging, one tile ahead: mode 0 the tile's TOK token rows of fp32 (one
+  // contiguous TOK K floats run) as float4 units, mode 1 the int64 indices of
+  // the codebooks an 8-k unit touches.  Loads are unconditional (pieces past
+  // the tile or past n re-read the last valid one and are zeroed at the
+  // store): no VALU write to a register with a load in flight, no control
+  // flow around the issue, so the wait before the store is exact
+  f32x4v ra[MODE == 0 ? SU0 : 1];
+  int32_t ri[MODE == 1 ? SU1 : 1][2];   // low dwords of the int64 indices (lfq.py:117 indices.int())
+  auto load = [&](int64_t t) {
+    if constexpr (MODE == 0) {
+      const f32x4v* xt = reinterpret_cast<const f32x4v*>(x) + t * TOK * kK4;   // the tile's contiguous run
+      if ((t + 1) * TOK <= n) {
+#pragma unroll
+        for (int i = 0; i < SU0; ++i) ra[i] = __builtin_nontemporal_load(xt + tid + kThr * i);
+      } else {   // the last tile (or past t1): re-read the last valid piece
+        const int64_t last = n * kK4 - 1 - t * TOK * kK4;
+#pragma unroll
+        for (int i = 0; i < SU0; ++i) {
+          const int64_t u = tid + kThr * i;
+          ra[i] = __builtin_nontemporal_load(xt + (u < last ? u : last));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < SU1; ++i) {
+        const int u = min(tid + kThr * i, TOK * (kKp / 8) - 1);
+        const int row = u / (kKp / 8), k0 = min(8 * (u - row * (kKp / 8)), K - 1);
+        const int64_t tok = min(t * TOK + row, n - 1);
+        const int c0 = k0 / cd, c1 = min((k0 + 7) / cd, ncb - 1);
+        const int32_t* ip = reinterpret_cast<const int32_t*>(idx_in + tok * ncb);
+        ri[i][0] = ip[2 * c0];
+        ri[i][1] = ip[2 * c1];
+      }
     }
   };
-  auto store0 = [&](auto SET, int buf) {
-    constexpr int S = decltype(SET)::value;
+  auto store = [&](int64_t t, int buf) {
+    const int64_t tok0 = t * TOK;
+    if constexpr (MODE == 0) {
+      const bool full = tok0 + TOK <= n;
 #pragma unroll
-    for (int i = 0; i < kSU0; ++i) {
-      const int u = tid + kThr * i;
-      if (u < kTok * K4) {
-        const int row = u / K4, k4 = u - row * K4;
-        const f32x4v v = ra[S][i] * a_scale;
+      for (int i = 0; i < SU0; ++i) {
+        const int u = tid + kThr * i;
+        const int row = u / kK4, k4 = u - row * kK4;
+        f32x4v v = ra[i] * a_scale;
+        if (!full && tok0 + row >= n) v = f32x4v{0.f, 0.f, 0.f, 0.f};
         const hv4 h = __builtin_convertvector(v, hv4);
         const hv4 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x4v), hv4);
         *reinterpret_cast<hv4*>(&As[buf][0][row * kRow + 4 * k4]) = h;
         *reinterpret_cast<hv4*>(&As[buf][NPA - 1][row * kRow + 4 * k4]) = l;
       }
-    }
-  };
-  auto load1 = [&](int64_t t) {
-    const int64_t tok0 = t * kTok;
+    } else {
 #pragma unroll
-    for (int i = 0; i < kSU1; ++i) {
-      const int u = tid + kThr * i;
-      const int row = u / (kKp / 8), k0 = 8 * (u - row * (kKp / 8));
-      ri[i][0] = ri[i][1] = 0;
-      if (u < kTok * (kKp / 8) && tok0 + row < n && k0 < K) {
-        const int c0 = k0 / cd, c1 = min((k0 + 7) / cd, ncb - 1);
-        const int64_t* ip = idx_in + (tok0 + row) * ncb;
-        ri[i][0] = (int32_t)ip[c0];   // lfq.py:117 indices.int()
-        ri[i][1] = (int32_t)ip[c1];
-      }
-    }
-  };
-  auto store1 = [&](int64_t t, int buf) {
-    const int64_t tok0 = t * kTok;
+      for (int i = 0; i < SU1; ++i) {
+        const int u = tid + kThr * i;
+        if (u < TOK * (kKp / 8)) {
+          const int row = u / (kKp / 8), k0 = 8 * (u - row * (kKp / 8));
+          const int c0 = k0 / cd;
+          const bool live = tok0 + row < n;
+          const int i0 = ri[i][0], i1 = ri[i][1];
+          hv8 a;
 #pragma unroll
-    for (int i = 0; i < kSU1; ++i) {
-      const int u = tid + kThr * i;
-      if (u < kTok * (kKp / 8)) {
-        const int row = u / (kKp / 8), k0 = 8 * (u - row * (kKp / 8));
-        const int c0 = k0 / cd;
-        hv8 a;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int k = k0 + e, c = k / cd, b = k - c * cd;
-          const int id = c == c0 ? ri[i][0] : ri[i][1];
-          const bool bit = (id >> (cd - 1 - b)) & 1;
-          a[e] = (_Float16)(k < K ? (bit ? scale : -scale) : 0.f);   // lfq.py:117-124
+          for (int e = 0; e < 8; ++e) {
+            const int k = k0 + e, c = k / cd, b = k - c * cd;
+            const int id = c == c0 ? i0 : i1;
+            const bool bit = (id >> (cd - 1 - b)) & 1;
+            a[e] = (_Float16)(live && k < K ? (bit ? scale : -scale) : 0.f);   // lfq.py:117-124
+          }
+          *reinterpret_cast<hv8*>(&As[buf][0][row * kRow + k0]) = a;
         }
-        *reinterpret_cast<hv8*>(&As[buf][0][row * kRow + k0]) = a;
       }
-    }
-    if (inv.ch && tid < kTok) {
-      const int64_t row = tok0 + tid;
-      int64_t tb = -2;   // -2: past n, -1: out-of-range table index
-      if (row < n) {
-        const int64_t c = inv.ch[row], h = inv.pos[2 * row], w = inv.pos[2 * row + 1];
-        const bool ok = c >= 0 && c < 3 && h >= 0 && h < inv.maxph && w >= 0 && w < inv.maxpw;
-        if (!ok) atomicOr(inv.err, 1);
-        tb = ok ? ((c * inv.maxph + h) * inv.maxpw + w) * N : -1;
+      if (inv.ch && tid < TOK) {
+        const int64_t row = tok0 + tid;
+        int64_t tb = -2;   // -2: past n, -1: out-of-range table index
+        if (row < n) {
+          const int64_t c = inv.ch[row], h = inv.pos[2 * row], w = inv.pos[2 * row + 1];
+          const bool ok = c >= 0 && c < 3 && h >= 0 && h < inv.maxph && w >= 0 && w < inv.maxpw;
+          if (!ok) atomicOr(inv.err, 1);
+          tb = ok ? ((c * inv.maxph + h) * inv.maxpw + w) * N : -1;
+        }
+        Tb[buf * TOK + tid] = tb;
       }
-      Tb[buf * kTok + tid] = tb;
     }
   };
 
-  // one tile: `set` holds the loads of tile t + 1 (mode 0), the other set is
-  // refilled with tile t + 2's; LDS buffer buf holds tile t's A pieces
-  auto tile = [&](auto SET, int64_t t) {
-    constexpr int S = decltype(SET)::value;
-    const int buf = MODE == 0 ? S ^ 1 : (int)((t - t0) & 1);   // (t - t0) & 1
-    const int64_t tok0 = t * kTok;
-    if constexpr (MODE == 0) {
-      if (t + 2 < t1) load0(std::integral_constant<int, S ^ 1>{}, t + 2);
-    } else {
-      if (t + 1 < t1) load1(t + 1);
-    }
-    constexpr int kU1 = (kTok * 32 * kNW / 4 + kThr - 1) / kThr;   // float4 output units per thread
-    f32x4v tm[MODE == 1 ? kU1 : 1], tbv[MODE == 1 ? kU1 : 1];
-    const int N4 = N >> 2;
-    floatx16 acc;
+  __syncthreads();   // the zero fill before the first tile's stores
+  load(t0);
+  store(t0, 0);
+  __syncthreads();
+  const int N4 = N >> 2;
+  for (int64_t t = t0; t < t1; ++t) {
+    const int buf = (int)((t - t0) & 1);
+    const int64_t tok0 = t * TOK;
+    load(t + 1);   // past t1: clamped, unused
+    floatx16 acc[MT];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
-    const _Float16* ap = &As[buf][0][l32 * kRow + 8 * half];
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[m][v] = 0.f;
 #pragma unroll
     for (int s = 0; s < kKS; ++s) {
-      const hv8 a0 = *reinterpret_cast<const hv8*>(ap + 16 * s);
-      if constexpr (MODE == 0) {
-        const hv8 a1 = *reinterpret_cast<const hv8*>(ap + kTok * kRow + 16 * s);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, wb[0][s], acc, 0, 0, 0);
-      }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[1][s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[0][s], acc, 0, 0, 0);
-    }
-    // C/D map: feature = col (lane & 31), token row = (v & 3) + 8 (v >> 2) + 4 half
-    if constexpr (MODE == 0) {
-      uint32_t* msk = Msk + buf * kTok * kMw;
 #pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const float h = acc[v] * unscale + bb;
-        const uint64_t mk = __ballot(col < N && h > 0.0f);   // lfq.py:175 (NaN -> False)
-        const int row = (v & 3) + 8 * (v >> 2);
-        if (lane == 0) {
-          msk[row * kMw + wave] = (uint32_t)mk;
-          msk[(row + 4) * kMw + wave] = (uint32_t)(mk >> 32);
+      for (int m = 0; m < MT; ++m) {
+        const _Float16* ap = &As[buf][0][(32 * m + l32) * kRow + 8 * half + 16 * s];
+        const hv8 a0 = *reinterpret_cast<const hv8*>(ap);
+        if constexpr (MODE == 0) {
+          const hv8 a1 = *reinterpret_cast<const hv8*>(ap + TOK * kRow);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, wb[0][s], acc[m], 0, 0, 0);
+        }
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[1][s], acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[0][s], acc[m], 0, 0, 0);
+      }
+    }
+    // C/D map: feature = col (lane & 31), token row = 32 m + (v & 3) + 8 (v >> 2) + 4 half
+    f32x4v tm[MODE == 1 ? U1 : 1], tbv[MODE == 1 ? U1 : 1];
+    if constexpr (MODE == 0) {
+      // ballot v = rows (v & 3) + 8 (v >> 2) (bits 0-31) and + 4 (bits 32-63) of
+      // this wave's 32 features; lane v collects both words, lanes 0-15 store
+      uint32_t* msk = Msk + buf * TOK * kMw;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        int wlo = 0, whi = 0;
+        static_for(std::make_integer_sequence<int, 16>{}, [&](auto V) {
+          constexpr int v = decltype(V)::value;
+          const uint64_t mk = __ballot(acc[m][v] > thr);   // h > 0, lfq.py:175 (NaN -> False)
+          writelane<v>(wlo, (uint32_t)mk);
+          writelane<v>(whi, (uint32_t)(mk >> 32));
+        });
+        if (lane < 16) {
+          const int row = 32 * m + (lane & 3) + 8 * (lane >> 2);
+          msk[row * kMw + wave] = (uint32_t)wlo;
+          msk[(row + 4) * kMw + wave] = (uint32_t)whi;
         }
       }
-      if (t + 1 < t1) store0(std::integral_constant<int, S>{}, buf ^ 1);
     } else {
-      float* ys = Ys + buf * kTok * kYs;
+      float* ys = Ys + buf * TOK * kYs;
       if (col < N) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) ys[((v & 3) + 8 * (v >> 2) + 4 * half) * kYs + col] = acc[v] * unscale + bb;
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int v = 0; v < 16; ++v)
+            ys[(32 * m + (v & 3) + 8 * (v >> 2) + 4 * half) * kYs + col] = acc[m][v] * unscale + bb;
       }
       // this tile's table pieces, in flight during the next tile's staging and the barrier
       if (inv.ch) {
 #pragma unroll
-        for (int i = 0; i < kU1; ++i) {
+        for (int i = 0; i < U1; ++i) {
           const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
-          const int64_t tb = u < kTok * N4 ? Tb[buf * kTok + row] : -2;
+          const int64_t tb = u < TOK * N4 ? Tb[buf * TOK + row] : -2;
           tm[i] = tbv[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
           if (tb >= 0) {
             tm[i] = *reinterpret_cast<const f32x4v*>(inv.med + tb + 4 * c4);
@@ -240,18 +286,18 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
           }
         }
       }
-      if (t + 1 < t1) store1(t + 1, buf ^ 1);
     }
+    if (t + 1 < t1) store(t + 1, buf ^ 1);
     __syncthreads();
     if constexpr (MODE == 0) {
       // (token i, codebook c) pairs of the tile, token-major: contiguous stores
-      const uint32_t* msk = Msk + buf * kTok * kMw;
-      for (int p = tid; p < kTok * ncb; p += kThr) {
-        const int i = p / ncb, c = p - i * ncb;
-        if (tok0 + i >= n) break;
-        const int o0 = c * cd, wd = o0 >> 5, sh = o0 & 31;
-        const uint64_t win = (uint64_t)msk[i * kMw + wd] | ((uint64_t)msk[i * kMw + wd + 1] << 32);
-        const uint32_t bits = (uint32_t)(win >> sh) & ((1u << cd) - 1u);   // bit b = feature o0 + b
+      const uint32_t* msk = Msk + buf * TOK * kMw;
+#pragma unroll
+      for (int j = 0; j < NPJ; ++j) {
+        const int p = tid + kThr * j;
+        if (p >= TOK * ncb || tok0 + pi[j] >= n) break;
+        const uint64_t win = (uint64_t)msk[pw[j]] | ((uint64_t)msk[pw[j] + 1] << 32);
+        const uint32_t bits = (uint32_t)(win >> psh[j]) & cmask;   // bit b = feature c cd + b
         const uint32_t code = __builtin_bitreverse32(bits) >> (32 - cd);
         if (idx16)
           idx16[tok0 * ncb + p] = (uint16_t)code;   // encode staging (cd <= 16), gathered by k_sort_pack2
@@ -262,14 +308,14 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
     } else {
       // outputs as float4 pieces along each token's N floats, the inverse
       // PatchNorm on the prefetched table pieces (same fp32 ops as dctae_norm_inverse)
-      const float* ys = Ys + buf * kTok * kYs;
+      const float* ys = Ys + buf * TOK * kYs;
 #pragma unroll
-      for (int i = 0; i < kU1; ++i) {
+      for (int i = 0; i < U1; ++i) {
         const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
-        if (u >= kTok * N4 || tok0 + row >= n) continue;
+        if (u >= TOK * N4 || tok0 + row >= n) continue;
         f32x4v y = *reinterpret_cast<const f32x4v*>(ys + row * kYs + 4 * c4);
         if (inv.ch) {
-          const int64_t tb = Tb[buf * kTok + row];
+          const int64_t tb = Tb[buf * TOK + row];
           if (tb >= 0) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) y[e] = pn_inverse(y[e], tm[i][e], tbv[i][e], inv.eps);
@@ -280,25 +326,6 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
         __builtin_nontemporal_store(y, reinterpret_cast<f32x4v*>(out + (tok0 + row) * N) + c4);
       }
     }
-  };
-
-  __syncthreads();   // the zero fill before the first tile's stores
-  if constexpr (MODE == 0) {
-    load0(std::integral_constant<int, 0>{}, t0);
-    store0(std::integral_constant<int, 0>{}, 0);
-    if (t0 + 1 < t1) load0(std::integral_constant<int, 1>{}, t0 + 1);
-  } else {
-    load1(t0);
-    store1(t0, 0);
-  }
-  __syncthreads();
-  if constexpr (MODE == 0) {
-    for (int64_t t = t0; t < t1; t += 2) {
-      tile(std::integral_constant<int, 1>{}, t);
-      if (t + 1 < t1) tile(std::integral_constant<int, 0>{}, t + 1);
-    }
-  } else {
-    for (int64_t t = t0; t < t1; ++t) tile(std::integral_constant<int, 0>{}, t);
   }
 }
 
@@ -317,7 +344,7 @@ int cu_count() {
 }  // namespace
 
 bool lfq_ws_fits(int mode, int K, int N, int cd, int ncb) {
-  const bool k_ok = K > 16 * (kKS - 1) && K <= kKp && (mode == 1 || K % 4 == 0);
+  const bool k_ok = mode == 0 ? K == 4 * kK4 : (K > 16 * (kKS - 1) && K <= kKp);
   const bool n_ok = N > 32 * (kNW - 1) && N <= 32 * kNW;
   // mode 1: an 8-k unit touches at most two codebooks; mode 0: u16 / 31-bit codes
   const bool cd_ok = mode == 1 ? cd >= 8 : (cd >= 1 && cd <= 16);
@@ -328,17 +355,20 @@ void launch_lfq_ws(int mode, hipStream_t s, const float* x, const int64_t* idx_i
                    const float* bias, int cd, int ncb, float scale, int64_t* idx_out, float* out, uint16_t* idx16,
                    const int64_t* ch, const int64_t* pos, const float* med, const float* nb, float eps, int maxph,
                    int maxpw, int* err, const uint16_t* wsp, int NPw, int Kp, float a_scale) {
-  const int64_t ntiles = (n + kTok - 1) / kTok;
+  // mode 0: 64-token tiles (two 32-row MFMA chains per wave), mode 1: 32
+  // (its output tile is staged in LDS twice over)
+  const int tok = mode == 0 ? 64 : 32;
+  const int64_t ntiles = (n + tok - 1) / tok;
   if (ntiles <= 0) return;
   const int64_t nb_ = ntiles < cu_count() ? ntiles : cu_count();
   const int64_t per = (ntiles + nb_ - 1) / nb_;
   const WsInv inv{ch, pos, med, nb, eps, maxph, maxpw, err};
   const dim3 g((unsigned)((ntiles + per - 1) / per));
   if (mode == 0)
-    hipLaunchKernelGGL(k_lfq_ws<0>, g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
+    hipLaunchKernelGGL((k_lfq_ws<0, 2>), g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
                        idx16, inv, wsp, NPw, Kp, a_scale, per);
   else
-    hipLaunchKernelGGL(k_lfq_ws<1>, g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
+    hipLaunchKernelGGL((k_lfq_ws<1, 1>), g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
                        idx16, inv, wsp, NPw, Kp, a_scale, per);
 }
 

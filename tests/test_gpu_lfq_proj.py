@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 CFG = ref_cpu.FEConfig()
 LCFG = ref_cpu.LFQConfig(dim=196, codebook_size=2 ** 13, num_codebooks=16)
-LFQ_WS_DEFAULT = 0   # dctae_api.hip: ctx->lfq_ws
+LFQ_WS_DEFAULT = 1   # dctae_api.hip: ctx->lfq_ws
 
 
 @pytest.fixture(scope="module")

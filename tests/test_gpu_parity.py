@@ -810,8 +810,8 @@ def test_sort_overlap_bit_identical(fe, pn, lfq):
 
 
 def test_cols_wide_bit_identical(fe, pn, lfq):
-    """Option cols_wide (default on: the codes-only column pass of 512^2 band
-    images on k_cols512w, two tile strips per 7-wave block) against
+    """Option cols_wide (off by default, measured slower: the codes-only column
+    pass of 512^2 band images on k_cols512w, two tile strips per 7-wave block) against
     k_cols512b (cols_wide=0): codes, raw tokens, scores and packing equal bit
     for bit, odd image count included."""
     ops = _ops()
@@ -836,7 +836,7 @@ HALVES_DEFAULT = 0   # dctae_ctx::halves
 
 @pytest.mark.parametrize("n", [33, 64])
 def test_halves_bit_identical(fe, pn, lfq, n):
-    """Option halves (default on; config 2's 224^2 batches of >= 32 images:
+    """Option halves (off by default, measured slower; config 2's 224^2 batches of >= 32 images:
     the first half's columns and sort / pack on a side stream beside the
     second half's rows and columns): every packed output equal to the
     one-stream encode (halves=0), odd image count included."""

@@ -19,7 +19,8 @@ NAMES = {"k_rows512": "fft_rows", "k_rows512pk": "fft_rows", "k_fft_rows2": "fft
          "k_fft_cols4": "fft_cols", "k_rows224p": "fft_rows", "k_cols224": "fft_cols", "k_fft_cols": "fft_cols", "k_sort_pack2": "sort_pack", "k_sort_pack": "sort_pack",
          "k_pad_fill": "pad_fill", "k_dec_map": "dec_map", "k_idct_cols512": "idct_cols", "k_idct_rows2": "idct_rows", "k_idct_rows512": "idct_rows",
          "k_gemm_f32": "gemm", "k_rgb_to_ipt": "rgb_to_ipt", "k_tile_epilogue_p": "tile_epilogue",
-         "k_tile_epilogue": "tile_epilogue", "k_gemm_x3": "gemm", "k_idct_cols512b": "idct_cols", "k_gemm_h2": "gemm"}
+         "k_tile_epilogue": "tile_epilogue", "k_gemm_x3": "gemm", "k_idct_cols512b": "idct_cols", "k_gemm_h2": "gemm",
+         "k_lfq_ws": "lfq_ws", "k_lfq_proj_h2": "lfq_proj_h2", "k_lfq_proj": "lfq_proj"}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("dir")
