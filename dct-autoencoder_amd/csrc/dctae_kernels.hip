@@ -77,6 +77,24 @@ __device__ __forceinline__ void block_amax(uint32_t m, uint32_t* dst) {
   }
 }
 
+// cache policy of k_rgb_to_ipt's RGB loads / folded IPT stores: A/B switches,
+// both off (nontemporal measured slower on config 4, round 5: rgb_to_ipt
+// 1.41 -> 1.63 ms with NT loads, 1.93 ms with NT stores)
+#ifndef DCTAE_IPT_ST_NT
+#define DCTAE_IPT_ST_NT 0
+#endif
+#ifndef DCTAE_RGB_LD_NT
+#define DCTAE_RGB_LD_NT 0
+#endif
+__device__ __forceinline__ void ipt_store(float* p, float v) {
+  if (DCTAE_IPT_ST_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ float rgb_load(const float* p) {
+  if (DCTAE_RGB_LD_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
 __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ imgs, const int2* __restrict__ blocks,
                                                     const float* __restrict__ rgb, float* __restrict__ ws,
                                                     ColorMats cm, uint32_t* __restrict__ amax) {
@@ -106,7 +124,7 @@ __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ 
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int c = 0; c < 3; ++c) px[k][q][c] = src[c * hw + o[q]];
+      for (int c = 0; c < 3; ++c) px[k][q][c] = rgb_load(src + c * hw + o[q]);
   }
   uint32_t mx = 0;   // |max| of the values written (k_gemm_h2's operand scale)
 #pragma unroll
@@ -140,12 +158,12 @@ __global__ __launch_bounds__(256) void k_rgb_to_ipt(const ImgDesc* __restrict__ 
       float* ro = dst + c * hw + (int64_t)y * W;
       const float u0 = xp ? a[c] + b[c] : a[c], v0 = a[c] - b[c];
       const float u1 = xp ? c2[c] + d2[c] : c2[c], v1 = c2[c] - d2[c];
-      ro[x] = u0;
-      if (xp) ro[Wh + x] = v0;
+      ipt_store(ro + x, u0);
+      if (xp) ipt_store(ro + Wh + x, v0);
       if (yp) {
         float* r2 = dst + c * hw + (int64_t)y2 * W;
-        r2[x] = u1;
-        if (xp) r2[Wh + x] = v1;
+        ipt_store(r2 + x, u1);
+        if (xp) ipt_store(r2 + Wh + x, v1);
       }
       mx = max(mx, __float_as_uint(u0) & 0x7fffffffu);
       if (xp) mx = max(mx, __float_as_uint(v0) & 0x7fffffffu);

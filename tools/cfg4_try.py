@@ -42,11 +42,14 @@ def main():
     imgs = [ops.synth_images(1, int(h), int(w), seed=7, first_index=i, device=dev)[0] for i, (h, w) in enumerate(hw)]
     fe.encode_batch(imgs, pn, lfq)
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
+    fe.encode_batch(imgs, pn, lfq)   # warm-up call in flight: steady state as bench.config_legs
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
     for _ in range(args.steps):
         fe.encode_batch(imgs, pn, lfq)
+    e1.record()
     torch.cuda.synchronize(dev)
-    el = (time.perf_counter() - t0) / args.steps
+    el = e0.elapsed_time(e1) / 1e3 / args.steps
     kern = kernel_times(lib.context(dev), lambda: fe.encode_batch(imgs, pn, lfq), 2)
     print(json.dumps({"ms": round(el * 1e3, 3), "device_ms": round(sum(v["total_ms"] for v in kern.values()), 3),
                       "kernels": {k: v["total_ms"] for k, v in kern.items()}}))
