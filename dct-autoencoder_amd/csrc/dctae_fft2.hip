@@ -687,7 +687,7 @@ __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ im
     sb[0] = __fdiv_rn(-(float)(g16 + strip), ep.ci[c]);
     sb[1] = __fdiv_rn(-(float)(g16 + 16 + strip), ep.ci[c]);
   }
-  float4 qa[8];
+  TPiece qa[8];
   cols512b_load(c, strip, ws + imgs[list[k0]].ws_t, qa);
   __syncthreads();   // tables
 #pragma unroll
@@ -699,14 +699,15 @@ __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ im
       // opaque values here: without it the compiler moves their register
       // shuffles up to the loads and waits for the NEXT image's prefetch
       // before computing this one (no overlap at all)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(qa[r].x), "+v"(qa[r].y), "+v"(qa[r].z), "+v"(qa[r].w));
+      t_opaque(qa);
       // the next image's loads in flight during this one; unconditional (the
       // last image of the list reloads itself): a conditional load makes the
       // compiler merge qn / qa with register copies right behind the loads
-      float4 qn[8];
+      TPiece qn[8];
       if (u + 1 < IPB) cols512b_load(c, strip, ws + imgs[list[min(k + 1, n_list - 1)]].ws_t, qn);
-      cols512b_compute<THR>(dk, c, strip, L, qa, pcM, sb, thr_r, ep, sk);
+      float4 qf[8];
+      t_decode(qa, qf);
+      cols512b_compute<THR>(dk, c, strip, L, qf, pcM, sb, thr_r, ep, sk);
       __syncthreads();   // epilogue reads of X before the next image's transposes
       if (u + 1 < IPB) {
 #pragma unroll
@@ -736,16 +737,8 @@ struct Cols512wLds {
   float4 pc[256];
 };                              // 70,656 B: 2 blocks per CU
 
-__device__ __forceinline__ void cols512w_load(int c, int kx, const float* __restrict__ T, float4 (&q)[8]) {
-  const int j = opaque_tid() & 15;
-  constexpr int KW = 448;
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
-                                                      0x00020000);
-  const int o = t4_index(j, kx) * 16;   // band4 = 16 b + j
-  constexpr int bstep = 16 * KW * 16;
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, DCTAE_T_LD_AUX));
+__device__ __forceinline__ void cols512w_load(int c, int kx, const float* __restrict__ T, TPiece (&q)[8]) {
+  t_load_column(c, kx, opaque_tid() & 15, T, q);
 }
 
 // the transform of group G = column col of strip 2 sp + sg, image k: band T'
@@ -868,20 +861,21 @@ __global__ __launch_bounds__(448) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int G = opaque_tid() >> 4, sg = G >= KS ? 1 : 0;
     return KS * (2 * sp + sg) + G - KS * sg;
   }();
-  float4 qa[8];
+  TPiece qa[8];
   cols512w_load(c, kx, ws + imgs[list[k0]].ws_t, qa);
   __syncthreads();   // tables
 #pragma unroll
   for (int u = 0; u < IPB; ++u) {
     const int k = k0 + u;
     if (k >= n_list) break;   // block-uniform
-#pragma unroll
-    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(qa[r].x), "+v"(qa[r].y), "+v"(qa[r].z), "+v"(qa[r].w));
-    float4 qn[8];
+    t_opaque(qa);
+    TPiece qn[8];
     if (u + 1 < IPB) cols512w_load(c, kx, ws + imgs[list[min(k + 1, n_list - 1)]].ws_t, qn);
     // the previous image's scores (its rmax was written before the barrier that ended it)
     if (u > 0) cols512w_scores(L, imgs[list[k - 1]], c, sp, ep, sk);
-    cols512w_transform(L, qa, pcM);
+    float4 qf[8];
+    t_decode(qa, qf);
+    cols512w_transform(L, qf, pcM);
     __syncthreads();
     cols512w_epilogue(L, imgs[list[k]], c, sp, thr_r, ep, sk);
     __syncthreads();   // X / rmax reads before the next image's transposes and the score reads

@@ -418,10 +418,61 @@ struct Cols512bLds {
   float4 pc[256];               // c1..c4 of the Makhoul post, k < M (k = M in registers)
 };                              // 40,960 B: 4 blocks per CU
 
-__device__ __forceinline__ void cols512b_load(int c, int strip, const float* __restrict__ T, float4 (&q)[8]) {
+// the band T' of one column as loaded (float4 of 4 rows, or with DCTAE_T23 the
+// 12-byte record quarter, decoded by t_decode when the transform starts)
+#if DCTAE_T23
+typedef v3u TPiece;
+#else
+typedef float4 TPiece;
+#endif
+__device__ __forceinline__ void t_decode(const TPiece (&q)[8], float4 (&f)[8]) {
+#if DCTAE_T23
+  const int j = opaque_tid() & 15;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) f[b] = t23_unpack(q[b], j & 3);
+#else
+#pragma unroll
+  for (int b = 0; b < 8; ++b) f[b] = q[b];
+#endif
+}
+__device__ __forceinline__ void t_opaque(TPiece (&q)[8]) {   // the loads become opaque values here
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+#if DCTAE_T23
+    asm volatile("" : "+v"(q[r].x), "+v"(q[r].y), "+v"(q[r].z));
+#else
+    asm volatile("" : "+v"(q[r].x), "+v"(q[r].y), "+v"(q[r].z), "+v"(q[r].w));
+#endif
+  }
+}
+// lane j of column kx loads band4 = 16 b + j: record (band16 4 b + j / 4, kx), slot j % 4
+__device__ __forceinline__ void t_load_column(int c, int kx, int j, const float* __restrict__ T, TPiece (&q)[8]) {
+  constexpr int KW = 448;
+#if DCTAE_T23
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(reinterpret_cast<const char*>(T)) +
+                                                          (int64_t)c * 512 * KW * 3, 0, 512 * KW * 3, 0x00020000);
+  const int o = (((j >> 2) * KW + kx) * 4 + (j & 3)) * 12;
+  constexpr int bstep = 4 * KW * 4 * 12;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) q[b] = __builtin_amdgcn_raw_buffer_load_b96(rsrc, o, b * bstep, DCTAE_T_LD_AUX);
+#else
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
+                                                      0x00020000);
+  const int o = t4_index(j, kx) * 16;   // band4 = 16 b + j
+  constexpr int bstep = 16 * KW * 16;   // t4_index(16 b + j, kx) - t4_index(16 (b - 1) + j, kx), both layouts
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+    q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, DCTAE_T_LD_AUX));
+#endif
+}
+
+__device__ __forceinline__ void cols512b_load(int c, int strip, const float* __restrict__ T, TPiece (&q)[8]) {
   const int tid = opaque_tid();
   const int G = tid >> 4, j = tid & 15;
   constexpr int KW = 448;
+#if DCTAE_T23
+  t_load_column(c, 14 * strip + min(G, 13), j, T, q);
+#else
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(T) + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
                                                       0x00020000);
   const int kx = 14 * strip + min(G, 13);
@@ -437,6 +488,7 @@ __device__ __forceinline__ void cols512b_load(int c, int strip, const float* __r
 #pragma unroll
   for (int b = 0; b < 8; ++b)
     q[b] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, b * bstep, DCTAE_T_LD_AUX));
+#endif
 }
 
 template <bool THR>
