@@ -356,10 +356,15 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * kernel), "gemm_h2" (1, default: the encode's DCT GEMMs and the fused LFQ
  * projections on fp16 MFMAs with two-piece operands scaled by powers of two
  * (k_gemm_h2 / k_lfq_proj_h2: tokens within 5e-7 x max|Y|); 0: split-bf16),
- * "halves" (1, default: a batch of >= 32 images of one size whose rows and
- * columns each run one compile-time plan kernel, e.g. 224 x 224, runs its
+ * "halves" (0, default / 1: a batch of >= 32 images of one size whose rows
+ * and columns each run one compile-time plan kernel, e.g. 224 x 224, runs its
  * first half's columns and sort / pack on the side stream beside the second
- * half's rows and columns; outputs bit-identical; 0: one stream).
+ * half's rows and columns; outputs bit-identical; measured slower),
+ * "cols_wide" (0, default / 1: the codes-only column pass of 512 x 512 band
+ * images on k_cols512w, two tile strips per 7-wave block; bit-identical;
+ * measured slower), "lfq_ws" (1, default: the fp16 LFQ projections of the
+ * conf/patch14-l.json shapes (196 -> 208 project_in, 208 -> 196 project_out)
+ * on the W-stationary kernel k_lfq_ws; 0: k_lfq_proj_h2).
  * Profiling builds only (make
  * PROFILING=1; the shipped library returns DCTAE_EUNSUP): "bs_ablate",
  * "t_alias" (these write wrong outputs on purpose). */
