@@ -92,6 +92,8 @@ _SIGS = {
     "dctae_lfq_forward": ([_P, C.POINTER(LFQCfg), _P, C.c_int64, _P, _P, _P], C.c_int),
     "dctae_lfq_indices_to_codes": ([_P, C.POINTER(LFQCfg), _P, C.c_int64, _P, _P], C.c_int),
     "dctae_lfq_project_in": ([_P, C.POINTER(LFQCfg), _P, C.c_int64, C.c_int32, _P, _P, _P, _P], C.c_int),
+    "dctae_lfq_project_in_bounded": ([_P, C.POINTER(LFQCfg), _P, C.c_int64, C.c_int32, _P, _P, C.c_float, _P, _P],
+                                     C.c_int),
     "dctae_lfq_project_out": ([_P, C.POINTER(LFQCfg), _P, C.c_int64, C.c_int32, _P, _P, _P, _P], C.c_int),
     "dctae_lfq_project_out_inverse_norm": ([_P, C.POINTER(LFQCfg), _P, C.c_int64, C.c_int32, _P, _P, C.POINTER(Norm),
                                             C.c_int32, C.c_int32, _P, _P, _P, _P], C.c_int),

@@ -291,14 +291,17 @@ def lfq_codes(idx: torch.Tensor, cfg: LFQCfg) -> torch.Tensor:
     return out
 
 
-def lfq_project_in(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], cfg: LFQCfg) -> torch.Tensor:
+def lfq_project_in(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], cfg: LFQCfg,
+                   x_bound: Optional[float] = None) -> torch.Tensor:
     """LFQ.forward's indices with project_in fused (dctae_lfq_project_in):
     x (..., dim) -> (..., num_codebooks) int64.  w / b: project_in's fp32
-    weight (ncb*cd, dim) and bias on x's device."""
-    return lfq_project_in_into(x, w, b, cfg, None)
+    weight (ncb*cd, dim) and bias on x's device.  x_bound: the caller's bound
+    |x| <= x_bound (dctae_lfq_project_in_bounded: the fp16 kernels)."""
+    return lfq_project_in_into(x, w, b, cfg, None, x_bound)
 
 
-def lfq_project_in_into(x, w, b, cfg: LFQCfg, idx: Optional[torch.Tensor]) -> torch.Tensor:
+def lfq_project_in_into(x, w, b, cfg: LFQCfg, idx: Optional[torch.Tensor],
+                        x_bound: Optional[float] = None) -> torch.Tensor:
     dev = _check_dev(x, w, b)
     ctx = _lib.context(dev)
     xs = x.float().contiguous()
@@ -307,6 +310,11 @@ def lfq_project_in_into(x, w, b, cfg: LFQCfg, idx: Optional[torch.Tensor]) -> to
     shape = (*xs.shape[:-1], cfg.num_codebooks)
     if idx is None or idx.shape != shape or idx.dtype != torch.long or not idx.is_contiguous() or idx.device != dev:
         idx = torch.empty(shape, dtype=torch.long, device=dev)
+    if x_bound is not None:
+        rc = ctx.lib.dctae_lfq_project_in_bounded(ctx.h, C.byref(cfg), ptr(xs), n, dim, ptr(w), ptr(b),
+                                                  float(x_bound), ptr(idx), _lib.stream_ptr(dev))
+        ctx.check(rc, "dctae_lfq_project_in_bounded")
+        return idx
     rc = ctx.lib.dctae_lfq_project_in(ctx.h, C.byref(cfg), ptr(xs), n, dim, ptr(w), ptr(b), ptr(idx),
                                       _lib.stream_ptr(dev))
     ctx.check(rc, "dctae_lfq_project_in")

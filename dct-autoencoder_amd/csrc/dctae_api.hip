@@ -2009,8 +2009,8 @@ static int lfq_proj_check(dctae_ctx* ctx, const dctae_lfq* lfq, int64_t n, int32
   return 0;
 }
 
-int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, int32_t dim,
-                         const float* w, const float* b, int64_t* idx, void* stream) {
+static int lfq_project_in_impl(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, int32_t dim,
+                               const float* w, const float* b, float x_bound, int64_t* idx, void* stream) {
   if (!ctx) return DCTAE_EINVAL;
   if (int rc = lfq_proj_check(ctx, lfq, n, dim, x, w, idx, 64)) return rc;
   if (n == 0) return 0;
@@ -2022,11 +2022,23 @@ int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, i
   {
     Timer t(ctx, s, "lfq_project_in");
     launch_lfq_project_in(x, n, dim, w, b, lfq->codebook_dim, lfq->num_codebooks, lfq->codebook_scale, idx,
-                          ctx->proj_ws, s);
+                          ctx->proj_ws, s, ctx->gemm_h2 ? x_bound : 0.0f, ctx->lfq_ws != 0);
   }
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
   return 0;
+}
+
+int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, int32_t dim,
+                         const float* w, const float* b, int64_t* idx, void* stream) {
+  return lfq_project_in_impl(ctx, lfq, x, n, dim, w, b, 0.0f, idx, stream);
+}
+
+int dctae_lfq_project_in_bounded(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x, int64_t n, int32_t dim,
+                                 const float* w, const float* b, float x_bound, int64_t* idx, void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (!(x_bound > 0.0f) || !std::isfinite(x_bound)) return fail(ctx, DCTAE_EINVAL, "x_bound must be finite and > 0");
+  return lfq_project_in_impl(ctx, lfq, x, n, dim, w, b, x_bound, idx, stream);
 }
 
 int dctae_lfq_project_out(dctae_ctx* ctx, const dctae_lfq* lfq, const int64_t* idx, int64_t n, int32_t dim,

@@ -47,7 +47,8 @@ void launch_lfq_codes(const int64_t* idx, int64_t n, int cb_dim, int ncb, float 
 // wsp: scratch of lfq_proj_scratch_bytes(out features, in features) for the pre-split weight
 size_t lfq_proj_scratch_bytes(int N, int K);
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                           float scale, int64_t* idx, uint16_t* wsp, hipStream_t s);
+                           float scale, int64_t* idx, uint16_t* wsp, hipStream_t s, float x_bound = 0.f,
+                           bool ws = false);
 void launch_lfq_project_in16(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
                              uint16_t* idx, uint16_t* wsp, hipStream_t s,
                              float x_bound = 0.f, bool ws = false);

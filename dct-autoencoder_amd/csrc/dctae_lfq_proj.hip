@@ -486,10 +486,12 @@ static void launch_mode(int nt, hipStream_t s, const float* x, const int64_t* id
 }
 
 // x (n, D) fp32, w_in (ncb cd, D), b_in (ncb cd) or null -> indices (n, ncb)
+// x_bound > 0: |x| <= x_bound (NaN aside), the fp16 forms
 void launch_lfq_project_in(const float* x, int64_t n, int D, const float* w, const float* b, int cd, int ncb,
-                           float scale, int64_t* idx, uint16_t* wsp, hipStream_t s) {
+                           float scale, int64_t* idx, uint16_t* wsp, hipStream_t s, float x_bound, bool ws) {
   if (n <= 0) return;
-  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, scale, idx, nullptr, wsp);
+  launch_mode<0>((cd * ncb + 15) / 16, s, x, nullptr, n, D, cd * ncb, w, b, cd, ncb, scale, idx, nullptr, wsp, nullptr,
+                 InvNorm{}, x_bound, ws);
 }
 
 // the same into the encode's u16 token staging (cd <= 16)

@@ -23,7 +23,6 @@
 #include "dctae_device.h"
 #include "dctae_launch.h"
 
-#include <utility>
 
 
 namespace dctae {
@@ -37,24 +36,11 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 constexpr int kKS = 13;              // 16-k MFMA steps: 192 < K <= 208
 constexpr int kNW = 7;               // waves = 32-feature output tiles: 192 < N <= 224
-constexpr int kThr = 64 * kNW;
 constexpr int kKp = 16 * kKS;        // k per LDS row
 constexpr int kRow = kKp + 8;        // LDS row stride in halves (108 dwords: the 16 rows of a
                                      // b128 fragment read phase start on 16 distinct bank quads)
 constexpr int kMw = 8;               // mask words per token (256 features)
 constexpr int kK4 = 49;              // mode 0: float4 per token row (K = 196, conf/patch14-l.json's dim)
-constexpr int kYs = 32 * kNW + 8;    // mode 1's output tile row stride in floats (4 x 232 = 32 mod 64 banks)
-
-// lane L of the VGPR w = the wave-uniform x (v_writelane_b32; no builtin in this hipcc)
-template <int L>
-__device__ __forceinline__ void writelane(int& w, uint32_t x) {
-  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(w) : "s"(x), "n"(L));
-}
-
-template <typename F, int... Vs>
-__device__ __forceinline__ void static_for(std::integer_sequence<int, Vs...>, F&& f) {
-  (f(std::integral_constant<int, Vs>{}), ...);
-}
 
 struct WsInv {
   const int64_t* ch;    // (n) channels of the tokens, or null: no inverse
@@ -66,29 +52,44 @@ struct WsInv {
   int* err;             // bit 1: a table index out of range (the reference raises IndexError)
 };
 
-template <int MODE, int MT>
-__global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
+// at most 256 registers per wave: two waves per SIMD (mode 0's 7-wave block;
+// mode 1's two 4-wave blocks per CU)
+template <int MODE, int MT, int NWB>
+__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(2))) void k_lfq_ws(const float* __restrict__ x, const int64_t* __restrict__ idx_in,
                                                  int64_t n, int K, int N, const float* __restrict__ bias, int cd,
                                                  int ncb, float scale, int64_t* __restrict__ idx_out,
                                                  float* __restrict__ out, uint16_t* __restrict__ idx16, WsInv inv,
                                                  const uint16_t* __restrict__ wsp, int NPw, int Kp, float a_scale,
                                                  int64_t tiles_per_block) {
+  constexpr int kThr = 64 * NWB;           // NWB waves = output tiles per block
+  constexpr int NSPLIT = (kNW + NWB - 1) / NWB;   // blocks sharing a token range, one output slice each
+  constexpr int kYsB = 32 * NWB + 8;       // mode 1's output tile row stride (4 x stride = 32 mod 64 banks)
+  static_assert(MODE == 1 || NSPLIT == 1, "project_in needs every feature of a token in one block");
   constexpr int TOK = 32 * MT;             // tokens per tile: MT 32-row M blocks
   constexpr int NPA = MODE == 0 ? 2 : 1;   // A pieces
   constexpr int SU0 = TOK * kK4 / kThr;                    // mode 0: float4 units per thread
   static_assert(MODE == 1 || TOK * kK4 % kThr == 0, "mode 0: whole float4 units per thread");
   constexpr int SU1 = (TOK * kKp / 8 + kThr - 1) / kThr;   // mode 1: 8-k units per thread
-  constexpr int U1 = (TOK * 32 * kNW / 4 + kThr - 1) / kThr;   // mode 1: float4 output units per thread
+  constexpr int U1 = (TOK * 32 * NWB / 4 + kThr - 1) / kThr;   // mode 1: float4 output units per thread
   __shared__ __attribute__((aligned(16))) _Float16 As[2][NPA][TOK * kRow];
   __shared__ uint32_t Msk[MODE == 0 ? 2 * TOK * kMw : 1];   // sign bits [buf][token][32-feature word]
   __shared__ int64_t Tb[MODE == 1 ? 2 * TOK : 1];           // inverse PatchNorm table rows [buf][token]
   // mode 1: the tile's outputs [buf][token][kYs], re-read as float4 along each token's N floats
-  __shared__ __attribute__((aligned(16))) float Ys[MODE == 1 ? 2 * TOK * kYs : 1];
+  __shared__ __attribute__((aligned(16))) float Ys[MODE == 1 ? 2 * TOK * kYsB : 1];
+  __shared__ hv8 Lut[MODE == 1 ? 256 : 1];   // mode 1: the 8 codes of each byte of index bits
+  __shared__ int32_t Ix[MODE == 1 ? 2 * TOK * 32 : 1];   // mode 1: the tiles' indices [buf][token][codebook]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5;
+  // NSPLIT > 1: blocks 2 i, 2 i + 1 (..) run the same tokens, block 2 i + q the
+  // output tiles q NWB .. q NWB + NWB - 1 (two blocks per CU: each one's waits
+  // overlap the other's MFMAs)
+  const int slice = NSPLIT > 1 ? (int)(blockIdx.x % NSPLIT) : 0;
+  const int tw = slice * NWB + wave;           // this wave's 32-feature output tile
+  const bool mf = 32 * tw < N;                 // wave-uniform: a tile past N does no MFMA
+  const int fbase = 32 * NWB * slice;          // the block's first output feature
   const int64_t ntiles = (n + TOK - 1) / TOK;
-  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
+  const int64_t t0 = (int64_t)(NSPLIT > 1 ? blockIdx.x / NSPLIT : blockIdx.x) * tiles_per_block;
   const int64_t t1 = t0 + tiles_per_block < ntiles ? t0 + tiles_per_block : ntiles;
   if (t0 >= t1) return;   // whole block
 
@@ -108,10 +109,10 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
 #pragma unroll
     for (int s = 0; s < kKS; ++s)
       wb[p][s] = __builtin_bit_cast(
-          hv8, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((32 * wave + l32) * Kp + 16 * s + 8 * half) * 2 + p * NPw * Kp * 2,
+          hv8, __builtin_amdgcn_raw_buffer_load_b128(wrs, ((32 * tw + l32) * Kp + 16 * s + 8 * half) * 2 + p * NPw * Kp * 2,
                                                      0, 0));
   const float unscale = ldexpf(1.0f / a_scale, -w_exp[0]);
-  const int col = 32 * wave + l32;   // this lane's output feature
+  const int col = 32 * tw + l32;   // this lane's output feature
   const float bb = (bias && col < N) ? bias[col] : 0.f;
   // mode 0: h = acc unscale + bb > 0  <=>  acc > -bb / unscale (unscale a power
   // of two: the product and the quotient are exact); +inf past N: never set
@@ -138,7 +139,29 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
   // store): no VALU write to a register with a load in flight, no control
   // flow around the issue, so the wait before the store is exact
   f32x4v ra[MODE == 0 ? SU0 : 1];
-  int32_t ri[MODE == 1 ? SU1 : 1][2];   // low dwords of the int64 indices (lfq.py:117 indices.int())
+  // mode 1: the tile's TOK x ncb int64 indices are one contiguous run; their low
+  // dwords (lfq.py:117 indices.int()) go through registers (two tiles ahead)
+  // into the LDS index buffers Ix (one tile ahead), where the staging reads them
+  constexpr int RX = (TOK * 32 + kThr - 1) / kThr;   // ncb <= 32
+  int32_t rx[MODE == 1 ? RX : 1];
+  // mode 1: unit (row, k0 .. k0 + 7)'s codebooks c0 = k0 / cd, c1 and the shift of
+  // its 8 bits in (i0 << cd | i1): k0 / cd = (k0 rc) >> 16 with rc = ceil(2^16 / cd)
+  // (exact for k0 < 2^10), the rest from it
+  const uint32_t rc = (65536u + (uint32_t)cd - 1u) / (uint32_t)cd;
+  auto unit_cb = [&](int k0, int& c0, int& c1, int& sh) {
+    c0 = (int)(((uint32_t)k0 * rc) >> 16);
+    c1 = min((int)(((uint32_t)(k0 + 7) * rc) >> 16), ncb - 1);
+    sh = 2 * cd - 8 - (k0 - c0 * cd);
+  };
+  if constexpr (MODE == 1) {
+    // +-scale of the 8 bits of a byte, MSB first (lfq.py:117-124)
+    for (int e = tid; e < 256; e += kThr) {
+      hv8 v;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) v[b] = (_Float16)(((e >> (7 - b)) & 1) ? scale : -scale);
+      Lut[e] = v;
+    }
+  }
   auto load = [&](int64_t t) {
     if constexpr (MODE == 0) {
       const f32x4v* xt = reinterpret_cast<const f32x4v*>(x) + t * TOK * kK4;   // the tile's contiguous run
@@ -154,17 +177,18 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
         }
       }
     } else {
+      const int64_t last = n * ncb - 1;   // unconditional, clamped (past n: unused)
 #pragma unroll
-      for (int i = 0; i < SU1; ++i) {
-        const int u = min(tid + kThr * i, TOK * (kKp / 8) - 1);
-        const int row = u / (kKp / 8), k0 = min(8 * (u - row * (kKp / 8)), K - 1);
-        const int64_t tok = min(t * TOK + row, n - 1);
-        const int c0 = k0 / cd, c1 = min((k0 + 7) / cd, ncb - 1);
-        const int32_t* ip = reinterpret_cast<const int32_t*>(idx_in + tok * ncb);
-        ri[i][0] = ip[2 * c0];
-        ri[i][1] = ip[2 * c1];
+      for (int i = 0; i < RX; ++i) {
+        const int64_t f = t * TOK * ncb + tid + kThr * i;
+        rx[i] = reinterpret_cast<const int32_t*>(idx_in)[2 * (f < last ? f : last)];
       }
     }
+  };
+  auto put_idx = [&](int b) {   // mode 1: the loaded indices -> Ix[b]
+#pragma unroll
+    for (int i = 0; i < RX; ++i)
+      if (tid + kThr * i < TOK * ncb) Ix[b * TOK * 32 + tid + kThr * i] = rx[i];
   };
   auto store = [&](int64_t t, int buf) {
     const int64_t tok0 = t * TOK;
@@ -182,21 +206,31 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
         *reinterpret_cast<hv4*>(&As[buf][NPA - 1][row * kRow + 4 * k4]) = l;
       }
     } else {
-#pragma unroll
+#pragma unroll 1
       for (int i = 0; i < SU1; ++i) {
         const int u = tid + kThr * i;
         if (u < TOK * (kKp / 8)) {
           const int row = u / (kKp / 8), k0 = 8 * (u - row * (kKp / 8));
-          const int c0 = k0 / cd;
           const bool live = tok0 + row < n;
-          const int i0 = ri[i][0], i1 = ri[i][1];
+          int c0, c1, sh;
+          unit_cb(min(k0, K - 1), c0, c1, sh);
+          const int i0 = Ix[buf * TOK * 32 + row * ncb + c0], i1 = Ix[buf * TOK * 32 + row * ncb + c1];
           hv8 a;
+          if (live && k0 + 8 <= K) {
+            // the unit's 8 code bits (MSB first, lfq.py:117-124 mask 2^(cd-1..0))
+            // out of codebooks c0 / c1's low cd bits, then one LUT read
+            const uint32_t cm = (1u << cd) - 1u;
+            const uint32_t comb = ((uint32_t)i0 & cm) << cd | ((uint32_t)i1 & cm);
+            a = Lut[(comb >> sh) & 0xffu];
+          } else {
+            const int c0 = k0 / cd;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int k = k0 + e, c = k / cd, b = k - c * cd;
-            const int id = c == c0 ? i0 : i1;
-            const bool bit = (id >> (cd - 1 - b)) & 1;
-            a[e] = (_Float16)(live && k < K ? (bit ? scale : -scale) : 0.f);   // lfq.py:117-124
+            for (int e = 0; e < 8; ++e) {
+              const int k = k0 + e, c = k / cd, b = k - c * cd;
+              const int id = c == c0 ? i0 : i1;
+              const bool bit = (id >> (cd - 1 - b)) & 1;
+              a[e] = (_Float16)(live && k < K ? (bit ? scale : -scale) : 0.f);   // lfq.py:117-124
+            }
           }
           *reinterpret_cast<hv8*>(&As[buf][0][row * kRow + k0]) = a;
         }
@@ -217,13 +251,19 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
 
   __syncthreads();   // the zero fill before the first tile's stores
   load(t0);
+  if constexpr (MODE == 1) {
+    put_idx(0);
+    load(t0 + 1);
+    __syncthreads();   // Ix[0]
+  }
   store(t0, 0);
+  if constexpr (MODE == 1) put_idx(1);
   __syncthreads();
-  const int N4 = N >> 2;
+  const int N4 = (N - fbase < 32 * NWB ? N - fbase : 32 * NWB) >> 2;   // the block's float4 outputs per token
   for (int64_t t = t0; t < t1; ++t) {
     const int buf = (int)((t - t0) & 1);
     const int64_t tok0 = t * TOK;
-    load(t + 1);   // past t1: clamped, unused
+    load(MODE == 1 ? t + 2 : t + 1);   // past t1: clamped, unused
     floatx16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -231,6 +271,7 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
       for (int v = 0; v < 16; ++v) acc[m][v] = 0.f;
 #pragma unroll
     for (int s = 0; s < kKS; ++s) {
+      if (!mf) break;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const _Float16* ap = &As[buf][0][(32 * m + l32) * kRow + 8 * half + 16 * s];
@@ -243,6 +284,8 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, wb[0][s], acc[m], 0, 0, 0);
       }
     }
+    // mode 1: keep the next tile's staging out of the MFMA chain's registers
+    if constexpr (MODE == 1) __builtin_amdgcn_sched_barrier(0);
     // C/D map: feature = col (lane & 31), token row = 32 m + (v & 3) + 8 (v >> 2) + 4 half
     f32x4v tm[MODE == 1 ? U1 : 1], tbv[MODE == 1 ? U1 : 1];
     if constexpr (MODE == 0) {
@@ -251,29 +294,37 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
       uint32_t* msk = Msk + buf * TOK * kMw;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        int wlo = 0, whi = 0;
-        static_for(std::make_integer_sequence<int, 16>{}, [&](auto V) {
-          constexpr int v = decltype(V)::value;
+        // (v_cndmask on the ballot's SGPRs: the compiler inserts the wait states
+        // a VALU read of a VALU-written SGPR needs; an inline-asm v_writelane
+        // right behind the v_cmp read stale SGPRs -- wrong words for most rows)
+        uint32_t wlo = 0, whi = 0;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
           const uint64_t mk = __ballot(acc[m][v] > thr);   // h > 0, lfq.py:175 (NaN -> False)
-          writelane<v>(wlo, (uint32_t)mk);
-          writelane<v>(whi, (uint32_t)(mk >> 32));
-        });
+          const bool mine = lane == v;
+          wlo = mine ? (uint32_t)mk : wlo;
+          whi = mine ? (uint32_t)(mk >> 32) : whi;
+        }
         if (lane < 16) {
           const int row = 32 * m + (lane & 3) + 8 * (lane >> 2);
-          msk[row * kMw + wave] = (uint32_t)wlo;
-          msk[(row + 4) * kMw + wave] = (uint32_t)whi;
+          msk[row * kMw + wave] = wlo;
+          msk[(row + 4) * kMw + wave] = whi;
         }
       }
     } else {
-      float* ys = Ys + buf * TOK * kYs;
+      float* ys = Ys + buf * TOK * kYsB;
       if (col < N) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
           for (int v = 0; v < 16; ++v)
-            ys[(32 * m + (v & 3) + 8 * (v >> 2) + 4 * half) * kYs + col] = acc[m][v] * unscale + bb;
+            ys[(32 * m + (v & 3) + 8 * (v >> 2) + 4 * half) * kYsB + col - fbase] = acc[m][v] * unscale + bb;
       }
-      // this tile's table pieces, in flight during the next tile's staging and the barrier
+    }
+    if (t + 1 < t1) store(t + 1, buf ^ 1);
+    if constexpr (MODE == 1) {
+      put_idx(buf);   // Ix[buf] held tile t's indices, read by the staging before the last barrier
+      // this tile's table pieces, in flight during the barrier
       if (inv.ch) {
 #pragma unroll
         for (int i = 0; i < U1; ++i) {
@@ -281,13 +332,12 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
           const int64_t tb = u < TOK * N4 ? Tb[buf * TOK + row] : -2;
           tm[i] = tbv[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
           if (tb >= 0) {
-            tm[i] = *reinterpret_cast<const f32x4v*>(inv.med + tb + 4 * c4);
-            tbv[i] = *reinterpret_cast<const f32x4v*>(inv.b + tb + 4 * c4);
+            tm[i] = *reinterpret_cast<const f32x4v*>(inv.med + tb + fbase + 4 * c4);
+            tbv[i] = *reinterpret_cast<const f32x4v*>(inv.b + tb + fbase + 4 * c4);
           }
         }
       }
     }
-    if (t + 1 < t1) store(t + 1, buf ^ 1);
     __syncthreads();
     if constexpr (MODE == 0) {
       // (token i, codebook c) pairs of the tile, token-major: contiguous stores
@@ -308,12 +358,12 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
     } else {
       // outputs as float4 pieces along each token's N floats, the inverse
       // PatchNorm on the prefetched table pieces (same fp32 ops as dctae_norm_inverse)
-      const float* ys = Ys + buf * TOK * kYs;
+      const float* ys = Ys + buf * TOK * kYsB;
 #pragma unroll
       for (int i = 0; i < U1; ++i) {
         const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
         if (u >= TOK * N4 || tok0 + row >= n) continue;
-        f32x4v y = *reinterpret_cast<const f32x4v*>(ys + row * kYs + 4 * c4);
+        f32x4v y = *reinterpret_cast<const f32x4v*>(ys + row * kYsB + 4 * c4);
         if (inv.ch) {
           const int64_t tb = Tb[buf * TOK + row];
           if (tb >= 0) {
@@ -323,11 +373,15 @@ __global__ __launch_bounds__(kThr) void k_lfq_ws(const float* __restrict__ x, co
             y = f32x4v{1.f, 1.f, 1.f, 1.f} * __int_as_float(0x7fc00000);
           }
         }
-        __builtin_nontemporal_store(y, reinterpret_cast<f32x4v*>(out + (tok0 + row) * N) + c4);
+        __builtin_nontemporal_store(y, reinterpret_cast<f32x4v*>(out + (tok0 + row) * N + fbase) + c4);
       }
     }
   }
 }
+
+#ifndef DCTAE_LFQWS_OUT_NWB
+#define DCTAE_LFQWS_OUT_NWB 4   // project_out: waves per block (4: two blocks per token range; 7: one)
+#endif
 
 int cu_count() {
   static int cached[64] = {0};
@@ -355,21 +409,25 @@ void launch_lfq_ws(int mode, hipStream_t s, const float* x, const int64_t* idx_i
                    const float* bias, int cd, int ncb, float scale, int64_t* idx_out, float* out, uint16_t* idx16,
                    const int64_t* ch, const int64_t* pos, const float* med, const float* nb, float eps, int maxph,
                    int maxpw, int* err, const uint16_t* wsp, int NPw, int Kp, float a_scale) {
-  // mode 0: 64-token tiles (two 32-row MFMA chains per wave), mode 1: 32
-  // (its output tile is staged in LDS twice over)
+  // mode 0: 64-token tiles (two 32-row MFMA chains per wave), 7-wave blocks,
+  // one per CU; mode 1: 32-token tiles, the 7 output tiles split over two
+  // 4-wave blocks per token range, two blocks per CU
   const int tok = mode == 0 ? 64 : 32;
   const int64_t ntiles = (n + tok - 1) / tok;
   if (ntiles <= 0) return;
   const int64_t nb_ = ntiles < cu_count() ? ntiles : cu_count();
   const int64_t per = (ntiles + nb_ - 1) / nb_;
+  const int64_t ranges = (ntiles + per - 1) / per;
   const WsInv inv{ch, pos, med, nb, eps, maxph, maxpw, err};
-  const dim3 g((unsigned)((ntiles + per - 1) / per));
   if (mode == 0)
-    hipLaunchKernelGGL((k_lfq_ws<0, 2>), g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
-                       idx16, inv, wsp, NPw, Kp, a_scale, per);
+    hipLaunchKernelGGL((k_lfq_ws<0, 2, kNW>), dim3((unsigned)ranges), dim3(64 * kNW), 0, s, x, idx_in, n, K, N, bias,
+                       cd, ncb, scale, idx_out, out, idx16, inv, wsp, NPw, Kp, a_scale, per);
+  else if (DCTAE_LFQWS_OUT_NWB == kNW)
+    hipLaunchKernelGGL((k_lfq_ws<1, 1, kNW>), dim3((unsigned)ranges), dim3(64 * kNW), 0, s, x, idx_in, n, K, N, bias,
+                       cd, ncb, scale, idx_out, out, idx16, inv, wsp, NPw, Kp, a_scale, per);
   else
-    hipLaunchKernelGGL((k_lfq_ws<1, 1>), g, dim3(kThr), 0, s, x, idx_in, n, K, N, bias, cd, ncb, scale, idx_out, out,
-                       idx16, inv, wsp, NPw, Kp, a_scale, per);
+    hipLaunchKernelGGL((k_lfq_ws<1, 1, 4>), dim3((unsigned)(2 * ranges)), dim3(256), 0, s, x, idx_in, n, K, N, bias,
+                       cd, ncb, scale, idx_out, out, idx16, inv, wsp, NPw, Kp, a_scale, per);
 }
 
 }  // namespace dctae

@@ -30,6 +30,7 @@ Deviations (documented in DESIGN.md):
 """
 from __future__ import annotations
 
+import math
 import random
 from dataclasses import dataclass
 from typing import Any, Dict, Iterator, List, Optional, Sequence, Tuple
@@ -434,7 +435,10 @@ class DCTAutoencoderFeatureExtractor:
                               want_codes=lcfg is not None, want_patches=want_norm, want_raw=return_raw,
                               want_scores=return_scores)
             if proj:   # codes only: lfq.py:136-187 without the quantized output's project_out
-                res["codes"] = lfq.project_codes(res["patches"])   # fused project_in + sign + pack
+                # fused project_in + sign + pack on the PatchNorm output, whose clamp
+                # (patchnorm.py:163) bounds it: the kernels of BatchEncoder's staged path
+                xb = max(abs(norm.min_val), abs(norm.max_val))
+                res["codes"] = lfq.project_codes(res["patches"], x_bound=xb if 0.0 < xb < math.inf else None)
             pt = res["patches"] if return_patches else res.get("raw")
             if pt is None:
                 pt = torch.empty((plan.n_rows, self.max_seq_len, 0), device=dev)

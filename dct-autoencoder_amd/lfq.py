@@ -83,12 +83,14 @@ class LFQ(nn.Module):
             return None if t is None else t.detach().to(device=dev, dtype=torch.float32).contiguous()
         return f32(lin.weight), f32(lin.bias)
 
-    def project_codes(self, x):
+    def project_codes(self, x, x_bound=None):
         """Indices only (the encode path): x (..., dim) -> (..., num_codebooks),
-        project_in fused with the sign / packing when there are projections."""
+        project_in fused with the sign / packing when there are projections.
+        x_bound: |x| <= x_bound is known (the PatchNorm clamp in
+        encode_batch): the fp16 kernels, as the fused BatchEncoder path."""
         if self._fused_proj():
             w, b = self._proj_w(self.project_in, x.device)
-            return _ops.lfq_project_in(x, w, b, self.cfg(self.project_in.weight.dtype))
+            return _ops.lfq_project_in(x, w, b, self.cfg(self.project_in.weight.dtype), x_bound)
         h = self.project_in(x)
         _, idx = _ops.lfq_forward(h, self.cfg(h.dtype), want_quantized=False)
         return idx

@@ -230,6 +230,17 @@ int dctae_encode_lfq_proj(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_i
 int dctae_lfq_project_in(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, int64_t n, int32_t dim,
                          const float* w_in_dev, const float* b_in_dev, int64_t* indices_dev, void* stream);
 
+/* The same for an x the caller bounds, |x| <= x_bound (NaN aside), e.g. the
+ * PatchNorm output (clamped to [min_val, max_val], patchnorm.py:163) that
+ * DCTAutoencoderFeatureExtractor.encode_batch projects: the operand then
+ * scales exactly into the fp16 range and the projection runs on the fp16
+ * two-piece MFMA kernels -- the ones dctae_encode_lfq_proj uses on its staged
+ * tokens, so both give the same codes (option "gemm_h2" 0: the split-bf16
+ * kernel of dctae_lfq_project_in).  x_bound > 0 and finite. */
+int dctae_lfq_project_in_bounded(dctae_ctx* ctx, const dctae_lfq* lfq, const float* x_dev, int64_t n, int32_t dim,
+                                 const float* w_in_dev, const float* b_in_dev, float x_bound, int64_t* indices_dev,
+                                 void* stream);
+
 /* Decode direction: LFQ.indices_to_codes with project_out (lfq.py:105-127):
  * indices (n, ncb) -> +-scale codes -> out (n, dim) = codes w_out^T + b_out,
  * w_out (dim, ncb*cd), b_out (dim, nullable).  dim <= 256, ncb*cd % 4 == 0,

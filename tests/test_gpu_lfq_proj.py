@@ -235,3 +235,34 @@ def test_w_stationary_kernel_vs_lfq_proj_h2(pkg, fe, pn, lfq_p, sizes):
     for a, r in zip(o1, o0):
         scale = max(1.0, float(r.abs().max()))
         assert torch.all((a - r).abs() <= 1e-5 * scale + 2e-5 * r.abs())
+
+
+@pytest.mark.parametrize("n", [3072 * 3 + 5, 1, 130, 64])
+@pytest.mark.parametrize("ws", [1, 0])
+def test_project_in_bounded_vs_linear(pkg, n, ws):
+    """dctae_lfq_project_in_bounded (|x| <= 6, the PatchNorm clamp: the fp16
+    kernels -- k_lfq_ws with option lfq_ws=1, k_lfq_proj_h2 with 0) against
+    torch fp32 nn.Linear on the CPU, conf/patch14-l.json's 196 -> 16 x 13.
+    Tolerance: a code bit may differ only where the CPU's projected value lies
+    in the band |h| <= 4e-6 (|W| |x| + |b|); ragged n (tiles of 64 / 32)."""
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    dev = torch.device(DEV, 0)
+    torch.manual_seed(n + ws)
+    m = pkg.LFQ(dim=196, codebook_size=2 ** 13, num_codebooks=16).to(DEV).eval()
+    x = (torch.rand(n, 196) * 12 - 6)
+    x[0, :2] = 6.0
+    W, b = m.project_in.weight.detach().cpu(), m.project_in.bias.detach().cpu()
+    w_d, b_d = m._proj_w(m.project_in, dev)
+    try:
+        ops.set_option("lfq_ws", ws, dev)
+        idx = ops.lfq_project_in(x.to(DEV), w_d, b_d, m.cfg(m.project_in.weight.dtype), 6.0).cpu()
+    finally:
+        ops.set_option("lfq_ws", LFQ_WS_DEFAULT, dev)
+    h = F.linear(x, W, b)
+    _, oidx = ref_cpu.lfq_forward(x[None], LCFG, project_in=lambda t: F.linear(t, W, b))
+    diff = idx != oidx[0]
+    band = 4e-6 * F.linear(x.abs(), W.abs(), b.abs())
+    near = (h.abs() <= band).view(n, 16, 13).any(-1)
+    assert torch.all(near[diff]), f"{int((diff & ~near).sum())} codes outside the rounding band"
+    assert int(diff.sum()) <= max(2, idx.numel() // 1000)
