@@ -541,6 +541,11 @@ struct ICols512bLds {
 #ifndef DCTAE_IC5B_WPE
 #define DCTAE_IC5B_WPE 0
 #endif
+// 1: the token map entries two images ahead, the codes one image ahead (issued
+// right after the expansion); 0: map one ahead, codes after the FFT
+#ifndef DCTAE_IC5B_AHEAD2
+#define DCTAE_IC5B_AHEAD2 1
+#endif
 template <int IPB>
 __global__ __launch_bounds__(256)
 #if DCTAE_IC5B_WPE
@@ -569,9 +574,15 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
   // the tokens of image u + 1 in flight during image u: its map entries are
   // loaded right after image u's expansion, its codes (dependent on them)
   // after image u's FFT, before image u's U stores
-  IcTok tk;
+  IcTok tk, tm;   // this image's map entries + codes; the next image's map entries
   icols_map(i0, imgs[i0], c, strip, map, a, tk);
   icols_codes(a, tk);
+#if DCTAE_IC5B_AHEAD2
+  if (IPB > 1) {
+    const int i1 = min(i0 + 1, n_img - 1);
+    icols_map(i1, imgs[i1], c, strip, map, a, tm);
+  }
+#endif
 #pragma unroll
   for (int u = 0; u < IPB; ++u) {
     const int img = i0 + u;
@@ -580,8 +591,19 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
     __syncthreads();   // tables (u = 0) / the previous image's transposes (x aliases xch)
     icols_expand(tk, a, vt, L.u.x, false);
     IcTok tn;
+#if DCTAE_IC5B_AHEAD2
+    // the next image's codes (its map entries arrived during this image's
+    // predecessor) and the map entries of the one after, all in flight
+    // through this image's transform and stores (unconditional: past the end
+    // of the list the last image reloads itself)
+    tn = tm;
+    if (u + 1 < IPB) icols_codes(a, tn);
+    const int img_n2 = min(img + 2, n_img - 1);
+    if (u + 2 < IPB) icols_map(img_n2, imgs[img_n2], c, strip, map, a, tm);
+#else
     const int img_n = min(img + 1, n_img - 1);   // unconditional (the last image reloads itself)
     if (u + 1 < IPB) icols_map(img_n, imgs[img_n], c, strip, map, a, tn);
+#endif
     __syncthreads();
     // conj Z_k, k = j + 16 i (Ys[M + k] = 0 for i >= 12, Ys[N - k] = 0 for k <= 64)
     cf v[16];
@@ -606,7 +628,9 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
     }
     __syncthreads();   // every group's X reads before the transposes
     fft256_group(v, L.u.xch[G], j, j, L.tw2);
+#if !DCTAE_IC5B_AHEAD2
     if (u + 1 < IPB) icols_codes(a, tn);
+#endif
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws + d.ws_t + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
                                                         0x00020000);
 #pragma unroll
