@@ -655,8 +655,12 @@ __global__ __launch_bounds__(256) void k_fft_cols7(const ImgDesc* __restrict__ i
 // XCD-aware: blocks b and b + 8 share an XCD, each XCD lane owns 12 adjacent
 // items (neighbouring strips share L2 lines; their threshold tables stay in
 // that XCD's L2), the next image's T' loads in flight during the transform.
+// Images per block, same-box A/B (1024 x 512^2, NT T', round 5): 2 -> 0.588-
+// 0.590 ms, 3 -> 0.570-0.571 (default: a block's first image, whose loads
+// nothing hides, is a third of its work instead of half), 4 -> 0.581, 6 ->
+// 0.575-0.577, 8 -> 0.579-0.580.
 #ifndef DCTAE_C5B_IPB
-#define DCTAE_C5B_IPB 2
+#define DCTAE_C5B_IPB 3
 #endif
 template <bool THR, int IPB>
 __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ imgs, const int* __restrict__ list,
