@@ -207,6 +207,13 @@ void default_colors(ColorMats& cm) {
   }
 }
 
+// the call-ordering event (order_after_previous / mark_done) only orders this
+// context's calls across streams of one device: no system-scope fence (its
+// cache write-back sat between back-to-back calls)
+#ifndef DCTAE_DONE_EVT_FLAGS
+#define DCTAE_DONE_EVT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
+
 struct Timer {
   dctae_ctx* ctx;
   hipStream_t s;
@@ -797,7 +804,7 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
   c->device = device;
   default_colors(c->cm);
   if (hipEventCreateWithFlags(&c->plan_evt, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->done_evt, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->done_evt, DCTAE_DONE_EVT_FLAGS) != hipSuccess ||
       hipMalloc((void**)&c->err_dev, sizeof(int)) != hipSuccess || hipMemset(c->err_dev, 0, sizeof(int)) != hipSuccess) {
     g_err = "context allocation failed";
     delete c;
