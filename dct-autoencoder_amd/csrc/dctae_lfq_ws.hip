@@ -42,6 +42,12 @@ constexpr int kRow = kKp + 8;        // LDS row stride in halves (108 dwords: th
 constexpr int kMw = 8;               // mask words per token (256 features)
 constexpr int kK4 = 49;              // mode 0: float4 per token row (K = 196, conf/patch14-l.json's dim)
 
+// mode 1's inverse-PatchNorm table pieces of a tile: 1 = loaded at the top of
+// the tile's iteration (in flight during its MFMAs), 0 = after its staging
+#ifndef DCTAE_LFQWS_TAB_EARLY
+#define DCTAE_LFQWS_TAB_EARLY 1
+#endif
+
 struct WsInv {
   const int64_t* ch;    // (n) channels of the tokens, or null: no inverse
   const int64_t* pos;   // (n, 2)
@@ -264,6 +270,21 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(2))) v
     const int buf = (int)((t - t0) & 1);
     const int64_t tok0 = t * TOK;
     load(MODE == 1 ? t + 2 : t + 1);   // past t1: clamped, unused
+    f32x4v tm[MODE == 1 ? U1 : 1], tbv[MODE == 1 ? U1 : 1];
+#if DCTAE_LFQWS_TAB_EARLY
+    // mode 1: this tile's table pieces (Tb[buf]: staged last iteration), in
+    // flight during the MFMAs and the next tile's staging
+    if (MODE == 1 && inv.ch) {
+#pragma unroll
+      for (int i = 0; i < U1; ++i) {
+        const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
+        const int64_t tb = u < TOK * N4 ? Tb[buf * TOK + row] : -2;
+        const int64_t o = tb >= 0 ? tb + fbase + 4 * c4 : 0;   // unconditional loads
+        tm[i] = *reinterpret_cast<const f32x4v*>(inv.med + o);
+        tbv[i] = *reinterpret_cast<const f32x4v*>(inv.b + o);
+      }
+    }
+#endif
     floatx16 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -287,7 +308,6 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(2))) v
     // mode 1: keep the next tile's staging out of the MFMA chain's registers
     if constexpr (MODE == 1) __builtin_amdgcn_sched_barrier(0);
     // C/D map: feature = col (lane & 31), token row = 32 m + (v & 3) + 8 (v >> 2) + 4 half
-    f32x4v tm[MODE == 1 ? U1 : 1], tbv[MODE == 1 ? U1 : 1];
     if constexpr (MODE == 0) {
       // ballot v = rows (v & 3) + 8 (v >> 2) (bits 0-31) and + 4 (bits 32-63) of
       // this wave's 32 features; lane v collects both words, lanes 0-15 store
@@ -325,7 +345,7 @@ __global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(2))) v
     if constexpr (MODE == 1) {
       put_idx(buf);   // Ix[buf] held tile t's indices, read by the staging before the last barrier
       // this tile's table pieces, in flight during the barrier
-      if (inv.ch) {
+      if (!DCTAE_LFQWS_TAB_EARLY && inv.ch) {
 #pragma unroll
         for (int i = 0; i < U1; ++i) {
           const int u = tid + kThr * i, row = u / N4, c4 = u - row * N4;
