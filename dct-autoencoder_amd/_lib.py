@@ -100,6 +100,9 @@ _SIGS = {
     "dctae_decode": ([_P, C.POINTER(FECfg), C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.c_int32,
                       C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32), _P, _P, _P, _P,
                       C.POINTER(Norm), C.POINTER(LFQCfg), _P, _P, _P, _P], C.c_int),
+    "dctae_decode_normed": ([_P, C.POINTER(FECfg), C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.c_int32,
+                             C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int32), _P, _P, _P, _P,
+                             C.POINTER(Norm), _P, _P, _P], C.c_int),
     "dctae_vq_forward": ([_P, C.POINTER(VQCfg), _P, _P, C.c_int64, _P, _P, _P], C.c_int),
     "dctae_vq_codes_from_indices": ([_P, C.POINTER(VQCfg), _P, C.c_int64, _P, _P], C.c_int),
     "dctae_vq_output_from_indices": ([_P, C.POINTER(VQCfg), _P, C.c_int64, _P, _P], C.c_int),

@@ -408,8 +408,10 @@ def vq_from_indices(cfg: VQCfg, idx: torch.Tensor, project_out: bool) -> torch.T
 def decode(p: FEParams, ids: torch.Tensor, key_pad: torch.Tensor, positions: torch.Tensor, channels: torch.Tensor,
            patch_sizes: Sequence, original_sizes: Sequence, codes: Optional[torch.Tensor] = None,
            patches: Optional[torch.Tensor] = None, norm: Optional[NormState] = None,
-           lfq: Optional[LFQCfg] = None) -> List[torch.Tensor]:
-    """dctae_decode; returns a list of (3, H, W) fp32 device images."""
+           lfq: Optional[LFQCfg] = None, normed: bool = False) -> List[torch.Tensor]:
+    """dctae_decode; returns a list of (3, H, W) fp32 device images.  normed:
+    patches are PatchNorm outputs and the inverse_norm runs inside the decode
+    (dctae_decode_normed; norm required, no codes)."""
     dev = _check_dev(ids, key_pad, positions, channels, codes, patches)
     ctx = _lib.context(dev)
     R, S = ids.shape
@@ -442,12 +444,23 @@ def decode(p: FEParams, ids: torch.Tensor, key_pad: torch.Tensor, positions: tor
     cc = codes.long().contiguous() if codes is not None else None
     pp = patches.float().contiguous() if patches is not None else None
     nc = norm.c() if norm is not None else None
-    rc = ctx.lib.dctae_decode(ctx.h, C.byref(p.c(S)), R, C.cast(keep[0], C.POINTER(C.c_int32)), lut_w, n_img,
-                              C.cast(keep[1], C.POINTER(C.c_int32)), C.cast(keep[2], C.POINTER(C.c_int64)),
-                              C.cast(keep[3], C.POINTER(C.c_int32)), ptr(ids_c), ptr(kp), ptr(pos), ptr(ch),
-                              C.byref(nc) if nc is not None else None, C.byref(lfq) if lfq is not None else None,
-                              ptr(cc), ptr(pp), ptr(out), _lib.stream_ptr(dev))
-    ctx.check(rc, "dctae_decode")
+    if normed:
+        if nc is None or codes is not None:
+            raise AssertionError("normed decode needs the PatchNorm state and patches (no codes)")
+        rc = ctx.lib.dctae_decode_normed(ctx.h, C.byref(p.c(S)), R, C.cast(keep[0], C.POINTER(C.c_int32)), lut_w,
+                                         n_img, C.cast(keep[1], C.POINTER(C.c_int32)),
+                                         C.cast(keep[2], C.POINTER(C.c_int64)), C.cast(keep[3], C.POINTER(C.c_int32)),
+                                         ptr(ids_c), ptr(kp), ptr(pos), ptr(ch), C.byref(nc), ptr(pp), ptr(out),
+                                         _lib.stream_ptr(dev))
+        ctx.check(rc, "dctae_decode_normed")
+        check_device_errors(dev)
+    else:
+        rc = ctx.lib.dctae_decode(ctx.h, C.byref(p.c(S)), R, C.cast(keep[0], C.POINTER(C.c_int32)), lut_w, n_img,
+                                  C.cast(keep[1], C.POINTER(C.c_int32)), C.cast(keep[2], C.POINTER(C.c_int64)),
+                                  C.cast(keep[3], C.POINTER(C.c_int32)), ptr(ids_c), ptr(kp), ptr(pos), ptr(ch),
+                                  C.byref(nc) if nc is not None else None, C.byref(lfq) if lfq is not None else None,
+                                  ptr(cc), ptr(pp), ptr(out), _lib.stream_ptr(dev))
+        ctx.check(rc, "dctae_decode")
     imgs = []
     for i in range(n_img):
         h, w = hw[2 * i], hw[2 * i + 1]

@@ -2254,7 +2254,8 @@ int dctae_vq_output_from_indices(dctae_ctx* ctx, const dctae_vq* vq, const int64
 static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDesc>& D, const FftPlan& fpl,
                       int32_t n_rows, const int32_t* img_lut, int32_t lut_w, const int64_t* ids,
                       const uint8_t* key_pad, const int64_t* pos, const int64_t* ch, const dctae_norm* norm,
-                      const dctae_lfq* lfq, const int64_t* codes, const float* patches, float* rgb, hipStream_t s) {
+                      const dctae_lfq* lfq, const int64_t* codes, const float* patches, float* rgb, hipStream_t s,
+                      bool normed) {
   const int n_img = (int)D.size();
   const int S = cfg->max_seq_len, P = cfg->patch_size;
   int64_t wsf = 0;
@@ -2291,11 +2292,13 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
   a.lut_w = lut_w;
   a.S = S;
   a.P = P;
-  a.use_codes = codes ? 1 : 0;
+  a.use_codes = codes ? 1 : (normed ? 2 : 0);
   if (codes) {
     a.cb_dim = lfq->codebook_dim;
     a.ncb = lfq->num_codebooks;
     a.scale = lfq->codebook_scale;
+  }
+  if (codes || normed) {
     a.median = norm->median_dev;
     a.b = norm->b_dev;
     a.eps = norm->eps;
@@ -2332,17 +2335,23 @@ static int decode_fft(dctae_ctx* ctx, const dctae_fe_cfg* cfg, std::vector<ImgDe
   return 0;
 }
 
-int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut, int32_t lut_w,
-                 int32_t n_img, const int32_t* out_hw, const int64_t* out_off, const int32_t* patch_hw,
-                 const int64_t* ids, const uint8_t* key_pad, const int64_t* pos, const int64_t* ch,
-                 const dctae_norm* norm, const dctae_lfq* lfq, const int64_t* codes, const float* patches,
-                 float* rgb, void* stream) {
+// normed: patches are PatchNorm outputs (before inverse_norm); the FFT path
+// applies the inverse in its column kernel (the (c, strip) tables of a block
+// are image-independent), other geometries run dctae_norm_inverse's kernel
+// into the staging buffer first
+static int decode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut,
+                       int32_t lut_w, int32_t n_img, const int32_t* out_hw, const int64_t* out_off,
+                       const int32_t* patch_hw, const int64_t* ids, const uint8_t* key_pad, const int64_t* pos,
+                       const int64_t* ch, const dctae_norm* norm, const dctae_lfq* lfq, const int64_t* codes,
+                       const float* patches, float* rgb, void* stream, bool normed) {
   if (!ctx) return DCTAE_EINVAL;
   hipSetDevice(ctx->device);
   int rc = check_cfg(ctx, cfg);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int P = cfg->patch_size, PP = P * P, S = cfg->max_seq_len;
+  if (normed && (!norm || !norm->median_dev || !norm->b_dev || codes))
+    return fail(ctx, DCTAE_EINVAL, "decode of PatchNorm-space patches needs the PatchNorm tables (and no codes)");
   if (n_rows < 0 || n_img < 0 || lut_w < 1 || !img_lut || (n_img > 0 && (!out_hw || !out_off || !patch_hw || !rgb)))
     return fail(ctx, DCTAE_EINVAL, "bad decode descriptor");
   if (n_rows > 0 && (!ids || !key_pad || !pos || !ch)) return fail(ctx, DCTAE_EINVAL, "NULL batch tensor");
@@ -2389,8 +2398,23 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
     fftdec = D[i].H == 512 && D[i].W == 512 && D[i].qh <= 32 && D[i].qw == D[0].qw;
   FftPlan fpl{};
   if (fftdec) fftdec = fft_plan_for(ctx, 512, P, &fpl) == 0 && fpl.spec == 1;
-  if (fftdec) return decode_fft(ctx, cfg, D, fpl, n_rows, img_lut, lut_w, ids, key_pad, pos, ch, norm, lfq, codes,
-                                patches, rgb, s);
+  if (fftdec)
+    return decode_fft(ctx, cfg, D, fpl, n_rows, img_lut, lut_w, ids, key_pad, pos, ch, norm, lfq, codes, patches,
+                      rgb, s, normed);
+  if (normed && n_rows > 0) {
+    // other geometries: the inverse over every packed token into the staging
+    // buffer (after the previous call, which may still read it), then as patches
+    const int64_t n_tok = (int64_t)n_rows * S;
+    if ((rc = ensure_ws(ctx, 0, (size_t)n_tok * PP * 4))) return rc;
+    order_after_previous(ctx, s);
+    float* inv = reinterpret_cast<float*>(ctx->stage);
+    {
+      Timer t(ctx, s, "norm_inverse");
+      launch_norm(patches, ch, pos, n_tok, PP, cfg->max_patch_h, cfg->max_patch_w, norm->median_dev, norm->b_dev,
+                  norm->eps, norm->min_val, norm->max_val, 1, inv, ctx->err_dev, s);
+    }
+    patches = inv;
+  }
   if ((rc = ensure_ws(ctx, (size_t)(gmap_off + gmap_n) * 4, 256))) return rc;
   const int rows_cap = P * std::max(cfg->max_patch_h, cfg->max_patch_w);
   std::vector<GemmProblem> probs;
@@ -2474,6 +2498,26 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
   HIPCHK(ctx, hipGetLastError());
   mark_done(ctx, s);
   return 0;
+}
+
+int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut, int32_t lut_w,
+                 int32_t n_img, const int32_t* out_hw, const int64_t* out_off, const int32_t* patch_hw,
+                 const int64_t* ids, const uint8_t* key_pad, const int64_t* pos, const int64_t* ch,
+                 const dctae_norm* norm, const dctae_lfq* lfq, const int64_t* codes, const float* patches,
+                 float* rgb, void* stream) {
+  return decode_impl(ctx, cfg, n_rows, img_lut, lut_w, n_img, out_hw, out_off, patch_hw, ids, key_pad, pos, ch, norm,
+                     lfq, codes, patches, rgb, stream, false);
+}
+
+int dctae_decode_normed(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut,
+                        int32_t lut_w, int32_t n_img, const int32_t* out_hw, const int64_t* out_off,
+                        const int32_t* patch_hw, const int64_t* ids, const uint8_t* key_pad, const int64_t* pos,
+                        const int64_t* ch, const dctae_norm* norm, const float* normed_patches, float* rgb,
+                        void* stream) {
+  if (!ctx) return DCTAE_EINVAL;
+  if (n_rows > 0 && !normed_patches) return fail(ctx, DCTAE_EINVAL, "decode needs the PatchNorm-space patches");
+  return decode_impl(ctx, cfg, n_rows, img_lut, lut_w, n_img, out_hw, out_off, patch_hw, ids, key_pad, pos, ch, norm,
+                     nullptr, nullptr, normed_patches, rgb, stream, true);
 }
 
 // ---------------------------------------------------------------------------

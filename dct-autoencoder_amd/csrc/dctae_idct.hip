@@ -159,7 +159,7 @@ __device__ __forceinline__ void icols_map(int img, const ImgDesc& d, int c, int 
 __device__ __forceinline__ void icols_codes(const DecodeArgs& a, IcTok& t) {
   constexpr int KS = 14;
   const int jl = itid() & 15;
-  if (!a.use_codes) return;
+  if (a.use_codes != 1) return;
 #pragma unroll
   for (int r = 0; r < 2; ++r) {   // unconditional loads; the low word of the int64 code (lfq.py:117 .int())
     const int64_t s0 = t.sl[r] >= 0 ? t.sl[r] : 0;
@@ -180,7 +180,7 @@ __device__ __forceinline__ void icols_expand(const IcTok& t, const DecodeArgs& a
 #endif
   const int g16 = tid >> 4, jl = tid & 15;
   float pv[2][KS];
-  if (!a.use_codes) {
+  if (a.use_codes != 1) {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int64_t s0 = t.sl[r] >= 0 ? t.sl[r] : 0;   // unconditional loads
@@ -197,7 +197,12 @@ __device__ __forceinline__ void icols_expand(const IcTok& t, const DecodeArgs& a
 #pragma unroll
       for (int p = 0; p < KS / 2; ++p) {
         float v0, v1;
-        if (a.use_codes) {
+        if (a.use_codes == 2) {
+          // PatchNorm-space tokens (dctae_decode_normed): the inverse with this
+          // thread's (median, std) pair, pn_inverse's fp32 ops
+          v0 = __fadd_rn(__fmul_rn(pv[r][2 * p], vt[r][2 * p].y), vt[r][2 * p].x);
+          v1 = __fadd_rn(__fmul_rn(pv[r][2 * p + 1], vt[r][2 * p + 1].y), vt[r][2 * p + 1].x);
+        } else if (a.use_codes) {
           // bit select by masks: a ?: on the pair lets the compiler select
           // the address instead and move vt to scratch
           const uint32_t m0 = 0u - ((uint32_t)(t.code[r] >> (KS - 1 - 2 * p)) & 1u);
@@ -237,7 +242,11 @@ __device__ __forceinline__ void icols_vt(int c, int strip, const DecodeArgs& a, 
   for (int r = 0; r < 2; ++r) {
     const int h = min(g16 + 16 * r, a.maxph - 1);
     const int64_t tab = (((int64_t)c * a.maxph + h) * a.maxpw + strip) * PP + (jl < KS ? jl : 0) * KS;
-    if (a.use_codes) {
+    if (a.use_codes == 2) {   // (median, b sqrt2 + eps) of pn_inverse
+#pragma unroll
+      for (int p = 0; p < KS; ++p)
+        vt[r][p] = make_float2(a.median[tab + p], __fadd_rn(__fmul_rn(a.b[tab + p], 1.41421353816986083984375f), a.eps));
+    } else if (a.use_codes) {
       const float yp = __fsub_rn(__fmul_rn(1.0f, a.scale * 2.0f), a.scale);
       const float yn = __fsub_rn(__fmul_rn(0.0f, a.scale * 2.0f), a.scale);
 #pragma unroll

@@ -156,7 +156,7 @@ struct DecodeArgs {
   const int64_t* codes;     // (R,S,ncb) when use_codes
   const float* patches;     // (R,S,PP) otherwise
   const int32_t* lut;       // (R, lut_w) row-local id -> image index (-1 = none)
-  int32_t lut_w, S, P, use_codes;
+  int32_t lut_w, S, P, use_codes;   // use_codes: 1 = codes, 0 = patches, 2 = PatchNorm-space patches (FFT path)
   int32_t cb_dim, ncb;
   float scale;
   const float* median;

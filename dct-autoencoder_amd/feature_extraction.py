@@ -496,9 +496,13 @@ class DCTAutoencoderFeatureExtractor:
         if lfq.has_projections:
             dp = dct_patches.shallow_copy()
             if lfq._fused_proj() and lfq.dim == self.patch_size ** 2:
+                # project_out alone, the inverse PatchNorm inside the decode
+                # (dctae_decode_normed)
                 w, b = lfq._proj_w(lfq.project_out, codes.device)
-                dp.patches = _ops.lfq_project_out_inverse_norm(codes, w, b, lfq.cfg(), patchnorm.state(thresholds=False),
-                                                               self.params(), dp.patch_channels, dp.patch_positions)
+                x = _ops.lfq_project_out(codes, w, b, lfq.cfg())
+                return _ops.decode(self.params(dp.key_pad_mask.shape[1]), dp.batched_image_ids, dp.key_pad_mask,
+                                   dp.patch_positions, dp.patch_channels, dp.patch_sizes, dp.original_sizes,
+                                   patches=x, norm=patchnorm.state(thresholds=False), normed=True)
             else:
                 dp.patches = lfq.indices_to_codes(codes)
                 dp.patches = patchnorm.inverse_norm(dp)
@@ -626,6 +630,12 @@ class BatchDecoder:
         # kernel, dctae_lfq_project_out) -> inverse PatchNorm (dctae_norm_inverse)
         # -> the fused decode from tokens
         self.proj = lfq.has_projections
+        # projections: project_out alone (dctae_lfq_project_out) and the
+        # inverse PatchNorm inside the decode's column kernel
+        # (dctae_decode_normed: per-block (c, strip) tables instead of a
+        # per-token table gather); False: project_out with the inverse fused
+        # (dctae_lfq_project_out_inverse_norm) then dctae_decode
+        self.normed_decode = True
         self.out = torch.empty((enc.B, 3, H, W), dtype=torch.float32, device=enc.dev)
 
     def __call__(self, packed) -> torch.Tensor:
@@ -635,6 +645,15 @@ class BatchDecoder:
         lut, hw, offs, phw = self._ptr
         if self.proj:
             from . import _ops
+            if self.lfq._fused_proj() and self.normed_decode:
+                w, b = self.lfq._proj_w(self.lfq.project_out, e.dev)
+                x = _ops.lfq_project_out(packed["codes"], w, b, self.lcfg)
+                rc = e.ctx.lib.dctae_decode_normed(e.ctx.h, C.byref(e._cfg), e.n_rows, lut, self.lut_w, e.B, hw, offs,
+                                                   phw, ptr(packed["image_ids"]), ptr(packed["key_pad_mask"]),
+                                                   ptr(packed["positions"]), ptr(packed["channels"]),
+                                                   C.byref(self._ncfg), ptr(x), ptr(self.out), stream_ptr(e.dev))
+                e.ctx.check(rc, "dctae_decode_normed")
+                return self.out
             if self.lfq._fused_proj():
                 w, b = self.lfq._proj_w(self.lfq.project_out, e.dev)
                 x = _ops.lfq_project_out_inverse_norm(packed["codes"], w, b, self.lcfg, self.norm, e.fe.params(),

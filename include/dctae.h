@@ -325,6 +325,22 @@ int dctae_decode(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const 
                  const dctae_lfq* lfq, const int64_t* codes_dev, const float* patches_dev,
                  float* rgb_dev, void* stream);
 
+/* dctae_decode of PatchNorm-space patches (PatchNorm outputs, e.g. the LFQ
+ * project_out of codes, lfq.py:126-134 / dctae_lfq_project_out): the
+ * PatchNorm.inverse_norm (patchnorm.py:167-177) runs inside the decode --
+ * on 512 x 512 images in the FFT column kernel with the tile's (median, std)
+ * rows held per block (the same fp32 ops as dctae_norm_inverse, so the result
+ * equals dctae_norm_inverse followed by dctae_decode bit for bit), on other
+ * geometries as dctae_norm_inverse into the context's staging buffer first.
+ * Replaces inv_normalize_ (modeling_dct_autoencoder.py:122-127) + the
+ * processor's postprocess (FE:289-310) after LFQ.indices_to_codes with
+ * projections (the codes path: dctae_decode with codes_dev). */
+int dctae_decode_normed(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, const int32_t* img_lut,
+                        int32_t lut_w, int32_t n_img, const int32_t* out_hw, const int64_t* out_off,
+                        const int32_t* patch_hw, const int64_t* image_ids_dev, const uint8_t* key_pad_dev,
+                        const int64_t* positions_dev, const int64_t* channels_dev, const dctae_norm* norm,
+                        const float* normed_patches_dev, float* rgb_dev, void* stream);
+
 /* thr[e] = the smallest fp32 x with PatchNorm(x)[e] > 0, for the n table
  * elements (patchnorm.py:157-165 is monotone in x for a positive std), so
  * that the LFQ bit of a token element is exactly (x >= thr[e]); NaN = never.

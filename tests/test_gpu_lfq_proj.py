@@ -179,6 +179,40 @@ def test_batch_decoder_with_projections(pkg, fe, pn, lfq_p):
         assert torch.equal(got[i], ref[i]), float((got[i] - ref[i]).abs().max())
 
 
+def test_decode_normed_equals_inverse_then_decode(pkg, fe, pn, lfq_p):
+    """dctae_decode_normed (PatchNorm-space tokens, the inverse inside the
+    decode) == dctae_norm_inverse then dctae_decode, bit for bit: on 512^2
+    (the FFT column kernel applies the inverse with per-block tables;
+    BatchDecoder's projections path, against its project_out + inverse path)
+    and on GEMM-path geometries (the inverse into the staging buffer first)."""
+    from importlib import import_module
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    ops = import_module("dct_autoencoder_amd._ops")
+    enc = fe_mod.BatchEncoder(fe, 3, 512, 512, pn, lfq_p, device=DEV)
+    imgs = _images(82, [(512, 512)] * 3)
+    out = enc(torch.stack(imgs).contiguous())
+    dec = fe_mod.BatchDecoder(enc, pn, lfq_p)
+    assert dec.normed_decode
+    a = dec(out).clone()
+    dec.normed_decode = False
+    b = dec(out).clone()
+    assert torch.equal(a, b), float((a - b).abs().max())
+    imgs = _images(83, [(224, 224), (300, 500), (97, 1000)])
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq_p)
+    w, bb = lfq_p._proj_w(lfq_p.project_out, codes.device)
+    x = ops.lfq_project_out(codes, w, bb, lfq_p.cfg())
+    st = pn.state(thresholds=False)
+    args = (fe.params(dp.key_pad_mask.shape[1]), dp.batched_image_ids, dp.key_pad_mask, dp.patch_positions,
+            dp.patch_channels, dp.patch_sizes, dp.original_sizes)
+    got = ops.decode(*args, patches=x, norm=st, normed=True)
+    d2 = dp.shallow_copy()
+    d2.patches = x
+    ref = ops.decode(*args, patches=pn.inverse_norm(d2))
+    assert len(got) == len(ref) == 3
+    for g, r in zip(got, ref):
+        assert torch.equal(g, r), float((g - r).abs().max())
+
+
 def test_project_out_inverse_norm_fused(pkg, fe, pn, lfq_p):
     """dctae_lfq_project_out_inverse_norm == project_out kernel then the
     dctae_norm_inverse kernel, bit for bit (same fp32 ops, no FMA)."""
