@@ -67,13 +67,24 @@ __device__ __forceinline__ int64_t cols_tok(const ImgDesc& d, int c, int strip, 
 // 14 are the 196 contiguous floats Xf[196 h ..], the token's staged layout, so
 // the whole block stores them as 16-byte pieces (49 per token) instead of 14
 // scattered 4-byte stores per lane
+#ifndef DCTAE_TOK_ST_NT
+#define DCTAE_TOK_ST_NT 1
+#endif
+typedef float tok4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void cols_store_tokens(const ImgDesc& d, int c, int strip, const float* Xf, float* dst,
                                                   int C) {
   constexpr int KS = 14;
   for (int e = opaque_tid(); e < d.qh * 49; e += 256) {
     const int h = e / 49, q = e - h * 49;
+    // write-once staging (the projection kernel reads it later, 196 floats a
+    // token): nontemporal, as T'
+#if DCTAE_TOK_ST_NT
+    __builtin_nontemporal_store(reinterpret_cast<const tok4v*>(Xf + KS * KS * h)[q],
+                                reinterpret_cast<tok4v*>(dst + cols_tok(d, c, strip, h, C) * (KS * KS)) + q);
+#else
     reinterpret_cast<float4*>(dst + cols_tok(d, c, strip, h, C) * (KS * KS))[q] =
         reinterpret_cast<const float4*>(Xf + KS * KS * h)[q];
+#endif
   }
 }
 
