@@ -349,7 +349,7 @@ def config_legs(pkg, fe, pn, lfq, dev, rank, steps):
     torch.cuda.synchronize(dev)
     el = (time.perf_counter() - t0) / steps
     out["lfq_projections"]["decode"] = {
-        "workload": "decode of those codes: codes -> project_out -> inverse PatchNorm in one kernel, IDCT -> RGB",
+        "workload": "decode of those codes: codes -> project_out, the inverse PatchNorm inside the decode's column kernel (dctae_decode_normed), IDCT -> RGB",
         "ms_per_step": round(el * 1e3, 4), "value": round(1024 * 512 * 512 / el / 1e6, 1), "unit": "Mpix/s",
         "kernels": kernel_times(lib.context(dev), lambda: decp(packed), 5)}
     del x3, encp, decp, packed
