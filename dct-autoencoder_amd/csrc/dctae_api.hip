@@ -103,6 +103,12 @@ struct dctae_ctx {
   // 2: rocPRIM block radix sort (<= 3072 tokens per image); 1: the bitonic
   // kernel that serves larger images (selectable for the parity tests)
   int sort_kernel = 2;
+  // odd 7-smooth sides (N <= 256, the column kernel's LDS) on the generic FFT
+  // kernels in the real-FFT form (M = N); 0 (default): the GEMM DCT (or
+  // Bluestein) -- measured faster: config 4 6.37-6.39 vs 6.41-6.44 ms with
+  // the odd plans (their sides added ~40 us to each generic FFT launch, the
+  // GEMM launches they left did not shrink)
+  int fft_odd = 0;
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
   // decode columns with k_idct_rows512: 2 = k_idct_cols512b (band-layout U, default), 1 = k_idct_cols512
@@ -648,8 +654,12 @@ constexpr int kBsL[4] = {256, 512, 1024, 2048};
 
 // FFT plan for length N (Makhoul: M = N/2 point complex FFT); -1 if N has no plan
 int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
-  if (!ctx->fft_enabled || N < 4 || (N & 1) || N / 2 > 512) return -1;
-  if ((size_t)16 * (N / 2) * kMaxP > ctx->lds_limit) return -1;
+  // even N: Makhoul on the N / 2 point complex FFT of z[m] = v[2m] + i v[2m + 1];
+  // odd N (ctx->fft_odd): the N point complex FFT of v (the real-FFT form)
+  const bool odd = (N & 1) != 0;
+  const int Mc = odd ? N : N / 2;
+  if (!ctx->fft_enabled || N < 4 || (odd && (!ctx->fft_odd || N < 15)) || Mc > 512) return -1;
+  if ((size_t)16 * Mc * kMaxP > ctx->lds_limit) return -1;
   auto it = ctx->fft_plans.find(N);
   if (it != ctx->fft_plans.end()) {
     *out = it->second;
@@ -659,7 +669,8 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   }
   FftPlan p{};
   p.N = N;
-  p.M = N / 2;
+  p.M = Mc;
+  p.odd = odd ? 1 : 0;
   int m = p.M, np = 0;
   const int rads[7] = {16, 8, 4, 2, 7, 5, 3};
   while (m > 1 && np < 8) {
@@ -693,7 +704,14 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
     double a = -2.0 * pi * k / p.M;
     h[k] = make_float2((float)std::cos(a), (float)std::sin(a));
   }
-  for (int k = 0; k <= p.M; ++k) {
+  for (int k = 0; odd && k <= p.M; ++k) {
+    // X_k = Re(w_k V_k), w_k = s_k e^{-i pi k / (2N)} (Makhoul's reordering holds for odd N)
+    const double sk = (k == 0) ? std::sqrt(1.0 / N) : std::sqrt(2.0 / N);
+    const double t1 = -pi * k / (2.0 * N);
+    h[p.M + 2 * k] = make_float2((float)(std::cos(t1) * sk), (float)(std::sin(t1) * sk));
+    h[p.M + 2 * k + 1] = make_float2(0.0f, 0.0f);
+  }
+  for (int k = 0; !odd && k <= p.M; ++k) {
     // W = alpha (A + B) + beta (A - B), A = Z[k], B = conj Z[M-k]
     //   alpha = a/2 * s, beta = -i * a * e^{-2 pi i k / N} / 2 * s, a = e^{-i pi k / (2N)}
     const double sk = (k == 0) ? std::sqrt(1.0 / N) : std::sqrt(2.0 / N);
@@ -703,7 +721,11 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
     h[p.M + 2 * k] = make_float2((float)ar, (float)ai);
     h[p.M + 2 * k + 1] = make_float2((float)bi, (float)-br);  // -i * (br + i bi) = bi - i br
   }
-  for (int k = 0; k < p.M; ++k) {
+  for (int k = 0; odd && k < p.M; ++k) {   // no DCT-III on odd plans (the FFT decode is 512 only)
+    h[p.M + 2 * (p.M + 1) + 2 * k] = make_float2(0.0f, 0.0f);
+    h[p.M + 2 * (p.M + 1) + 2 * k + 1] = make_float2(0.0f, 0.0f);
+  }
+  for (int k = 0; !odd && k < p.M; ++k) {
     // DCT-III pre-processing (dctae_idct.hip): Z_k = a_k A_k + b_k B_k; stored conjugated
     const double g = std::sqrt(N / 2.0) / p.M;
     const double e = 2.0 * pi * k / N;                       // i e^{i e} = (-sin e, cos e)
@@ -924,6 +946,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
   else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
+  else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1364,7 +1387,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)want_raw, (int64_t)want_norm, ctx->chunk_bytes, ctx->ws_limit,
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
                              64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3 +
-                             4096 * ctx->cols512b + 8192 * ctx->rows_kernel + 65536 * ctx->gemm_h2,
+                             4096 * ctx->cols512b + 8192 * ctx->rows_kernel + 65536 * ctx->gemm_h2 +
+                             131072 * ctx->fft_odd,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);

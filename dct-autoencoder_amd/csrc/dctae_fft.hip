@@ -14,6 +14,9 @@
 //   W_k = alpha_k (Z[k] + conj Z[M-k]) + beta_k (Z[k] - conj Z[M-k]),  k = 0..M
 //   X[k] = Re W_k,  X[N-k] = -Im W_k  (alpha/beta fold the twiddles and the
 //   ortho scale; tables built in float64 on the host, dctae_api.hip).
+// Odd N (plan.odd): M = N, z[m] = v[m] + 0 i, X[k] = Re(w_k Z[k]) with
+//   w_k = s_k e^{-i pi k / (2N)} at post[2 k] (the same reordering; the
+//   real-FFT form of torch_dct.dct, util.py:333, for N without a factor 2).
 #include "dctae_device.h"
 #include "dctae_fft_common.h"
 #include "dctae_launch.h"
@@ -126,6 +129,7 @@ __global__ __launch_bounds__(256) void k_fft_rows(const ImgDesc* __restrict__ im
   const int64_t hw = (int64_t)d.H * d.W;
   const float* src = rgb + d.rgb_off + (int64_t)y0 * N;
   const float gam = 0.430000007152557373046875f;
+  const bool odd = plp->odd != 0;   // block-uniform
   for (int e = tid; e < rows * N; e += nth) {
     const int r = e / N, px = e - r * N;
     const int64_t o = (int64_t)r * N + px;
@@ -134,16 +138,27 @@ __global__ __launch_bounds__(256) void k_fft_rows(const ImgDesc* __restrict__ im
     const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, R_, G_, B_), gam);
     const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, R_, G_, B_), gam);
     const int vidx = (px & 1) ? (N - 1 - (px >> 1)) : (px >> 1);
-    float* a = A + (r * 3) * js + vidx;
+    float* a = A + (r * 3) * js + (odd ? 2 * vidx : vidx);
     a[0] = mat3_row(cm.lms2ipt, 0, l0, l1, l2);
     a[js] = mat3_row(cm.lms2ipt, 1, l0, l1, l2);
     a[2 * js] = mat3_row(cm.lms2ipt, 2, l0, l1, l2);
+    if (odd) a[1] = a[js + 1] = a[2 * js + 1] = 0.0f;
   }
   __syncthreads();
   const JobLayout L{js, 2, 1};
   const float* Z = fft_all(plp, A, B, L, nj, tabs, tid, nth);
   const float2* post = tabs + plp->post_off;
   const int Kw = d.Kw;
+  if (odd) {
+    for (int e = tid; e < nj * Kw; e += nth) {
+      const int job = e / Kw, k = e - job * Kw;
+      const int r = job / 3, c = job - 3 * r;
+      const float* zk = Z + job * js + 2 * k;
+      const float2 w = post[2 * k];
+      ws[d.ws_t + ((int64_t)c * d.H + y0 + r) * Kw + k] = __fsub_rn(__fmul_rn(w.x, zk[0]), __fmul_rn(w.y, zk[1]));
+    }
+    return;
+  }
   for (int e = tid; e < nj * (M + 1); e += nth) {
     const int job = e / (M + 1), k = e - job * (M + 1);
     const int r = job / 3, c = job - 3 * r;
@@ -174,10 +189,17 @@ __global__ __launch_bounds__(256) void k_fft_cols(const ImgDesc* __restrict__ im
   float* B = lds + 2 * M * KS;
   const int tid = threadIdx.x, nth = blockDim.x;
   const float* T = ws + d.ws_t + (int64_t)c * d.H * d.Kw + kx0;
+  const bool odd = plp->odd != 0;   // block-uniform
   for (int e = tid; e < N * KS; e += nth) {
     const int y = e / KS, j = e - y * KS;
     const int vidx = (y & 1) ? (N - 1 - (y >> 1)) : (y >> 1);
-    A[vidx * KS + j] = T[(int64_t)y * d.Kw + j];
+    const float t = T[(int64_t)y * d.Kw + j];
+    if (odd) {
+      A[2 * vidx * KS + j] = t;
+      A[(2 * vidx + 1) * KS + j] = 0.0f;
+    } else {
+      A[vidx * KS + j] = t;
+    }
   }
   __syncthreads();
   const JobLayout L{1, 2 * KS, KS};
@@ -185,11 +207,19 @@ __global__ __launch_bounds__(256) void k_fft_cols(const ImgDesc* __restrict__ im
   float* Xs = (Z == A) ? B : A;
   const float2* post = tabs + plp->post_off;
   const int Kh = d.Kh;
-  for (int e = tid; e < (M + 1) * KS; e += nth) {
-    const int k = e / KS, j = e - k * KS;
-    const float2 W = makhoul_w(Z, L, j, k, M, post);
-    if (k < Kh) Xs[k * KS + j] = W.x;
-    if (k >= 1 && k < M && N - k < Kh) Xs[(N - k) * KS + j] = -W.y;
+  if (odd) {
+    for (int e = tid; e < Kh * KS; e += nth) {
+      const int k = e / KS, j = e - k * KS;
+      const float2 w = post[2 * k];
+      Xs[k * KS + j] = __fsub_rn(__fmul_rn(w.x, Z[2 * k * KS + j]), __fmul_rn(w.y, Z[(2 * k + 1) * KS + j]));
+    }
+  } else {
+    for (int e = tid; e < (M + 1) * KS; e += nth) {
+      const int k = e / KS, j = e - k * KS;
+      const float2 W = makhoul_w(Z, L, j, k, M, post);
+      if (k < Kh) Xs[k * KS + j] = W.x;
+      if (k >= 1 && k < M && N - k < Kh) Xs[(N - k) * KS + j] = -W.y;
+    }
   }
   __syncthreads();
   const int g16 = tid >> 4, jl = tid & 15;

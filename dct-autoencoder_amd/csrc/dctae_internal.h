@@ -82,7 +82,10 @@ struct GemmProblem {
 struct FftPlan {
   int32_t N, M, npass, rows_per_block;
   int32_t radix[8];
-  int32_t spec, spec_pad;  // compile-time specialised kernel id (dctae_fft2.hip), 0 = generic
+  int32_t spec;  // compile-time specialised kernel id (dctae_fft2.hip), 0 = generic
+  // odd N: M = N complex points of the real Makhoul sequence (imaginary parts
+  // zero), X_k = Re(w_k Z_k) with w_k = s_k e^{-i pi k / (2N)} at post[2 k]
+  int32_t odd;
   int64_t tw_off;    // float2 offset of W_M^k (k < M) in the FFT table buffer
   int64_t post_off;  // float2 offset of (alpha_k, beta_k), k = 0..M
   int64_t ipre_off;  // float2 offset of the DCT-III pre-processing table (conj a_k, conj b_k), k < M (dctae_idct.hip)

@@ -391,7 +391,10 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * images on k_cols512w, two tile strips per 7-wave block; bit-identical;
  * measured slower), "lfq_ws" (1, default: the fp16 LFQ projections of the
  * conf/patch14-l.json shapes (196 -> 208 project_in, 208 -> 196 project_out)
- * on the W-stationary kernel k_lfq_ws; 0: k_lfq_proj_h2).
+ * on the W-stationary kernel k_lfq_ws; 0: k_lfq_proj_h2), "fft_odd" (0,
+ * default / 1: odd 7-smooth sides N <= 256 on the generic FFT kernels in the
+ * real-FFT form, M = N; tokens within 2e-6 x max|Y| of the oracle; measured
+ * slower than the MFMA GEMM DCT on the ragged batch).
  * Profiling builds only (make
  * PROFILING=1; the shipped library returns DCTAE_EUNSUP): "bs_ablate",
  * "t_alias" (these write wrong outputs on purpose). */

@@ -564,6 +564,44 @@ def test_224_kernels_odd_shapes_vs_oracle(fe, pn, lfq, ref_tables, shape):
     _encode_vs_oracle(fe, pn, lfq, ref_tables, rng.synth_images(43, [shape] * 3), CFG, f"224 kernels {shape}")
 
 
+@pytest.mark.parametrize("shape", [(105, 225), (225, 105), (245, 63), (189, 175), (135, 256), (256, 135)])
+def test_odd_smooth_sides_fft_vs_oracle(fe, pn, lfq, ref_tables, shape):
+    """Odd 7-smooth sides (N <= 256) on the generic FFT kernels in the
+    real-FFT form (M = N complex points of Makhoul's reordered sequence,
+    X_k = Re(w_k Z_k); option fft_odd, off by default: measured slower than
+    the GEMM DCT on config 4): tokens and codes against the oracle, rows and
+    columns each odd or even."""
+    ops = _ops()
+    ops.set_option("fft_odd", 1)
+    try:
+        _encode_vs_oracle(fe, pn, lfq, ref_tables, rng.synth_images(53, [shape] * 2), CFG, f"odd sides {shape}")
+    finally:
+        ops.set_option("fft_odd", 0)
+
+
+def test_odd_smooth_sides_fft_matches_gemm(fe):
+    """The odd-side FFT plans against the MFMA GEMM DCT they replace
+    (fft_odd=0): the same tokens within 2e-6 x max|Y|."""
+    ops = _ops()
+    xs = rng.synth_images(54, [(105, 225), (243, 175), (63, 98)])
+    outs = {}
+    for odd in (1, 0):
+        ops.set_option("fft_odd", odd)
+        try:
+            outs[odd] = [fe.preprocess(torch.from_numpy(x).to(DEV)) for x in xs]
+        finally:
+            ops.set_option("fft_odd", 0)
+    for a, b in zip(outs[1], outs[0]):
+        # token orders may differ at near-tied scores: match tokens by (c, h, w)
+        ka = {(int(c), int(p[0]), int(p[1])): i for i, (p, c) in enumerate(zip(a["positions"].tolist(),
+                                                                              a["channels"].tolist()))}
+        idx = torch.tensor([ka[(int(c), int(p[0]), int(p[1]))] for p, c in zip(b["positions"].tolist(),
+                                                                                 b["channels"].tolist())])
+        pa, pb = a["patches"][idx].cpu(), b["patches"].cpu()
+        ymax = float(pb.abs().max())
+        assert float((pa - pb).abs().max()) <= 2e-6 * ymax, float((pa - pb).abs().max()) / ymax
+
+
 def test_gemm_h2_accuracy_vs_oracle_and_x3(fe):
     """The encode's DCT GEMMs on k_gemm_h2 (fp16 MFMA, two-piece operands
     scaled into the fp16 range, three products; default) against the oracle's
