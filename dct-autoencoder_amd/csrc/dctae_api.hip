@@ -109,6 +109,13 @@ struct dctae_ctx {
   // the odd plans (their sides added ~40 us to each generic FFT launch, the
   // GEMM launches they left did not shrink)
   int fft_odd = 0;
+  // sides whose FFT plan has no compile-time kernel (spec 0: every 7-smooth N
+  // other than 512 / 224) on the generic LDS Stockham kernels; 0 (default):
+  // the MFMA GEMM DCT, measured faster on every shape tried (same box,
+  // BatchEncoder ms: 256 x 448^2 2.23 -> 1.24, 512 x 256^2 1.19 -> 0.90,
+  // 128 x 480 x 640 1.45 -> 0.80, 256 x 336^2 1.17 -> 0.92, 1024 x 128^2
+  // 0.50 -> 0.49; config 4 6.36-6.39 -> 6.12-6.16)
+  int fft_generic = 0;
   int fft_decode = 1;                 // decode 512^2 batches on the FFT kernels (dctae_idct.hip)
   int dec_rows_kernel = 3;            // decode rows at Kw = 448: 3 = k_idct_rows512, 2 = k_idct_rows2
   // decode columns with k_idct_rows512: 2 = k_idct_cols512b (band-layout U, default), 1 = k_idct_cols512
@@ -665,6 +672,7 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
     *out = it->second;
     out->spec = ctx->fft_spec_enabled ? fft_spec_id(N, out->radix, out->npass, P) : 0;
     if (out->spec) out->rows_per_block = fft_spec_rows_per_block(out->spec);
+    if (!out->spec && !ctx->fft_generic) return -1;   // the GEMM DCT (see dctae_ctx::fft_generic)
     return it->second.npass > 0 ? 0 : -1;
   }
   FftPlan p{};
@@ -751,6 +759,7 @@ int fft_plan_for(dctae_ctx* ctx, int N, int P, FftPlan* out) {
   *out = p;
   out->spec = ctx->fft_spec_enabled ? fft_spec_id(N, out->radix, out->npass, P) : 0;
   if (out->spec) out->rows_per_block = fft_spec_rows_per_block(out->spec);
+  if (!out->spec && !ctx->fft_generic) return -1;   // the GEMM DCT (see dctae_ctx::fft_generic)
   return 0;
 }
 
@@ -947,6 +956,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
   else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
   else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
+  else if (k == "fft_generic") ctx->fft_generic = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1388,7 +1398,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
                              64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3 +
                              4096 * ctx->cols512b + 8192 * ctx->rows_kernel + 65536 * ctx->gemm_h2 +
-                             131072 * ctx->fft_odd,
+                             131072 * ctx->fft_odd + 262144 * ctx->fft_generic,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);

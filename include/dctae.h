@@ -394,7 +394,10 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * on the W-stationary kernel k_lfq_ws; 0: k_lfq_proj_h2), "fft_odd" (0,
  * default / 1: odd 7-smooth sides N <= 256 on the generic FFT kernels in the
  * real-FFT form, M = N; tokens within 2e-6 x max|Y| of the oracle; measured
- * slower than the MFMA GEMM DCT on the ragged batch).
+ * slower than the MFMA GEMM DCT on the ragged batch; needs "fft_generic"),
+ * "fft_generic" (0, default / 1: 7-smooth sides without a compile-time
+ * kernel -- every N but 512 and 224 -- on the generic LDS Stockham FFT
+ * kernels instead of the MFMA GEMM DCT; measured slower on every shape tried).
  * Profiling builds only (make
  * PROFILING=1; the shipped library returns DCTAE_EUNSUP): "bs_ablate",
  * "t_alias" (these write wrong outputs on purpose). */

@@ -532,7 +532,11 @@ def test_fft_path_matches_gemm_path(fe, pn, lfq, shape):
     partial last block."""
     ops = _ops()
     x = torch.from_numpy(np.stack(rng.synth_images(31, [shape] * 2))).to(DEV)
-    ((dp_f, c_f),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    ops.set_option("fft_generic", 1)   # sides without a compile-time kernel on the generic FFT kernels too
+    try:
+        ((dp_f, c_f),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    finally:
+        ops.set_option("fft_generic", 0)
     ops.set_fft(False)
     try:
         ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True)
@@ -573,10 +577,12 @@ def test_odd_smooth_sides_fft_vs_oracle(fe, pn, lfq, ref_tables, shape):
     columns each odd or even."""
     ops = _ops()
     ops.set_option("fft_odd", 1)
+    ops.set_option("fft_generic", 1)
     try:
         _encode_vs_oracle(fe, pn, lfq, ref_tables, rng.synth_images(53, [shape] * 2), CFG, f"odd sides {shape}")
     finally:
         ops.set_option("fft_odd", 0)
+        ops.set_option("fft_generic", 0)
 
 
 def test_odd_smooth_sides_fft_matches_gemm(fe):
@@ -587,10 +593,12 @@ def test_odd_smooth_sides_fft_matches_gemm(fe):
     outs = {}
     for odd in (1, 0):
         ops.set_option("fft_odd", odd)
+        ops.set_option("fft_generic", odd)
         try:
             outs[odd] = [fe.preprocess(torch.from_numpy(x).to(DEV)) for x in xs]
         finally:
             ops.set_option("fft_odd", 0)
+            ops.set_option("fft_generic", 0)
     for a, b in zip(outs[1], outs[0]):
         # token orders may differ at near-tied scores: match tokens by (c, h, w)
         ka = {(int(c), int(p[0]), int(p[1])): i for i, (p, c) in enumerate(zip(a["positions"].tolist(),
@@ -717,10 +725,12 @@ def test_specialised_kernels_match_generic(fe, pn, lfq, shape, variant):
         for k, v in DEFAULTS.items():
             ops.set_option(k, v)
     ops.set_option("fft_spec", 0)
+    ops.set_option("fft_generic", 1)
     try:
         ((dp_g, c_g),) = fe.encode_batch(x, pn, lfq, return_raw=True, return_scores=True)
     finally:
         ops.set_option("fft_spec", 1)
+        ops.set_option("fft_generic", 0)
     kp = dp_s.key_pad_mask.cpu()
     ids_s, ids_g = dp_s.batched_image_ids.cpu(), dp_g.batched_image_ids.cpu()
     for r in range(kp.shape[0]):
