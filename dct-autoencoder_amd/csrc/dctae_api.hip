@@ -477,13 +477,24 @@ GemmProblem gemm(const float* A, int64_t sAc, int64_t sAm, int64_t sAk, const fl
 // of once per XCD.  Groups go to the least-loaded XCD; the lanes are padded to
 // equal length with empty tiles (problem -1, the kernels return at once) so
 // the b % 8 affinity holds to the end of the launch.
+#ifndef DCTAE_DEAL_PROBLEM
+#define DCTAE_DEAL_PROBLEM 1
+#endif
 void xcd_deal_tiles(std::vector<TileRef>& t, const GemmProblem* probs, int share) {
   if (t.size() < 16 || share == 0) return;
   std::vector<std::vector<TileRef>> groups;
   std::map<std::pair<int, int>, size_t> gi;
   for (const TileRef& r : t) {
     const int tn = probs[r.problem].tiles_n;
+#if DCTAE_DEAL_PROBLEM
+    // all tiles of a problem on one XCD: its shared operand (a DCT matrix of up
+    // to ~1 MB pre-split) is fetched into one L2 instead of all eight, and the
+    // per-channel rows re-read by its N tiles hit there too
+    (void)tn;
+    const std::pair<int, int> key{r.problem, 0};
+#else
     const std::pair<int, int> key{r.problem, share == 1 ? r.tile / tn : r.tile % tn};
+#endif
     auto it = gi.find(key);
     if (it == gi.end()) {
       gi[key] = groups.size();
