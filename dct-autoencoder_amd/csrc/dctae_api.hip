@@ -482,19 +482,24 @@ GemmProblem gemm(const float* A, int64_t sAc, int64_t sAm, int64_t sAk, const fl
 #endif
 void xcd_deal_tiles(std::vector<TileRef>& t, const GemmProblem* probs, int share) {
   if (t.size() < 16 || share == 0) return;
+  // with many problems (>= 64, e.g. a batch of images), all tiles of a problem
+  // on one XCD: its shared operand (a DCT matrix of up to ~1 MB pre-split) is
+  // fetched into one L2 instead of all eight, and the per-channel rows re-read
+  // by its N tiles hit there too; with few, the tiles sharing the per-channel
+  // operand's rows (or columns) as the unit, so every XCD gets work
+  int n_prob = 0;
+  {
+    std::vector<int> seen;
+    for (const TileRef& r : t) seen.push_back(r.problem);
+    std::sort(seen.begin(), seen.end());
+    n_prob = (int)(std::unique(seen.begin(), seen.end()) - seen.begin());
+  }
+  const bool per_problem = DCTAE_DEAL_PROBLEM && n_prob >= 64;
   std::vector<std::vector<TileRef>> groups;
   std::map<std::pair<int, int>, size_t> gi;
   for (const TileRef& r : t) {
     const int tn = probs[r.problem].tiles_n;
-#if DCTAE_DEAL_PROBLEM
-    // all tiles of a problem on one XCD: its shared operand (a DCT matrix of up
-    // to ~1 MB pre-split) is fetched into one L2 instead of all eight, and the
-    // per-channel rows re-read by its N tiles hit there too
-    (void)tn;
-    const std::pair<int, int> key{r.problem, 0};
-#else
-    const std::pair<int, int> key{r.problem, share == 1 ? r.tile / tn : r.tile % tn};
-#endif
+    const std::pair<int, int> key{r.problem, per_problem ? 0 : (share == 1 ? r.tile / tn : r.tile % tn)};
     auto it = gi.find(key);
     if (it == gi.end()) {
       gi[key] = groups.size();
@@ -2483,6 +2488,10 @@ static int decode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, int32_t n_rows, 
     probs.push_back(g2);
     add_tiles(t1, pr, g1);
     add_tiles(t2, pr + 1, g2);
+  }
+  if (ctx->xcd_order) {   // as the encode's GEMMs (xcd_deal_tiles): speed only
+    xcd_deal_tiles(t1, probs.data(), 2);
+    xcd_deal_tiles(t2, probs.data(), 1);
   }
   PlanBuf pb;
   size_t d_off = pb.add(D.data(), D.size());
