@@ -529,6 +529,9 @@ __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict
 // an image stages the P spectrum rows it covers (contiguous in Y) through LDS
 // with coalesced loads, then one 16-lane group per tile runs
 // token_epilogue_p on its row held in registers.
+#ifndef DCTAE_TEPI_ROWS
+#define DCTAE_TEPI_ROWS 1
+#endif
 template <int P>
 __global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restrict__ imgs,
                                                          const float* __restrict__ ws, EncParams ep,
@@ -540,10 +543,27 @@ __global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restri
   if (h >= d.qh) return;
   const int Kw = d.Kw, ld = Kw + 1;
   const float* Y = ws + d.ws_y + ((int64_t)c * d.Kh + (int64_t)P * h) * Kw;
+#if DCTAE_TEPI_ROWS
+  // the tile row's P rows column chunk by column chunk: P independent loads per
+  // thread in flight, no per-element division (the flat loop's e / Kw cost
+  // ~20 VALU per element and serialised its loads)
+  for (int x0 = 0; x0 < Kw; x0 += 256) {
+    const int x = x0 + (int)threadIdx.x;
+    const bool on = x < Kw;
+    float a[P];
+#pragma unroll
+    for (int r = 0; r < P; ++r) a[r] = Y[(int64_t)r * Kw + (on ? x : 0)];
+    if (on) {
+#pragma unroll
+      for (int r = 0; r < P; ++r) ys[r * ld + x] = a[r];
+    }
+  }
+#else
   for (int e = threadIdx.x; e < P * Kw; e += 256) {
     const int r = e / Kw;
     ys[r * ld + (e - r * Kw)] = Y[e];
   }
+#endif
   __syncthreads();
   const int g16 = threadIdx.x >> 4, j = threadIdx.x & 15;
   const int jr = j < P ? j : 0;
