@@ -654,7 +654,7 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
 }
 
 #ifndef DCTAE_IC5B_IPB
-#define DCTAE_IC5B_IPB 8
+#define DCTAE_IC5B_IPB 12   // images per block (same-box A/Bs, decode 1024 x 512^2: 4 1.98, 6 1.93, 8 1.925 / 1.960, 12 1.910 / 1.945, 16 2.19 ms)
 #endif
 void launch_idct_cols512b(const ImgDesc* imgs, int n_img, float* ws, const int32_t* map, const float2* tw,
                           const float4* pre, const DecodeArgs& a, hipStream_t s) {
