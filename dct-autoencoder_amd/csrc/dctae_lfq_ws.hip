@@ -420,8 +420,9 @@ int cu_count() {
 bool lfq_ws_fits(int mode, int K, int N, int cd, int ncb) {
   const bool k_ok = mode == 0 ? K == 4 * kK4 : (K > 16 * (kKS - 1) && K <= kKp);
   const bool n_ok = N > 32 * (kNW - 1) && N <= 32 * kNW;
-  // mode 1: an 8-k unit touches at most two codebooks; mode 0: u16 / 31-bit codes
-  const bool cd_ok = mode == 1 ? cd >= 8 : (cd >= 1 && cd <= 16);
+  // mode 1: an 8-k unit touches at most two codebooks (cd >= 8) whose low cd
+  // bits are combined in 32 bits (cd <= 16); mode 0: u16 codes
+  const bool cd_ok = cd <= 16 && (mode == 1 ? cd >= 8 : cd >= 1);
   return k_ok && n_ok && cd_ok && ncb >= 1 && (int64_t)cd * ncb == (mode == 0 ? N : K);
 }
 

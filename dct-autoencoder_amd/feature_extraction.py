@@ -493,9 +493,10 @@ class DCTAutoencoderFeatureExtractor:
         (the decode half of SURVEY §3.4 without the transformer).  With LFQ
         projections the codes go through the fused codes -> project_out kernel and the HIP
         inverse PatchNorm first, and the fused decode starts from the tokens."""
-        if lfq.has_projections:
+        staged = self._staged_out()   # an overridden revert_patching / _transform_image_out (FE:289-310)
+        if lfq.has_projections or staged:
             dp = dct_patches.shallow_copy()
-            if lfq._fused_proj() and lfq.dim == self.patch_size ** 2:
+            if lfq.has_projections and lfq._fused_proj() and lfq.dim == self.patch_size ** 2 and not staged:
                 # project_out alone, the inverse PatchNorm inside the decode
                 # (dctae_decode_normed)
                 w, b = lfq._proj_w(lfq.project_out, codes.device)

@@ -1,0 +1,174 @@
+"""The bench's default paths at the bench's own scale, where size-selected fast
+paths run that the small parity batches never select:
+
+* config 4 exactly as bench.py builds it (1024 ragged images, (H, W) ~
+  U{14..1024}^2 from numpy default_rng(7), pixels from the counter RNG with
+  seed 7): >= 64 GEMM problems, so the encode's row / column GEMM tiles and the
+  decode's GEMM tiles are dealt to XCDs per problem (dctae_api.hip
+  xcd_deal_tiles); sampled images against the oracle (FE:129-177, 364-452,
+  patchnorm.py:157-165, lfq.py:136-187) and bit for bit against a small batch
+  of the same images (the other dealing branch), and decoded images against
+  the oracle's decode (lfq.py:105-134, patchnorm.py:167-177, FE:289-310);
+* the 1024 x 512^2 BatchEncoder with conf/patch14-l.json's LFQ (16 x 2^13,
+  project_in 196 -> 208, lfq.py:54-62, 164-187): k_lfq_ws walks up to 192
+  64-token tiles per block (the next tile's loads in flight), sampled images'
+  codes against fp32 nn.Linear + the oracle's LFQ.
+
+Tolerances: tokens 2e-6 x max|Y|; codes equal outside the guard band (DCT) /
+the fp32 rounding band |h| <= 4e-6 (|W||y| + |b|) (projection); decoded RGB
+1e-5 x image range + 2e-5 relative.  Run on an MI355X.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_cpu
+from test_gpu_parity import _check_image_vs_oracle, _image_slots, _rgb_close
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CFG = ref_cpu.FEConfig()
+
+
+@pytest.fixture(scope="module")
+def setup(pkg, ref_tables):
+    from importlib import import_module
+    ops = import_module("dct_autoencoder_amd._ops")
+    fe_mod = import_module("dct_autoencoder_amd.feature_extraction")
+    fe = pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, 32, 32, 3072)
+    pn = pkg.PatchNorm(32, 32, 14, 3).to(DEV)
+    pn.median.data.copy_(ref_tables.median)
+    pn.b.data.copy_(ref_tables.b)
+    pn.n.data.copy_(ref_tables.n)
+    pn.frozen = True
+    pn.eval()
+    lfq = pkg.LFQ(dim=196, codebook_size=2 ** 14, num_codebooks=14).to(DEV).eval()
+    return ops, fe_mod, fe, pn, lfq
+
+
+def _is_prime(n):
+    return n > 2 and all(n % p for p in range(2, int(n ** 0.5) + 1))
+
+
+def _smooth7(n):
+    for p in (2, 3, 5, 7):
+        while n % p == 0:
+            n //= p
+    return n == 1
+
+
+def _config4_images(ops):
+    """bench.py's config-4 batch at rank 0, image for image."""
+    hw = np.random.default_rng(7).integers(14, 1025, size=(1024, 2))
+    imgs = [ops.synth_images(1, int(h), int(w), seed=7, first_index=i, device=DEV)[0] for i, (h, w) in enumerate(hw)]
+    return hw, imgs
+
+
+def _picks(hw):
+    """first, last, largest, a side < 32, a prime side, an even side with a
+    7-smooth half that has no compile-time FFT kernel (the GEMM DCT)."""
+    n = len(hw)
+    area = hw[:, 0] * hw[:, 1]
+    pick = [0, n - 1, int(area.argmax())]
+    small = [i for i in range(n) if min(hw[i]) < 32]
+    prime = [i for i in range(n) if _is_prime(int(hw[i][0])) or _is_prime(int(hw[i][1]))]
+    smooth = [i for i in range(n) if any(s % 2 == 0 and s not in (224, 512) and s >= 32 and _smooth7(s // 2)
+                                         for s in map(int, hw[i]))]
+    for cand in (small, prime, smooth):
+        assert cand, "the seed-7 sizes have lost a class"
+        pick.append(next(i for i in cand if i not in pick))
+    pick += [1, n // 4, n // 2]
+    return sorted(set(pick))
+
+
+def test_config4_full_batch_vs_oracle_and_small_batch(setup, ref_tables):
+    ops, fe_mod, fe, pn, lfq = setup
+    hw, imgs = _config4_images(ops)
+    ((dp, codes),) = fe.encode_batch(imgs, pn, lfq)            # the timed call's path
+    ((dpr, codes_r),) = fe.encode_batch(imgs, pn, lfq, return_raw=True)
+    ops.check_device_errors(codes.device)
+    assert torch.equal(codes, codes_r), "raw tokens changed the codes"
+    kp, ids = dp.key_pad_mask.cpu(), dp.batched_image_ids.cpu()
+    slots = _image_slots(kp, ids)
+    assert len(slots) == 1024
+    pick = _picks(hw)
+    assert len(pick) >= 8
+    raw, cod = dpr.patches.cpu(), codes.cpu()
+    pos, ch = dp.patch_positions.cpu(), dp.patch_channels.cpu()
+    flips = n = 0
+    for i in pick:
+        r, _, tj = slots[i]
+        assert len(tj) == 3 * min(int(hw[i][0]) // 14, 32) * min(int(hw[i][1]) // 14, 32)
+        f, m = _check_image_vs_oracle(raw[r, tj], cod[r, tj], pos[r, tj], ch[r, tj], imgs[i].cpu().numpy(), ref_tables)
+        flips, n = flips + f, n + m
+    print(f"[config 4, images {pick}, sizes {[tuple(map(int, hw[i])) for i in pick]}] "
+          f"code mismatches inside the guard band: {flips} / {n}")
+    assert flips <= max(2, n // 10000)
+    # the same images in a small batch (< 64 GEMM problems: the other dealing)
+    ((ds, cs),) = fe.encode_batch([imgs[i] for i in pick], pn, lfq)
+    sslots = _image_slots(ds.key_pad_mask.cpu(), ds.batched_image_ids.cpu())
+    for m, i in enumerate(pick):
+        r, _, tj = slots[i]
+        rs, _, tjs = sslots[m]
+        assert torch.equal(cod[r, tj], cs.cpu()[rs, tjs]), f"image {i}: full batch != small batch"
+        assert torch.equal(pos[r, tj], ds.patch_positions.cpu()[rs, tjs])
+        assert torch.equal(ch[r, tj], ds.patch_channels.cpu()[rs, tjs])
+    del dpr, raw
+
+    # decode of the full batch (the dealt decode GEMM tiles) vs the oracle's
+    # decode of the same codes, on the packed rows of 3 sampled images
+    out = fe.decode_batch(dp, codes, pn, lfq)
+    ops.check_device_errors(codes.device)
+    assert len(out) == 1024
+    for i in (0, int((hw[:, 0] * hw[:, 1]).argmax()), 1023):
+        r, im, tj = slots[i]
+        y = ref_cpu.lfq_indices_to_codes(cod[r:r + 1], ref_cpu.LFQConfig())
+        xin = ref_cpu.norm_inverse(ref_tables, y, ch[r:r + 1], pos[r:r + 1, :, 0], pos[r:r + 1, :, 1])
+        row_imgs = [j for j, s in enumerate(slots) if s[0] == r]
+        batch = ref_cpu.Batch(xin, kp[r:r + 1], None, ids[r:r + 1], ch[r:r + 1], pos[r:r + 1],
+                              [dp.patch_sizes[j] for j in row_imgs], [dp.original_sizes[j] for j in row_imgs])
+        refs = ref_cpu.postprocess(batch, CFG)
+        ref = refs[row_imgs.index(i)]
+        a = out[i].cpu()
+        assert a.shape == ref.shape == (3, int(hw[i][0]), int(hw[i][1]))
+        scale = max(1.0, float(ref.abs().max()))
+        ok, dmax = _rgb_close(a, ref, atol=1e-5 * scale, rtol=2e-5)
+        assert ok, (i, dmax, scale)
+
+
+def test_lfq_projections_full_batch_vs_linear(setup):
+    """The bench's lfq_projections leg: BatchEncoder(1024 x 512^2) with
+    LFQ(196, 2^13, 16) (torch.manual_seed(0) as bench.py), whose 3.1 M tokens
+    give k_lfq_ws up to 192 tiles per block; images 0, 511 and 1023 (the last
+    block's tail) against fp32 nn.Linear + the oracle's LFQ on the GPU's own
+    PatchNorm output, and bit-equal to encode_batch's codes of those images."""
+    ops, fe_mod, fe, pn, _ = setup
+    torch.manual_seed(0)
+    from importlib import import_module
+    LFQ = import_module("dct_autoencoder_amd.lfq").LFQ
+    lfq_p = LFQ(dim=196, codebook_size=2 ** 13, num_codebooks=16).to(DEV).eval()
+    x = ops.synth_images(1024, 512, 512, seed=1234, first_index=0, device=DEV)
+    enc = fe_mod.BatchEncoder(fe, 1024, 512, 512, pn, lfq_p, device=DEV)
+    assert enc.proj_staged
+    codes_b = enc(x)["codes"].clone()
+    ops.check_device_errors(codes_b.device)
+    assert codes_b.shape == (1024, 3072, 16)
+    pick = [0, 511, 1023]
+    ((dp, codes_s),) = fe.encode_batch([x[i] for i in pick], pn, lfq_p, return_patches=True)
+    W, b = lfq_p.project_in.weight.detach().cpu(), lfq_p.project_in.bias.detach().cpu()
+    lcfg = ref_cpu.LFQConfig(dim=196, codebook_size=2 ** 13, num_codebooks=16)
+    flips = n = 0
+    for m, i in enumerate(pick):
+        assert torch.equal(codes_b[i], codes_s[m]), f"image {i}: BatchEncoder != encode_batch"
+        y = dp.patches[m].cpu()
+        h = F.linear(y, W, b)
+        _, oidx = ref_cpu.lfq_forward(y[None], lcfg, project_in=lambda t: F.linear(t, W, b))
+        g = codes_b[i].cpu()
+        diff = g != oidx[0]
+        band = 4e-6 * F.linear(y.abs(), W.abs(), b.abs())
+        near = (h.abs() <= band).view(3072, 16, 13).any(-1)
+        assert torch.all(near[diff]), f"image {i}: {int((diff & ~near).sum())} codes outside the rounding band"
+        flips, n = flips + int(diff.sum()), n + g.numel()
+    print(f"[lfq projections 1024 x 512^2, images {pick}] codes inside the rounding band: {flips} / {n}")
+    assert flips <= max(2, n // 1000)

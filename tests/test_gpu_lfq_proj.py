@@ -119,13 +119,16 @@ def test_batch_encoder_with_projections(pkg, fe, pn, lfq_p, B, H):
 
 @pytest.mark.parametrize("dim,cd,ncb,n,bias", [(196, 13, 16, 3072 * 3 + 5, True), (196, 13, 16, 1, True),
                                                (256, 15, 16, 700, True), (64, 5, 4, 130, False),
-                                               (196, 14, 12, 257, True), (12, 31, 4, 64, True)])
+                                               (196, 14, 12, 257, True), (12, 31, 4, 64, True),
+                                               (196, 17, 12, 300, True), (196, 20, 10, 100, True)])
 def test_project_kernels_vs_linear(pkg, dim, cd, ncb, n, bias):
     """dctae_lfq_project_in / _out (the fused MFMA kernels) against torch fp32
     nn.Linear on the CPU.  Tolerance: a code bit may differ only where the CPU's
     projected value lies in the fp32 rounding band |h| <= 4e-6 (|W| |x| + |b|);
     project_out within 2e-5 (|W| |codes| + |b|) (the f32 sum over <= 256 terms
-    in another order)."""
+    in another order).  codebook_dim 17 / 20 with K = 204 / 200 -> 196: shapes
+    k_lfq_ws's project_out must refuse (its code bits are combined in 32 bits,
+    cd <= 16), so they run on k_lfq_proj_h2."""
     torch.manual_seed(dim + cd + n)
     m = pkg.LFQ(dim=dim, codebook_size=2 ** cd, num_codebooks=ncb)
     if not bias:
@@ -271,14 +274,17 @@ def test_w_stationary_kernel_vs_lfq_proj_h2(pkg, fe, pn, lfq_p, sizes):
         assert torch.all((a - r).abs() <= 1e-5 * scale + 2e-5 * r.abs())
 
 
-@pytest.mark.parametrize("n", [3072 * 3 + 5, 1, 130, 64])
+@pytest.mark.parametrize("n", [3072 * 3 + 5, 1, 130, 64, 256 * 64 * 3 + 37])
 @pytest.mark.parametrize("ws", [1, 0])
 def test_project_in_bounded_vs_linear(pkg, n, ws):
     """dctae_lfq_project_in_bounded (|x| <= 6, the PatchNorm clamp: the fp16
     kernels -- k_lfq_ws with option lfq_ws=1, k_lfq_proj_h2 with 0) against
     torch fp32 nn.Linear on the CPU, conf/patch14-l.json's 196 -> 16 x 13.
     Tolerance: a code bit may differ only where the CPU's projected value lies
-    in the band |h| <= 4e-6 (|W| |x| + |b|); ragged n (tiles of 64 / 32)."""
+    in the band |h| <= 4e-6 (|W| |x| + |b|); ragged n (tiles of 64 / 32).
+    n = 256 x 64 x 3 + 37 gives k_lfq_ws four 64-token tiles per block on 256
+    CUs: the persistent loop's later tiles (the next tile's loads in flight),
+    which the bench's 3.1 M-token leg runs."""
     from importlib import import_module
     ops = import_module("dct_autoencoder_amd._ops")
     dev = torch.device(DEV, 0)
@@ -300,3 +306,32 @@ def test_project_in_bounded_vs_linear(pkg, n, ws):
     near = (h.abs() <= band).view(n, 16, 13).any(-1)
     assert torch.all(near[diff]), f"{int((diff & ~near).sum())} codes outside the rounding band"
     assert int(diff.sum()) <= max(2, idx.numel() // 1000)
+
+
+@pytest.mark.parametrize("proj", [True, False])
+def test_decode_batch_honours_out_hooks(pkg, pn, lfq_p, proj):
+    """decode_batch with an overridden _transform_image_out (decode_gif.py:86-91:
+    identity, so postprocess returns the kept spectrum) runs the staged
+    indices_to_codes -> inverse_norm -> postprocess sequence through the hook,
+    with and without LFQ projections; without the override the fused decode
+    runs again and equals the hook's spectrum put through the default
+    _transform_image_out (1e-5 x image range)."""
+    fe2 = pkg.DCTAutoencoderFeatureExtractor(3, 14, 0.0, 32, 32, 3072)
+    lfq = lfq_p if proj else pkg.LFQ(dim=196, codebook_size=2 ** 14, num_codebooks=14).to(DEV).eval()
+    imgs = _images(84, [(224, 224), (300, 500), (512, 512)])
+    ((dp, codes),) = fe2.encode_batch(imgs, pn, lfq)
+    fe2._transform_image_out = lambda t: t
+    spec = fe2.decode_batch(dp, codes, pn, lfq)
+    d2 = dp.shallow_copy()
+    d2.patches = lfq.indices_to_codes(codes)
+    d2.patches = pn.inverse_norm(d2)
+    want = fe2.postprocess(d2)
+    assert len(spec) == len(want) == len(imgs)
+    for s, w, im in zip(spec, want, imgs):
+        assert s.shape == im.shape and torch.equal(s, w)
+    del fe2._transform_image_out
+    rgb = fe2.decode_batch(dp, codes, pn, lfq)
+    for s, r in zip(spec, rgb):
+        back = fe2._transform_image_out(s)
+        scale = max(1.0, float(r.abs().max()))
+        assert torch.all((back - r).abs() <= 1e-5 * scale + 2e-5 * r.abs()), float((back - r).abs().max())
