@@ -135,6 +135,8 @@ struct dctae_ctx {
   // operands scaled into the fp16 range, three products: half k_gemm_x3's
   // MFMAs), 0 = k_gemm_x3
   int gemm_h2 = 1;
+  // images with both passes on the GEMM DCT: T / Y parity-planar (ImgDesc::tperm)
+  int tperm = 1;
   // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
   // (192 < in, out <= 208 / 224): 1 = the W-stationary kernel k_lfq_ws
   // (dctae_lfq_ws.hip), 0 = k_lfq_proj_h2
@@ -980,6 +982,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
   else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
   else if (k == "fft_generic") ctx->fft_generic = value != 0;
+  else if (k == "tperm") ctx->tperm = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }
@@ -1111,6 +1114,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     D[i].plan_h = plan_of(D[i].H);
     D[i].bs = (D[i].plan_w >= 0 && plans[D[i].plan_w].kind == 1 ? 1 : 0) |
               (D[i].plan_h >= 0 && plans[D[i].plan_h].kind == 1 ? 2 : 0);
+    D[i].tperm = ctx->tperm && D[i].plan_w < 0 && D[i].plan_h < 0;
     // band layout: rows on k_rows512pk (Kw = 448) and columns on k_cols512b (Kh = 448)
     D[i].tband = ctx->cols512b && ctx->rows_kernel == 4 && cfg->max_patch_w == 32 && cfg->max_patch_h == 32 &&
                  D[i].H == 512 && D[i].W == 512 && D[i].Kh == 448 && D[i].Kw == 448 && D[i].bs == 0 && D[i].plan_w >= 0 &&
@@ -1223,8 +1227,14 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           // the half DCT matrix (shared by the channels).  T rows y are the GEMM
           // rows, so a wave's stores run along kx (the accumulator's lane-fast
           // dimension; with the roles swapped they strided by Kw floats)
-          GemmProblem g = gemm(ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1, CW, 0, K, 1,
-                               ws + d.ws_t + par, (int64_t)d.Kw * d.H, d.Kw, 2, d.H, M, K, 3);
+          // parity-planar T (tperm: the columns are GEMMs too): each parity's
+          // outputs are contiguous runs (interleaved stores made every line
+          // twice-written: 4.4 GB of writes for 2.7 GB of T on config 4)
+          GemmProblem g = d.tperm ? gemm(ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1, CW, 0,
+                                         K, 1, ws + d.ws_t + (par ? (d.Kw + 1) / 2 : 0), (int64_t)d.Kw * d.H, d.Kw,
+                                         1, d.H, M, K, 3)
+                                  : gemm(ws + d.ws_p + (par ? (d.W + 1) / 2 : 0), (int64_t)d.H * d.W, d.W, 1, CW, 0,
+                                         K, 1, ws + d.ws_t + par, (int64_t)d.Kw * d.H, d.Kw, 2, d.H, M, K, 3);
           attach_x3(ctx, g);
           uint32_t* am = reinterpret_cast<uint32_t*>(ws + j.amax_off) + 2 * li;
           g.amax = am;                               // k_rgb_to_ipt's |max| of the folded IPT
@@ -1421,7 +1431,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
                              64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3 +
                              4096 * ctx->cols512b + 8192 * ctx->rows_kernel + 65536 * ctx->gemm_h2 +
-                             131072 * ctx->fft_odd + 262144 * ctx->fft_generic,
+                             131072 * ctx->fft_odd + 262144 * ctx->fft_generic + 524288 * ctx->tperm,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);

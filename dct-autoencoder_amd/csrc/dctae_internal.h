@@ -33,7 +33,22 @@ struct ImgDesc {
   int32_t bs;        // bit 0: rows, bit 1: columns on the Bluestein kernels (columns: Y + k_tile_epilogue)
   int32_t tband;     // bit 0: the row pass writes T in the band layout T' (512 x 512 on k_rows512pk + k_cols512b);
                      // bit 1: item-major token staging (stage_pos), packed encodes of band images only (qh = qw = 32)
+  int32_t tperm;     // rows AND columns on the GEMM DCT: T and Y hold their kx columns parity-planar, column
+                     // n' = kx / 2 for even kx, ceil(Kw / 2) + kx / 2 for odd kx (each parity problem of the row
+                     // GEMM then stores whole lines; kx_of_col maps back in the tile epilogue)
 };
+
+// tperm images: spectrum column kx of the parity-planar column n'
+__host__ __device__ inline int kx_of_col(const ImgDesc& d, int n) {
+  if (!d.tperm) return n;
+  const int ne = (d.Kw + 1) >> 1;
+  return n < ne ? 2 * n : 2 * (n - ne) + 1;
+}
+// ... and the column n' of spectrum column kx
+__host__ __device__ inline int col_of_kx(const ImgDesc& d, int kx) {
+  if (!d.tperm) return kx;
+  return (kx & 1) ? ((d.Kw + 1) >> 1) + (kx >> 1) : (kx >> 1);
+}
 
 // Token staging position of flat token f = (h qw + w) 3 + c (FE:374-380 order,
 // the sort's tie order): flat, or with tband bit 1 item-major (c qw + w) qh + h,

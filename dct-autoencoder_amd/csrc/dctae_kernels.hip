@@ -518,8 +518,8 @@ __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict
     const int c = f % ep.C, s = f / ep.C, h = s / d.qw, w = s % d.qw;
     float vals[kMaxP];
     if (j < ep.P) {
-      const float* row = Y + ((int64_t)c * d.Kh + (int64_t)ep.P * h + j) * d.Kw + (int64_t)ep.P * w;
-      for (int p2 = 0; p2 < ep.P; ++p2) vals[p2] = row[p2];
+      const float* row = Y + ((int64_t)c * d.Kh + (int64_t)ep.P * h + j) * d.Kw;
+      for (int p2 = 0; p2 < ep.P; ++p2) vals[p2] = row[col_of_kx(d, ep.P * w + p2)];
     }
     token_epilogue(ep, c, h, w, j, g16, vals, d.tok_off + f, sk, rowbits);
   }
@@ -554,14 +554,15 @@ __global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restri
 #pragma unroll
     for (int r = 0; r < P; ++r) a[r] = Y[(int64_t)r * Kw + (on ? x : 0)];
     if (on) {
+      const int kx = kx_of_col(d, x);   // parity-planar Y (tperm) back to natural columns
 #pragma unroll
-      for (int r = 0; r < P; ++r) ys[r * ld + x] = a[r];
+      for (int r = 0; r < P; ++r) ys[r * ld + kx] = a[r];
     }
   }
 #else
   for (int e = threadIdx.x; e < P * Kw; e += 256) {
     const int r = e / Kw;
-    ys[r * ld + (e - r * Kw)] = Y[e];
+    ys[r * ld + kx_of_col(d, e - r * Kw)] = Y[e];
   }
 #endif
   __syncthreads();
