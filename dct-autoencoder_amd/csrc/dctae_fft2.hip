@@ -662,7 +662,15 @@ __global__ __launch_bounds__(256) void k_fft_cols7(const ImgDesc* __restrict__ i
 #ifndef DCTAE_C5B_IPB
 #define DCTAE_C5B_IPB 3
 #endif
-template <bool THR, int IPB>
+// PatchNorm-output columns (cols512b_norm_epilogue): 1 = on, 0 = the generic
+// token epilogue; images per block
+#ifndef DCTAE_C5B_NORM
+#define DCTAE_C5B_NORM 1
+#endif
+#ifndef DCTAE_C5B_NORM_IPB
+#define DCTAE_C5B_NORM_IPB 3
+#endif
+template <bool THR, int IPB, bool NORM = false>
 __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ imgs, const int* __restrict__ list,
                                                   int n_list, const float* __restrict__ ws,
                                                   const float2* __restrict__ tw, const float2* __restrict__ post,
@@ -686,11 +694,13 @@ __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ im
   float2 thr_r[2][7];
   cols_thresholds<THR>(imgs[list[k0]], c, strip, ep, thr_r, nullptr);
   float sb[2] = {0.0f, 0.0f};
-  if (THR) {
+  if (THR || NORM) {
     const int g16 = tid >> 4;
     sb[0] = __fdiv_rn(-(float)(g16 + strip), ep.ci[c]);
     sb[1] = __fdiv_rn(-(float)(g16 + 16 + strip), ep.ci[c]);
   }
+  float2 tn[NORM ? 2 : 1][14];
+  if constexpr (NORM) cols_norm_tables(c, strip, ep, tn);
   TPiece qa[8];
   cols512b_load(c, strip, ws + imgs[list[k0]].ws_t, qa);
   __syncthreads();   // tables
@@ -711,7 +721,7 @@ __global__ __launch_bounds__(256) void k_cols512b(const ImgDesc* __restrict__ im
       if (u + 1 < IPB) cols512b_load(c, strip, ws + imgs[list[min(k + 1, n_list - 1)]].ws_t, qn);
       float4 qf[8];
       t_decode(qa, qf);
-      cols512b_compute<THR>(dk, c, strip, L, qf, pcM, sb, thr_r, ep, sk);
+      cols512b_compute<THR, NORM>(dk, c, strip, L, qf, pcM, sb, thr_r, ep, sk, tn);
       __syncthreads();   // epilogue reads of X before the next image's transposes
       if (u + 1 < IPB) {
 #pragma unroll
@@ -895,7 +905,11 @@ void launch_cols512b(const ImgDesc* imgs, const int* list, int n_list, const flo
                      const float2* post, const EncParams& ep, const TokenSinks& sk, hipStream_t s, bool wide) {
   if (n_list <= 0) return;
   const bool thr = ep.median && ep.thr && !sk.norm && ep.maxph <= 32 && ep.cb_dim == 14 && ep.ncb == 14;
-  const int ipb = thr ? DCTAE_C5B_IPB : 2;
+  // PatchNorm output (LFQ projections' staging, returned patches) with the
+  // tables held per block: no raw copy, codes (if any) one codebook per tile row
+  const bool norm = DCTAE_C5B_NORM && !thr && sk.norm && ep.median && !sk.raw && ep.maxph == 32 && ep.maxpw == 32 &&
+                    (!sk.codes || (ep.cb_dim == 14 && ep.ncb == 14));
+  const int ipb = thr ? DCTAE_C5B_IPB : norm ? DCTAE_C5B_NORM_IPB : 2;
   const int grid = 96 * ((n_list + ipb - 1) / ipb);
   if (thr && wide) {   // two strips per 7-wave block: 48 items
     hipLaunchKernelGGL((k_cols512w<DCTAE_C5B_IPB>), dim3(48 * ((n_list + DCTAE_C5B_IPB - 1) / DCTAE_C5B_IPB)), dim3(448),
@@ -905,6 +919,9 @@ void launch_cols512b(const ImgDesc* imgs, const int* list, int n_list, const flo
   if (thr)
     hipLaunchKernelGGL((k_cols512b<true, DCTAE_C5B_IPB>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, ws, tw,
                        post, ep, sk);
+  else if (norm)
+    hipLaunchKernelGGL((k_cols512b<false, DCTAE_C5B_NORM_IPB, true>), dim3(grid), dim3(256), 0, s, imgs, list, n_list,
+                       ws, tw, post, ep, sk);
   else
     hipLaunchKernelGGL((k_cols512b<false, 2>), dim3(grid), dim3(256), 0, s, imgs, list, n_list, ws, tw, post, ep, sk);
 }

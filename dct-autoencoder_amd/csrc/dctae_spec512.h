@@ -502,11 +502,82 @@ __device__ __forceinline__ void cols512b_load(int c, int strip, const float* __r
 #endif
 }
 
-template <bool THR>
+// PatchNorm-output epilogue of k_cols512b (the LFQ-projection encode's staged
+// tokens, or returned normalised patches; qh = qw = 32): per tile row the
+// PatchNorm (patchnorm.py:157-165, pn_forward's fp32 ops) on the (median, std)
+// pairs this thread holds for the block's (channel, strip) -- loaded once per
+// block, as the threshold path's tables, instead of 28 table loads per thread
+// and image -- scores (FE:409-416), the optional sign codes (one codebook per
+// tile row, MSB first), the values written back in place and stored as
+// 16-byte pieces (cols_store_tokens)
+__device__ __forceinline__ void cols512b_norm_epilogue(const ImgDesc& d, int c, int strip, float* Xf,
+                                                       const float (&sb)[2], const float2 (&tn)[2][14],
+                                                       const EncParams& ep, const TokenSinks& sk) {
+  constexpr int KS = 14;
+  const int tid = opaque_tid();
+  const int g16 = tid >> 4, jl = tid & 15, jlc = min(jl, KS - 1);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int h = g16 + 16 * r;
+    f2v* row = reinterpret_cast<f2v*>(Xf) + (KS * h + jlc) * (KS / 2);
+    float y[KS];
+    uint32_t am = 0, code = 0;
+#pragma unroll
+    for (int p = 0; p < KS / 2; ++p) {
+      const f2v v2 = row[p];
+      am = max(am, max(__float_as_uint(v2.x) & 0x7fffffffu, __float_as_uint(v2.y) & 0x7fffffffu));
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float x = e ? v2.y : v2.x;
+        const float2 t = tn[r][2 * p + e];   // (median, std = b sqrt2 + eps)
+        const float q = __fdiv_rn(__fsub_rn(x, t.x), t.y);
+        const float v = (q != q) ? q : fminf(fmaxf(q, ep.min_val), ep.max_val);   // torch.clamp_ keeps NaN
+        y[2 * p + e] = v;
+        code = 2 * code + (v > 0.0f ? 1u : 0u);
+      }
+    }
+    am = jl < KS ? am : 0u;
+    am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x128, 0xf, 0xf, false));
+    am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x124, 0xf, 0xf, false));
+    am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x122, 0xf, 0xf, false));
+    am = max(am, (uint32_t)__builtin_amdgcn_mov_dpp((int)am, 0x121, 0xf, 0xf, false));
+    const int64_t tok = cols_tok(d, c, strip, h, ep.C);
+    if (jl == 0) sk.scores[tok] = __fadd_rn(__fmul_rn(__uint_as_float(am), ep.mw), sb[r]);
+    if (jl < KS) {
+      if (sk.codes) sk.codes[tok * KS + jl] = (uint16_t)code;
+#pragma unroll
+      for (int p = 0; p < KS / 2; ++p) row[p] = (f2v){y[2 * p], y[2 * p + 1]};
+    }
+  }
+  __syncthreads();
+  cols_store_tokens(d, c, strip, Xf, sk.norm, ep.C);
+}
+
+// (median, b sqrt2 + eps) of this thread's two tile rows h = g16 + 16 r, row jl
+// (lanes 14 / 15: row 13) of the (channel, strip) item
+__device__ __forceinline__ void cols_norm_tables(int c, int strip, const EncParams& ep, float2 (&tn)[2][14]) {
+  constexpr int KS = 14;
+  const int tid = opaque_tid();
+  const int g16 = tid >> 4, jlc = min(tid & 15, KS - 1);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t tab = ((((int64_t)c * ep.maxph + g16 + 16 * r) * ep.maxpw) + strip) * (KS * KS) + (int64_t)jlc * KS;
+    const float2* m2 = reinterpret_cast<const float2*>(ep.median + tab);
+    const float2* b2 = reinterpret_cast<const float2*>(ep.b + tab);
+#pragma unroll
+    for (int p = 0; p < KS / 2; ++p) {
+      const float2 mv = m2[p], bv = b2[p];
+      tn[r][2 * p] = make_float2(mv.x, __fadd_rn(__fmul_rn(bv.x, 1.41421353816986083984375f), ep.eps));
+      tn[r][2 * p + 1] = make_float2(mv.y, __fadd_rn(__fmul_rn(bv.y, 1.41421353816986083984375f), ep.eps));
+    }
+  }
+}
+
+template <bool THR, bool NORM = false>
 __device__ __forceinline__ void cols512b_compute(const ImgDesc& d, int c, int strip, Cols512bLds& L,
                                                  const float4 (&q)[8], const float4 pcM, const float (&sb)[2],
                                                  const float2 (&thr_r)[2][7], const EncParams& ep,
-                                                 const TokenSinks& sk) {
+                                                 const TokenSinks& sk, const float2 (*tn)[14] = nullptr) {
 #pragma clang fp contract(fast)
   constexpr int N = 512, M = 256, KS = 14;
   const int tid = opaque_tid();
@@ -559,6 +630,8 @@ __device__ __forceinline__ void cols512b_compute(const ImgDesc& d, int c, int st
 #endif
   if (THR)
     cols512b_epilogue(d, c, strip, reinterpret_cast<const f2v*>(L.u.X), sb, thr_r, ep, sk);
+  else if (NORM)
+    cols512b_norm_epilogue(d, c, strip, L.u.X, sb, *reinterpret_cast<const float2(*)[2][14]>(tn), ep, sk);
   else
     cols_epilogue<false>(d, c, strip, reinterpret_cast<const f2v*>(L.u.X), sb, thr_r, ep, sk);
 }
