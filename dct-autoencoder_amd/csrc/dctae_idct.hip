@@ -642,6 +642,13 @@ void k_idct_cols512b(const ImgDesc* __restrict__ imgs, int n_img,
 #endif
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(ws + d.ws_t + (int64_t)c * 512 * KW, 0, 512 * KW * 4,
                                                         0x00020000);
+#if defined(DCTAE_PROFILING) && defined(DCTAE_IC_ABL)
+    // profiling ablation: no U' stores (wrong output; a never-true test keeps the transform live)
+    if ((DCTAE_IC_ABL & 4) && v[0].x != 1234.5f) {
+      if (u + 1 < IPB) tk = tn;
+      continue;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float px = mirror16(v[15 - i].x), py = mirror16(v[15 - i].y);
