@@ -20,7 +20,7 @@ token + key_pad share).  roofline.frac = those bytes x images per launch of
 the dominant kernel / that kernel's average launch time / 8 TB/s;
 roofline.frac_end_to_end uses the whole step time; roofline.traffic is the
 dominant kernel's HBM bytes per launch from the committed rocprofv3 PMC
-passes (profiles/pmc_r05.json) and traffic_ratio = traffic / algorithmic.
+passes (profiles/pmc_r06.json) and traffic_ratio = traffic / algorithmic.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
@@ -41,7 +41,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_ACHIEVABLE_GBS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured (float4 copy)
 FP32_MFMA_PEAK_TF = 157.3    # dense fp32 MFMA (= vector) peak
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r05.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r06.json")
 CPU_CAL_FILE = os.path.join(ROOT, "profiles", "cpu_calibration_r02.json")
 
 
