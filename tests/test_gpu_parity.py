@@ -967,3 +967,25 @@ def test_lfq_groupings_regroup_the_same_bits(pkg, fe, pn, lfq, cbd):
     wb = 2 ** torch.arange(cbd - 1, -1, -1, device=DEV)
     want = (bits.reshape(*c_a.shape[:-1], 196 // cbd, cbd).long() * wb).sum(-1)
     assert torch.equal(c_b.long(), want)
+
+
+@pytest.mark.parametrize("shapes", [[(512, 512)] * 3, [(224, 224), (300, 500), (512, 512)]], ids=["band", "mixed"])
+def test_normalised_patches_bit_exact(pkg, fe, pn, lfq, shapes):
+    """The PatchNorm output the fused encode returns (return_patches: on 512^2
+    images the column kernel's epilogue with the tables held per block and the
+    division's reciprocal hoisted, k_cols512b's NORM form; other sizes the
+    generic token epilogue) equals PatchNorm.forward (patchnorm.py:157-165,
+    the standalone kernel, __fdiv_rn) of the same raw tokens bit for bit --
+    including an image with +inf pixels (non-finite coefficients: the full
+    division's path)."""
+    xs = rng.synth_images(57, shapes)
+    xs[-1] = xs[-1].copy()
+    xs[-1][:, 5, 7] = np.inf
+    imgs = [torch.from_numpy(a).to(DEV) for a in xs]
+    ((dp_r, c_r),) = fe.encode_batch(imgs, pn, lfq, return_raw=True)
+    ((dp_n, c_n),) = fe.encode_batch(imgs, pn, lfq, return_patches=True)
+    assert torch.equal(dp_r.patch_positions, dp_n.patch_positions)
+    assert torch.equal(c_r, c_n)
+    ref = pn(dp_r.shallow_copy())
+    assert ref.shape == dp_n.patches.shape
+    assert torch.equal(ref.view(torch.int32), dp_n.patches.view(torch.int32))
