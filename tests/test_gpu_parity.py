@@ -989,3 +989,24 @@ def test_normalised_patches_bit_exact(pkg, fe, pn, lfq, shapes):
     ref = pn(dp_r.shallow_copy())
     assert ref.shape == dp_n.patches.shape
     assert torch.equal(ref.view(torch.int32), dp_n.patches.view(torch.int32))
+
+
+def test_tperm_layout_bit_identical(fe, pn, lfq):
+    """Option tperm (GEMM-path T / Y parity-planar, ImgDesc::tperm) changes only
+    where the row GEMM's parity problems store their outputs: codes, raw tokens
+    and scores equal the interleaved layout's bit for bit (GEMM rows and
+    columns, odd / even sides, a side < 32, and an FFT image in between)."""
+    ops = _ops()
+    xs = [torch.from_numpy(a).to(DEV) for a in rng.synth_images(61, [(333, 517), (512, 512), (29, 700), (448, 449)])]
+    outs = []
+    for tp in (0, 1):
+        ops.set_option("tperm", tp)
+        try:
+            ((dp, codes),) = fe.encode_batch(xs, pn, lfq, return_raw=True, return_scores=True)
+        finally:
+            ops.set_option("tperm", 1)
+        outs.append((dp, codes))
+    (d0, c0), (d1, c1) = outs
+    assert torch.equal(c0, c1)
+    assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
+    assert torch.equal(d0._data["scores"], d1._data["scores"])
