@@ -815,6 +815,8 @@ struct ChunkJob {
   size_t lds_rows, lds_cols;
   int64_t amax_off;   // k_gemm_h2: |max| bits per image (IPT, T) in the workspace, floats
   int h2;             // the job's GEMMs on k_gemm_h2
+  size_t epi_off;     // k_tile_epilogue_p blocks (local image, 3 h + c) of the images with Y in the workspace
+  int n_epi;
 };
 
 struct EncPlan {
@@ -1209,6 +1211,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     std::vector<int32_t> fold;
     std::vector<int2> ipt;
     std::vector<int32_t> pc, pb;
+    std::vector<int2> epi;
     int pc_qw = 0;
     bool pc_ok = cfg->max_patch_h <= 32;   // k_fft_cols7 keeps Kh <= 448 rows
     j.lds_rows = j.lds_cols = 0;
@@ -1261,6 +1264,9 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           j.lds_rows = std::max<size_t>(j.lds_rows, (size_t)2 * p.rows_per_block * 3 * (2 * p.M + 1) * 4);
         }
       }
+      if (d.plan_h < 0 || (d.bs & 2))   // Y in the workspace: the tile epilogue's (tile row, channel) blocks
+        for (int h = 0; h < d.qh; ++h)
+          for (int c = 0; c < 3; ++c) epi.push_back(make_int2(li, 3 * h + c));
       if (d.plan_h < 0) {
         // Y[c][ky][kx] = sum_y CH[ky][y] * T[c][y][kx], folded along y as the rows
         for (int par = 0; par < 2; ++par) {
@@ -1377,6 +1383,8 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     j.pc_off = E.pb.add(pc.data(), pc.size());
     j.n_pb = (int)pb.size();
     j.pb_off = E.pb.add(pb.data(), pb.size());
+    j.n_epi = (int)epi.size();
+    j.epi_off = E.pb.add(epi.data(), epi.size());
   }
   E.plans_off = E.pb.add(plans.data(), plans.size());
   E.all_desc_off = E.pb.add(D.data(), D.size());
@@ -1577,7 +1585,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
       }
     if (j.any_gemm_cols || j.any_bs_cols) {
       Timer t(ctx, st, "tile_epilogue");
-      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, skc, st);
+      launch_tile_epilogue(dd, nj, j.max_T, ctx->ws, epj, skc, st, (const int2*)(pd + j.epi_off), j.n_epi);
     }
     if (j.n_fc[0]) {
       Timer t(ctx, st, "fft_cols");

@@ -532,14 +532,21 @@ __global__ __launch_bounds__(256) void k_tile_epilogue(const ImgDesc* __restrict
 #ifndef DCTAE_TEPI_ROWS
 #define DCTAE_TEPI_ROWS 1
 #endif
+#ifndef DCTAE_TEPI_LIST
+#define DCTAE_TEPI_LIST 1   // 0: the grid over every image x 3 max_patch_h (A/B)
+#endif
+// list (nullable): the (local image, 3 h + c) blocks of the images with Y in the
+// workspace, built on the host (grid = list length): a grid over every image x
+// 3 max_patch_h spent most of its blocks exiting on ragged batches
 template <int P>
 __global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restrict__ imgs,
                                                          const float* __restrict__ ws, EncParams ep,
-                                                         TokenSinks sk) {
+                                                         TokenSinks sk, const int2* __restrict__ list) {
   extern __shared__ float ys[];
-  const ImgDesc d = imgs[blockIdx.y];
+  const int2 jb = list ? list[blockIdx.x] : make_int2((int)blockIdx.y, (int)blockIdx.x);
+  const ImgDesc d = imgs[jb.x];
   if (d.plan_h >= 0 && !(d.bs & 2)) return;
-  const int c = blockIdx.x % 3, h = blockIdx.x / 3;
+  const int c = jb.y % 3, h = jb.y / 3;
   if (h >= d.qh) return;
   const int Kw = d.Kw, ld = Kw + 1;
   const float* Y = ws + d.ws_y + ((int64_t)c * d.Kh + (int64_t)P * h) * Kw;
@@ -577,11 +584,17 @@ __global__ __launch_bounds__(256) void k_tile_epilogue_p(const ImgDesc* __restri
 }
 
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws,
-                          const EncParams& ep, const TokenSinks& sk, hipStream_t s) {
-  if (ep.P == 14 && ep.C == 3 && 14 * (14 * ep.maxpw + 1) * sizeof(float) <= 64 * 1024)
-    hipLaunchKernelGGL(k_tile_epilogue_p<14>, dim3(3 * ep.maxph, n_img), dim3(256),
-                       (size_t)14 * (14 * ep.maxpw + 1) * sizeof(float), s, imgs, ws, ep, sk);
-  else
+                          const EncParams& ep, const TokenSinks& sk, hipStream_t s, const int2* list, int n_list) {
+  if (ep.P == 14 && ep.C == 3 && 14 * (14 * ep.maxpw + 1) * sizeof(float) <= 64 * 1024) {
+    const size_t lds = (size_t)14 * (14 * ep.maxpw + 1) * sizeof(float);
+    if (list && DCTAE_TEPI_LIST) {
+      if (n_list > 0)
+        hipLaunchKernelGGL(k_tile_epilogue_p<14>, dim3(n_list), dim3(256), lds, s, imgs, ws, ep, sk, list);
+    } else {
+      hipLaunchKernelGGL(k_tile_epilogue_p<14>, dim3(3 * ep.maxph, n_img), dim3(256), lds, s, imgs, ws, ep, sk,
+                         (const int2*)nullptr);
+    }
+  } else
     hipLaunchKernelGGL(k_tile_epilogue, dim3((max_T + 63) / 64, n_img), dim3(256), 0, s, imgs, ws, ep, sk);
 }
 

@@ -32,7 +32,7 @@ void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, i
 void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share);
 void split_matrix_h2(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp, int* e_out);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
-                          const TokenSinks& sk, hipStream_t s);
+                          const TokenSinks& sk, hipStream_t s, const int2* list = nullptr, int n_list = 0);
 void launch_sort_pack(const ImgDesc* imgs, int n_img, int np2, const EncParams& ep, const TokenSinks& st,
                       const PackSinks& out, hipStream_t s, int kernel = 1, int max_T = 1 << 30);
 void launch_pad_fill(const int32_t* row_len, int n_rows, const EncParams& ep, uint8_t* key_pad,
