@@ -89,6 +89,12 @@ __device__ __forceinline__ Src make_src(const float* base, int64_t sr, int64_t s
 
 __device__ __forceinline__ f32x8 load_src(const Src& s, int k0, int K) {
   f32x8 v;
+#if defined(DCTAE_PROFILING) && defined(DCTAE_GEMM_ABL) && (DCTAE_GEMM_ABL & 2)
+  // profiling ablation: no fp32 operand loads (wrong output)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = 0.001f * (float)(s.row + e + k0);
+  return v;
+#endif
   if (s.kc) {
     const int o = s.voff + k0 * 4;
     const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, o, 0, 0));
@@ -126,8 +132,12 @@ template <int ROWS>
 __device__ __forceinline__ void split_store(Pieces<ROWS, 2>& L, const Src& s, int rbase, f32x8 v, float scale) {
   const f32x8 vs = v * scale;
   const hv8 h0 = __builtin_convertvector(vs, hv8);
+#if defined(DCTAE_PROFILING) && defined(DCTAE_GEMM_ABL) && (DCTAE_GEMM_ABL & 1)
+  const hv8 h1 = h0;   // profiling ablation: no residual piece (wrong output)
+#else
   const f32x8 r1 = vs - __builtin_convertvector(h0, f32x8);
   const hv8 h1 = __builtin_convertvector(r1, hv8);
+#endif
   const int o = lds_off(rbase + s.row, s.kq);
   *reinterpret_cast<hv8*>(&L.p[0][o]) = h0;
   *reinterpret_cast<hv8*>(&L.p[1][o]) = h1;
