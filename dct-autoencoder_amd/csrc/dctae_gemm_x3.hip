@@ -96,14 +96,22 @@ __device__ __forceinline__ f32x8 load_src(const Src& s, int k0, int K) {
   return v;
 #endif
   if (s.kc) {
+#if defined(DCTAE_PROFILING) && defined(DCTAE_GEMM_ABL) && (DCTAE_GEMM_ABL & 4)
+    const int o = (s.voff + k0 * 4) & 0x3fff0;   // profiling ablation: every tile reads a 256 KB window (L2-resident)
+#else
     const int o = s.voff + k0 * 4;
+#endif
     const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, o, 0, 0));
     const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rsrc, o + 16, 0, 0));
     v = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
   } else {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
+#if defined(DCTAE_PROFILING) && defined(DCTAE_GEMM_ABL) && (DCTAE_GEMM_ABL & 4)
+      v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(s.rsrc, (s.voff + (k0 + e) * s.kstep) & 0x3fffc, 0, 0));
+#else
       v[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(s.rsrc, s.voff + (k0 + e) * s.kstep, 0, 0));
+#endif
   }
   if (k0 + XK > K) {   // last chunk: k past K inside the range
 #pragma unroll
