@@ -397,10 +397,13 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * slower than the MFMA GEMM DCT on the ragged batch; needs "fft_generic"),
  * "fft_generic" (0, default / 1: 7-smooth sides without a compile-time
  * kernel -- every N but 512 and 224 -- on the generic LDS Stockham FFT
- * kernels instead of the MFMA GEMM DCT; measured slower on every shape tried).
- * Profiling builds only (make
- * PROFILING=1; the shipped library returns DCTAE_EUNSUP): "bs_ablate",
- * "t_alias" (these write wrong outputs on purpose). */
+ * kernels instead of the MFMA GEMM DCT; measured slower on every shape tried),
+ * "tperm" (1, default: images with both passes on the GEMM DCT keep their
+ * row-pass output T and spectrum Y parity-planar, so each parity problem of
+ * the row GEMM stores whole lines; 0: interleaved columns; outputs
+ * bit-identical).  Profiling builds only (make PROFILING=1; the shipped
+ * library returns DCTAE_EUNSUP): "bs_ablate", "t_alias", "gate" (these write
+ * wrong outputs on purpose). */
 int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
 
 /* Raise (return DCTAE_EINVAL) if a previous kernel of this context saw an
