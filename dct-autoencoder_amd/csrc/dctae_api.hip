@@ -135,6 +135,9 @@ struct dctae_ctx {
   // operands scaled into the fp16 range, three products: half k_gemm_x3's
   // MFMAs), 0 = k_gemm_x3
   int gemm_h2 = 1;
+  // the encode's row GEMM (with gemm_h2): 1 = k_gemm_h2r (operands streamed to
+  // LDS by buffer_load ... lds), 0 = k_gemm_h2<3, 1>
+  int gemm_dma = 1;
   // images with both passes on the GEMM DCT: T / Y parity-planar (ImgDesc::tperm)
   int tperm = 1;
   // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
@@ -981,6 +984,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "sort_kernel" && (value == 1 || value == 2)) ctx->sort_kernel = (int)value;
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
+  else if (k == "gemm_dma") ctx->gemm_dma = value != 0;
   else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
   else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
   else if (k == "fft_generic") ctx->fft_generic = value != 0;
@@ -1526,7 +1530,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   // row half / column half of a chunk job on a stream
   auto gemm = [&](const ChunkJob& j, size_t tiles_off, int n_tiles, hipStream_t st, int share) {
     if (j.h2)
-      launch_gemm_h2((const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share);
+      launch_gemm_h2((const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share,
+                     ctx->gemm_dma != 0);
     else
       ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share);
   };

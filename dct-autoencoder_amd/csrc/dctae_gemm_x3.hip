@@ -477,9 +477,218 @@ __global__ __launch_bounds__(256, DCTAE_H2_WPE) void k_gemm_h2(const GemmProblem
   gemm_x3_body<NC, SH, true, 2>(p, tm, tn, As, Bs);
 }
 
-void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
+// k_gemm_h2r: k_gemm_h2<3, 1> (the encode's row GEMM: A = the folded IPT of
+// the three channels, k contiguous; B = the pre-split half DCT matrix) with
+// both operands streamed global -> LDS by buffer_load ... lds: no staging
+// registers and no store phase.  A two-stage LDS ring of [A fp32 3 x 64 x 32 |
+// B fp16 2 planes x 128 x 32] (40 KB per stage: two blocks per CU), the next
+// chunk in flight during the current one's MFMAs, one barrier per chunk; A's
+// fp32 fragments are scaled and split into the two fp16 pieces in registers
+// (k past K zeroed there).  The ablations of k_gemm_h2 put ~0.75
+// ms of config 4's 2.3 ms row GEMM in its register-staged A loads.
+// LDS slots: an A row is 8 slots of 4 floats, slot s of row r at s ^ (r & 7);
+// a B row 4 slots of 8 halves at kq ^ swz(r), as Pieces.
+#ifndef DCTAE_GEMM_DMA
+#define DCTAE_GEMM_DMA 1
+#endif
+#ifndef DCTAE_GEMM_DMA_NS   // ring stages: 2 (two blocks per CU) .. 4 (one)
+#define DCTAE_GEMM_DMA_NS 2
+#endif
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int NS>
+__global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __restrict__ probs,
+                                                         const TileRef* __restrict__ tiles) {
+  constexpr int NC = 3, TM = 64, TN = 128;
+  constexpr int A_CH = TM * XK * 4;               // 8 KB per channel
+  constexpr int A_BYTES = NC * A_CH;              // 24 KB
+  constexpr int B_PL = TN * XK * 2;               // 8 KB per plane
+  constexpr int STAGE = A_BYTES + 2 * B_PL;       // 40 KB
+  constexpr int NDMA = 10;                        // buffer_load ... lds per wave per chunk (the waits below)
+  static_assert(NDMA == 10, "k_gemm_h2r: vmcnt immediates");
+  __shared__ __attribute__((aligned(16))) uint8_t ring[NS * STAGE];
+  const TileRef tr = tiles[blockIdx.x];
+  if (tr.problem < 0) return;   // padding of an XCD-dealt list
+  const GemmProblem p = probs[tr.problem];
+  const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, half = lane >> 5, l32 = lane & 31;
+  // the per-channel operand scaled by 2^ea (|max| < 2^14), the output unscaled (gemm_x3_body)
+  float scale = 1.0f, unscale = 1.0f;
+  {
+    const uint32_t mb = *p.amax;
+    int ea = 0;
+    if (mb != 0u && mb < 0x7f800000u) {
+      int e;
+      frexpf(__uint_as_float(mb), &e);
+      ea = min(max(14 - e, -100), 100);
+    }
+    scale = ldexpf(1.0f, ea);
+    unscale = ldexpf(1.0f, -(ea + p.xh_exp));
+  }
+  // A: channel c's element range [0, (M - 1) sAm + K - 1] (sAk = 1, sAm > 0);
+  // wave-instruction j of this wave: channel j / 2, rows 8 rg + lane / 8 with
+  // rg = 4 (j & 1) + wave, LDS slot lane % 8 = k slot (lane % 8) ^ (row & 7);
+  // rows past M: an offset past the range (the load returns 0, no access)
+  const int64_t a_ext = (int64_t)(p.M - 1) * p.sAm + p.K;
+  __amdgpu_buffer_rsrc_t arsrc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    arsrc[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.A + (int64_t)c * p.sAc), 0, (int)(a_ext * 4),
+                                                 0x00020000);
+  int aoff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * (4 * h + wave) + (lane >> 3), s8 = (lane & 7) ^ (row & 7);
+    aoff[h] = m0 + row < p.M ? (int)(((int64_t)(m0 + row) * p.sAm + 4 * s8) * 4) : kOob;
+  }
+  // B: plane j / 2, rows 16 rg + lane / 4 (rg = 4 (j & 1) + wave), LDS slot
+  // lane % 4 = k quad (lane % 4) ^ swz(row); the planes are padded (Rp, xs_ld)
+  const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.Xh), 0, (int)(2 * p.xs_plane * 2),
+                                                      0x00020000);
+  int boff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 16 * (4 * h + wave) + (lane >> 2), kq = (lane & 3) ^ swz(row);
+    boff[h] = ((n0 + row) * p.xs_ld + 8 * kq) * 2;
+  }
+  auto dma = [&](int st, int k0) {
+    uint8_t* base = ring + st * STAGE;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int c = j >> 1, h = j & 1;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc[c], (lds_void_t*)(base + c * A_CH + (4 * h + wave) * 1024), 16,
+                                               (int)((uint32_t)aoff[h] + (uint32_t)k0 * 4u), 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = j >> 1, h = j & 1;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(base + A_BYTES + pl * B_PL + (4 * h + wave) * 1024),
+                                               16, boff[h] + k0 * 2 + pl * (int)(p.xs_plane * 2), 0, 0, 0);
+    }
+  };
+  floatx16 acc[NC][2];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[c][x][r] = 0.0f;
+  const int ra = wm * 32 + l32;   // this lane's A row in the tile
+  auto compute = [&](int st, int k0) {
+    const uint8_t* base = ring + st * STAGE;
+    const float* Af = reinterpret_cast<const float*>(base);
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(base + A_BYTES);
+#pragma unroll
+    for (int ks = 0; ks < XK / 16; ++ks) {
+      const int kq = 2 * ks + half;
+      bf16x8 b[2][2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int rb = wn * 64 + 32 * x + l32;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          b[x][pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + rb * XK + 8 * (kq ^ swz(rb)));
+      }
+      const int kb = k0 + 8 * kq;   // this lane's first k
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float* ar = Af + c * (A_CH / 4) + ra * XK;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(ar + 4 * ((2 * kq) ^ (ra & 7)));
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(ar + 4 * ((2 * kq + 1) ^ (ra & 7)));
+        f32x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        if (kb + 8 > p.K) {   // the last chunk: k past K (the bytes after the row's range) -> 0
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (kb + e >= p.K) v[e] = 0.0f;
+        }
+        const f32x8 vs = v * scale;
+        const hv8 h0 = __builtin_convertvector(vs, hv8);
+        const hv8 h1 = __builtin_convertvector(vs - __builtin_convertvector(h0, f32x8), hv8);
+        const bf16x8 a[2] = {__builtin_bit_cast(bf16x8, h0), __builtin_bit_cast(bf16x8, h1)};
+#pragma unroll
+        for (int x = 0; x < 2; ++x) mfma_pieces(acc[c][x], a, b[x]);
+      }
+    }
+  };
+  // NS - 1 chunks in flight: chunk i lands in stage i % NS; at the top of
+  // iteration i this wave's chunk-i loads are done once at most the younger
+  // chunks' NDMA (NS - 2) loads are outstanding (all, near the end), the
+  // barrier makes that every wave's and frees stage (i - 1) % NS for chunk
+  // i + NS - 1
+  const int nk = (p.K + XK - 1) / XK;
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nk) dma(i, i * XK);
+  for (int i = 0; i < nk; ++i) {
+    if (NS == 2 || i + NS - 2 >= nk)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (NS == 3)
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    __syncthreads();
+    if (i + NS - 1 < nk) dma((i + NS - 1) % NS, (i + NS - 1) * XK);
+    compute(i % NS, i * XK);
+  }
+  __syncthreads();   // the ring is reused below
+  uint32_t mx = 0;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        acc[c][x][r] *= unscale;
+        mx = max(mx, __float_as_uint(acc[c][x][r]) & 0x7fffffffu);
+      }
+  if (p.omax) {   // T's |max| for the column GEMM; one atomic per block (partials in the freed ring)
+    uint32_t* part = reinterpret_cast<uint32_t*>(ring);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    if (lane == 0) part[wave] = mx;
+    __syncthreads();
+    if (tid == 0) atomicMax(p.omax, max(max(part[0], part[1]), max(part[2], part[3])));
+  }
+  // C/D map: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5); row-major
+  // outputs through buffer stores on the channel's range (gemm_x3_body)
+  const int64_t ext = (int64_t)(p.M - 1) * p.sOm + (int64_t)(p.N - 1) * p.sOn + 1;
+  if (p.sOm > 0 && p.sOn > 0 && p.sOm >= (int64_t)(p.N - 1) * p.sOn + 1 && (ext + 160 * p.sOm) * 4 < kOob) {
+    const int sOm4 = (int)(p.sOm * 4);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.O + (int64_t)c * p.sOc, 0, (int)(ext * 4), 0x00020000);
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int gm = m0 + wm * 32 + 4 * half, gn = n0 + wn * 64 + 32 * x + l32;
+        const int vo = gn < p.N ? gm * sOm4 + (int)(gn * p.sOn * 4) : kOob;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c][x][r]), rsrc, vo + ((r & 3) + 8 * (r >> 2)) * sOm4,
+                                                0, 0);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float* O = p.O + (int64_t)c * p.sOc;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * half, gn = n0 + wn * 64 + 32 * x + l32;
+        if (gm < p.M && gn < p.N) O[(int64_t)gm * p.sOm + (int64_t)gn * p.sOn] = acc[c][x][r];
+      }
+  }
+}
+
+void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma) {
   if (n_tiles <= 0) return;
-  if (share == 1)
+  if (share == 1 && dma && DCTAE_GEMM_DMA)
+    hipLaunchKernelGGL(k_gemm_h2r<DCTAE_GEMM_DMA_NS>, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else if (share == 1)
     hipLaunchKernelGGL((k_gemm_h2<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
   else
     hipLaunchKernelGGL((k_gemm_h2<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);

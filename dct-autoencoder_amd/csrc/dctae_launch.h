@@ -29,7 +29,8 @@ void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int 
 // three bf16 planes [3][Rp][Kp] of a row-major fp32 matrix (GemmProblem::Xs)
 void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp);
 // the encode's DCT GEMMs on fp16 MFMAs, two-piece scaled operands (k_gemm_h2; 3 channels, share 1 or 2)
-void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share);
+// share 1 (the encode's row GEMM: A k-contiguous, sAm > 0): dma = k_gemm_h2r
+void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma);
 void split_matrix_h2(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp, int* e_out);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s, const int2* list = nullptr, int n_list = 0);

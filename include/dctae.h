@@ -401,6 +401,9 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * "tperm" (1, default: images with both passes on the GEMM DCT keep their
  * row-pass output T and spectrum Y parity-planar, so each parity problem of
  * the row GEMM stores whole lines; 0: interleaved columns; outputs
+ * bit-identical), "gemm_dma" (1, default: the encode's row GEMM on
+ * k_gemm_h2r, both operands streamed into a two-stage LDS ring by
+ * buffer_load ... lds; 0: k_gemm_h2's register staging; outputs
  * bit-identical).  Profiling builds only (make PROFILING=1; the shipped
  * library returns DCTAE_EUNSUP): "bs_ablate", "t_alias", "gate" (these write
  * wrong outputs on purpose). */

@@ -1010,3 +1010,26 @@ def test_tperm_layout_bit_identical(fe, pn, lfq):
     assert torch.equal(c0, c1)
     assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
     assert torch.equal(d0._data["scores"], d1._data["scores"])
+
+
+def test_gemm_dma_bit_identical(fe, pn, lfq):
+    """Option gemm_dma (the row GEMM k_gemm_h2r streaming its operands into LDS
+    by buffer_load ... lds, against the register-staged k_gemm_h2<3, 1>): the
+    same fp16 pieces in the same MFMA order, so codes, raw tokens and scores are
+    bit-identical (rows past M, k past K, odd / even sides, a side < 32, a side
+    with K a multiple of the 32-deep chunk and an FFT image in between)."""
+    ops = _ops()
+    xs = [torch.from_numpy(a).to(DEV) for a in
+          rng.synth_images(62, [(333, 517), (512, 512), (29, 700), (448, 449), (130, 128), (1000, 67)])]
+    outs = []
+    for dm in (0, 1):
+        ops.set_option("gemm_dma", dm)
+        try:
+            ((dp, codes),) = fe.encode_batch(xs, pn, lfq, return_raw=True, return_scores=True)
+        finally:
+            ops.set_option("gemm_dma", 1)
+        outs.append((dp, codes))
+    (d0, c0), (d1, c1) = outs
+    assert torch.equal(c0, c1)
+    assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
+    assert torch.equal(d0._data["scores"], d1._data["scores"])
