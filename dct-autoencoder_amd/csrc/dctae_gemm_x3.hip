@@ -486,26 +486,51 @@ __global__ __launch_bounds__(256, DCTAE_H2_WPE) void k_gemm_h2(const GemmProblem
 // fp32 fragments are scaled and split into the two fp16 pieces in registers
 // (k past K zeroed there).  The ablations of k_gemm_h2 put ~0.75
 // ms of config 4's 2.3 ms row GEMM in its register-staged A loads.
-// LDS slots: an A row is 8 slots of 4 floats, slot s of row r at s ^ (r & 7);
+// LDS slots: an A row is 8 slots of 4 floats, slot s of row r at s ^ ((r >> 1) & 7)
+// (the 16 rows of a 16-lane ds_read_b128 group then cover the 16 slot
+// positions of the 256-byte bank window: with s ^ (r & 7) rows r and r + 8
+// collided, PMC 37 % of the kernel's LDS cycles in bank conflicts);
 // a B row 4 slots of 8 halves at kq ^ swz(r), as Pieces.
 #ifndef DCTAE_GEMM_DMA
 #define DCTAE_GEMM_DMA 1
 #endif
-#ifndef DCTAE_GEMM_DMA_NS   // ring stages: 2 (two blocks per CU) .. 4 (one)
+#ifndef DCTAE_GEMM_DMA_BR   // the matrix fragments in registers (needs NS >= 3)
+#define DCTAE_GEMM_DMA_BR 0
+#endif
+#ifndef DCTAE_GEMM_DMA_NS   // ring stages
 #define DCTAE_GEMM_DMA_NS 2
 #endif
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <int NS>
-__global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __restrict__ probs,
-                                                         const TileRef* __restrict__ tiles) {
-  constexpr int NC = 3, TM = 64, TN = 128;
-  constexpr int A_CH = TM * XK * 4;               // 8 KB per channel
-  constexpr int A_BYTES = NC * A_CH;              // 24 KB
-  constexpr int B_PL = TN * XK * 2;               // 8 KB per plane
-  constexpr int STAGE = A_BYTES + 2 * B_PL;       // 40 KB
-  constexpr int NDMA = 10;                        // buffer_load ... lds per wave per chunk (the waits below)
-  static_assert(NDMA == 10, "k_gemm_h2r: vmcnt immediates");
+// NS ring stages; BR: the pre-split matrix's fragments loaded straight into
+// registers one chunk ahead (the ring then holds the image operand only)
+template <int NS, bool BR>
+struct H2rShape {
+  static constexpr int NC = 3, TM = 64, TN = 128;
+  static constexpr int A_CH = TM * XK * 4;                  // 8 KB per channel
+  static constexpr int A_BYTES = NC * A_CH;                 // 24 KB
+  static constexpr int B_PL = TN * XK * 2;                  // 8 KB per plane
+  static constexpr int STAGE = A_BYTES + (BR ? 0 : 2 * B_PL);
+  static constexpr int BPC = (160 * 1024) / (NS * STAGE) < 4 ? (160 * 1024) / (NS * STAGE) : 4;   // blocks per CU
+  static constexpr int NDMA_A = 2 * NC;                     // buffer_load ... lds per wave per chunk: image
+  static constexpr int NDMA = NDMA_A + (BR ? 0 : 4);        //   ... and matrix
+};
+
+// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt in bits 3:0 and 15:14, expcnt and lgkmcnt left at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int NS, bool BR>
+__global__ __launch_bounds__(256, (H2rShape<NS, BR>::BPC)) void k_gemm_h2r(const GemmProblem* __restrict__ probs,
+                                                                        const TileRef* __restrict__ tiles) {
+  using S = H2rShape<NS, BR>;
+  constexpr int NC = S::NC, TM = S::TM, TN = S::TN, A_CH = S::A_CH, A_BYTES = S::A_BYTES, B_PL = S::B_PL;
+  constexpr int STAGE = S::STAGE;
+  static_assert(S::BPC >= 1 && NS >= 2, "k_gemm_h2r: ring");
+  static_assert(!BR || NS >= 3, "k_gemm_h2r: BR waits assume a chunk in flight behind the matrix loads");
   __shared__ __attribute__((aligned(16))) uint8_t ring[NS * STAGE];
   const TileRef tr = tiles[blockIdx.x];
   if (tr.problem < 0) return;   // padding of an XCD-dealt list
@@ -515,24 +540,26 @@ __global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __r
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, half = lane >> 5, l32 = lane & 31;
   // the per-channel operand scaled by 2^ea (|max| < 2^14), the output unscaled (gemm_x3_body)
-  float scale = 1.0f, unscale = 1.0f;
+  // (v_ldexp_f32 on the fragments: exact as the multiply, and beside MFMAs a
+  // packed f32 multiply costs ~5x its issue slot, MI355X_MICROARCH.md)
+  int ea = 0;
   {
     const uint32_t mb = *p.amax;
-    int ea = 0;
     if (mb != 0u && mb < 0x7f800000u) {
       int e;
       frexpf(__uint_as_float(mb), &e);
       ea = min(max(14 - e, -100), 100);
     }
-    scale = ldexpf(1.0f, ea);
-    unscale = ldexpf(1.0f, -(ea + p.xh_exp));
   }
+  const float unscale = ldexpf(1.0f, -(ea + p.xh_exp));
   // A: channel c's element range [0, (M - 1) sAm + K - 1] (sAk = 1, sAm > 0);
   // wave-instruction j of this wave: channel j / 2, rows 8 rg + lane / 8 with
-  // rg = 4 (j & 1) + wave, LDS slot lane % 8 = k slot (lane % 8) ^ (row & 7);
+  // rg = 4 (j & 1) + wave, LDS slot lane % 8 = k slot (lane % 8) ^ ((row >> 1) & 7);
   // rows past M: an offset past the range (the load returns 0, no access)
   const int64_t a_ext = (int64_t)(p.M - 1) * p.sAm + p.K;
-  __amdgpu_buffer_rsrc_t arsrc[NC];
+  // (with a template-dependent size this array made the host pass drop the
+  // kernel's launch stub without a diagnostic: undefined symbol at load time)
+  __amdgpu_buffer_rsrc_t arsrc[3];
 #pragma unroll
   for (int c = 0; c < NC; ++c)
     arsrc[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.A + (int64_t)c * p.sAc), 0, (int)(a_ext * 4),
@@ -540,33 +567,51 @@ __global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __r
   int aoff[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int row = 8 * (4 * h + wave) + (lane >> 3), s8 = (lane & 7) ^ (row & 7);
+    const int row = 8 * (4 * h + wave) + (lane >> 3), s8 = (lane & 7) ^ ((row >> 1) & 7);
     aoff[h] = m0 + row < p.M ? (int)(((int64_t)(m0 + row) * p.sAm + 4 * s8) * 4) : kOob;
   }
-  // B: plane j / 2, rows 16 rg + lane / 4 (rg = 4 (j & 1) + wave), LDS slot
-  // lane % 4 = k quad (lane % 4) ^ swz(row); the planes are padded (Rp, xs_ld)
+  // B: the planes are padded (Rp rows, xs_ld k), so every matrix load of a tile is in range
   const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.Xh), 0, (int)(2 * p.xs_plane * 2),
                                                       0x00020000);
+  const int xsp2 = (int)(p.xs_plane * 2);
+  // in the ring: plane j / 2, rows 16 rg + lane / 4 (rg = 4 (j & 1) + wave), LDS
+  // slot lane % 4 = k quad (lane % 4) ^ swz(row)
   int boff[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = 16 * (4 * h + wave) + (lane >> 2), kq = (lane & 3) ^ swz(row);
     boff[h] = ((n0 + row) * p.xs_ld + 8 * kq) * 2;
   }
+  // in registers (BR): this lane's fragments, rows wn 64 + 32 x + l32, k quad 2 ks + half
+  const int bro = ((n0 + wn * 64 + l32) * p.xs_ld + 8 * half) * 2;
   auto dma = [&](int st, int k0) {
     uint8_t* base = ring + st * STAGE;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
+    for (int j = 0; j < 2 * NC; ++j) {
       const int c = j >> 1, h = j & 1;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc[c], (lds_void_t*)(base + c * A_CH + (4 * h + wave) * 1024), 16,
                                                (int)((uint32_t)aoff[h] + (uint32_t)k0 * 4u), 0, 0, 0);
     }
+    if constexpr (!BR) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pl = j >> 1, h = j & 1;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(base + A_BYTES + pl * B_PL + (4 * h + wave) * 1024),
-                                               16, boff[h] + k0 * 2 + pl * (int)(p.xs_plane * 2), 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        const int pl = j >> 1, h = j & 1;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_void_t*)(base + A_BYTES + pl * B_PL + (4 * h + wave) * 1024),
+                                                 16, boff[h] + k0 * 2 + pl * xsp2, 0, 0, 0);
+      }
     }
+  };
+  typedef bf16x8 BFrag[XK / 16][2][2];   // [ks][x][plane]
+  auto load_b = [&](BFrag& f, int k0) {
+#pragma unroll
+    for (int ks = 0; ks < XK / 16; ++ks)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          f[ks][x][pl] = __builtin_bit_cast(
+              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brsrc, bro + (32 * x * p.xs_ld + k0 + 16 * ks) * 2 + pl * xsp2,
+                                                            0, 0));
   };
   floatx16 acc[NC][2];
 #pragma unroll
@@ -576,7 +621,7 @@ __global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __r
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[c][x][r] = 0.0f;
   const int ra = wm * 32 + l32;   // this lane's A row in the tile
-  auto compute = [&](int st, int k0) {
+  auto compute = [&](int st, int k0, const BFrag& bf) {
     const uint8_t* base = ring + st * STAGE;
     const float* Af = reinterpret_cast<const float*>(base);
     const uint16_t* Bp = reinterpret_cast<const uint16_t*>(base + A_BYTES);
@@ -589,48 +634,67 @@ __global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __r
         const int rb = wn * 64 + 32 * x + l32;
 #pragma unroll
         for (int pl = 0; pl < 2; ++pl)
-          b[x][pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + rb * XK + 8 * (kq ^ swz(rb)));
+          b[x][pl] = BR ? bf[ks][x][pl] : *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + rb * XK + 8 * (kq ^ swz(rb)));
       }
       const int kb = k0 + 8 * kq;   // this lane's first k
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const float* ar = Af + c * (A_CH / 4) + ra * XK;
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(ar + 4 * ((2 * kq) ^ (ra & 7)));
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(ar + 4 * ((2 * kq + 1) ^ (ra & 7)));
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(ar + 4 * ((2 * kq) ^ ((ra >> 1) & 7)));
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(ar + 4 * ((2 * kq + 1) ^ ((ra >> 1) & 7)));
         f32x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        if (kb + 8 > p.K) {   // the last chunk: k past K (the bytes after the row's range) -> 0
+        if (k0 + XK > p.K) {   // the last chunk (uniform): k past K (the bytes after the row's range) -> 0
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if (kb + e >= p.K) v[e] = 0.0f;
+          for (int e = 0; e < 8; ++e) v[e] = kb + e < p.K ? v[e] : 0.0f;
         }
-        const f32x8 vs = v * scale;
+        f32x8 vs;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vs[e] = ldexpf(v[e], ea);
         const hv8 h0 = __builtin_convertvector(vs, hv8);
-        const hv8 h1 = __builtin_convertvector(vs - __builtin_convertvector(h0, f32x8), hv8);
+        // the residual vs - h0 (exact) as one mixed-precision FMA per value
+        // (written out: the compiler forms cvt + sub, then packs the subs)
+        const u32x4 hw = __builtin_bit_cast(u32x4, h0);
+        f32x8 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r[2 * e]) : "v"(hw[e]), "v"(vs[2 * e]));
+          asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r[2 * e + 1]) : "v"(hw[e]), "v"(vs[2 * e + 1]));
+        }
+        const hv8 h1 = __builtin_convertvector(r, hv8);
         const bf16x8 a[2] = {__builtin_bit_cast(bf16x8, h0), __builtin_bit_cast(bf16x8, h1)};
 #pragma unroll
         for (int x = 0; x < 2; ++x) mfma_pieces(acc[c][x], a, b[x]);
       }
     }
   };
-  // NS - 1 chunks in flight: chunk i lands in stage i % NS; at the top of
-  // iteration i this wave's chunk-i loads are done once at most the younger
-  // chunks' NDMA (NS - 2) loads are outstanding (all, near the end), the
-  // barrier makes that every wave's and frees stage (i - 1) % NS for chunk
-  // i + NS - 1
+  // NS - 1 image chunks in flight: chunk i lands in stage i % NS.  Issue
+  // order per iteration i: [matrix chunk i + 1 (BR)] [image chunk i + NS - 1];
+  // at the top of iteration i this wave's chunk-i loads (and the matrix's) are
+  // done once at most the younger image chunks' loads are outstanding (all,
+  // near the end); the barrier makes that every wave's and frees stage
+  // (i - 1) % NS for chunk i + NS - 1
   const int nk = (p.K + XK - 1) / XK;
+  BFrag bf0, bf1;
+  if constexpr (BR) load_b(bf0, 0);
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i)
     if (i < nk) dma(i, i * XK);
-  for (int i = 0; i < nk; ++i) {
+  auto step = [&](int i, const BFrag& cur, BFrag& nxt) {
     if (NS == 2 || i + NS - 2 >= nk)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (NS == 3)
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      wait_vm<0>();
+    else if (BR)
+      wait_vm<S::NDMA_A>();   // image chunk i + 1 (NS = 3) may be outstanding
     else
-      asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+      wait_vm<S::NDMA * (NS - 2)>();
     __syncthreads();
+    if constexpr (BR)
+      if (i + 1 < nk) load_b(nxt, (i + 1) * XK);
     if (i + NS - 1 < nk) dma((i + NS - 1) % NS, (i + NS - 1) * XK);
-    compute(i % NS, i * XK);
+    compute(i % NS, i * XK, cur);
+  };
+  for (int i = 0; i < nk; i += 2) {
+    step(i, bf0, bf1);
+    if (i + 1 < nk) step(i + 1, bf1, bf0);
   }
   __syncthreads();   // the ring is reused below
   uint32_t mx = 0;
@@ -687,7 +751,8 @@ __global__ __launch_bounds__(256, 4 / NS) void k_gemm_h2r(const GemmProblem* __r
 void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma) {
   if (n_tiles <= 0) return;
   if (share == 1 && dma && DCTAE_GEMM_DMA)
-    hipLaunchKernelGGL(k_gemm_h2r<DCTAE_GEMM_DMA_NS>, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+    hipLaunchKernelGGL((k_gemm_h2r<DCTAE_GEMM_DMA_NS, DCTAE_GEMM_DMA_BR != 0>), dim3(n_tiles), dim3(256), 0, s, probs,
+                       tiles);
   else if (share == 1)
     hipLaunchKernelGGL((k_gemm_h2<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
   else
