@@ -138,6 +138,9 @@ struct dctae_ctx {
   // the encode's row GEMM (with gemm_h2): 1 = k_gemm_h2r (operands streamed to
   // LDS by buffer_load ... lds), 0 = k_gemm_h2<3, 1>
   int gemm_dma = 1;
+  // images with rows and columns on the GEMM DCT: 1 = colour transform, folds
+  // and row GEMM in one pass (k_rows_fused), 0 = k_rgb_to_ipt + the row GEMM
+  int rows_fused = 1;
   // images with both passes on the GEMM DCT: T / Y parity-planar (ImgDesc::tperm)
   int tperm = 1;
   // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
@@ -820,6 +823,8 @@ struct ChunkJob {
   int h2;             // the job's GEMMs on k_gemm_h2
   size_t epi_off;     // k_tile_epilogue_p blocks (local image, 3 h + c) of the images with Y in the workspace
   int n_epi;
+  size_t fused_t_off;  // k_rows_fused tiles (row problem, row-pair block)
+  int n_fused_tiles, any_fused;
 };
 
 struct EncPlan {
@@ -985,6 +990,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "gemm_x3") ctx->gemm_x3 = value != 0;
   else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
   else if (k == "gemm_dma") ctx->gemm_dma = value != 0;
+  else if (k == "rows_fused") ctx->rows_fused = value != 0;
   else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
   else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
   else if (k == "fft_generic") ctx->fft_generic = value != 0;
@@ -1189,7 +1195,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
     j.amax_off = wsf;
-    wsf += up(2ll * (j.i1 - j.i0));
+    wsf += up(3ll * (j.i1 - j.i0) + 1);   // |max| pairs, then k_rows_fused's per-image flags and "any" word
     E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
     E.max_T = std::max(E.max_T, j.max_T);
   }
@@ -1207,7 +1213,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
   for (auto& j : E.jobs) {
     j.desc_off = E.pb.add(D.data() + j.i0, j.i1 - j.i0);
     const size_t p0 = probs.size();
-    std::vector<TileRef> rt, ct;
+    std::vector<TileRef> rt, ct, ft;
     std::vector<int2> fr[kVariants];
     std::vector<int4> fc[kVariants];
     std::vector<int2> br[4];
@@ -1225,6 +1231,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       if (d.plan_w < 0) {
         // T[c][y][kx] = sum_x CW[kx][x] * IPT[c][y][x], folded: even kx over
         // IPT[x] + IPT[W-1-x], odd kx over IPT[x] - IPT[W-1-x] (half the flops)
+        const size_t q0 = probs.size();
         for (int par = 0; par < 2; ++par) {
           const int M = par ? d.Kw / 2 : (d.Kw + 1) / 2, K = par ? d.W / 2 : (d.W + 1) / 2;
           if (M == 0) continue;
@@ -1246,11 +1253,23 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
           uint32_t* am = reinterpret_cast<uint32_t*>(ws + j.amax_off) + 2 * li;
           g.amax = am;                               // k_rgb_to_ipt's |max| of the folded IPT
           g.omax = d.plan_h < 0 ? am + 1 : nullptr;  // T's |max| for the column GEMM
-          add_tiles(rt, (int)(probs.size() - p0), g);
+          g.pad2 = li;                               // k_rows_fused: the image and the parity
+          g.pad3 = par;
           probs.push_back(g);
         }
-        j.any_gemm_rows = 1;
-        {
+        // k_rows_fused (colour transform + folds + row GEMM in one pass) for the
+        // tperm images whose parity matrices are cached pre-split (both forms:
+        // the fix-up runs the bf16 one) and fit its 256 output columns
+        bool fz = ctx->rows_fused && d.tperm && probs.size() == q0 + 2;   // both parities, consecutive
+        for (size_t q = q0; q < probs.size(); ++q) fz = fz && probs[q].Xh && probs[q].N <= fused_max_n();
+        if (fz)
+          for (int rb = 0; rb * fused_pairs_per_block() < (d.H + 1) / 2; ++rb) ft.push_back(TileRef{(int)(q0 - p0), rb});
+        else
+          for (size_t q = q0; q < probs.size(); ++q) add_tiles(rt, (int)(q - p0), probs[q]);
+        if (fz) {
+          j.any_fused = 1;
+        } else {
+          j.any_gemm_rows = 1;
           // k_rgb_to_ipt's (x, y)-mirrored pixel groups of this image
           const int64_t ng = (int64_t)(d.plan_h < 0 ? (d.H + 1) / 2 : d.H) * ((d.W + 1) / 2);
           for (int64_t g0 = 0; g0 < ng; g0 += rgb_to_ipt_groups_per_block()) ipt.push_back(make_int2(li, (int)g0));
@@ -1331,8 +1350,11 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
     if (ctx->xcd_order) {
       xcd_deal_tiles(rt, probs.data() + p0, 1);
       xcd_deal_tiles(ct, probs.data() + p0, 2);
+      xcd_deal_tiles(ft, probs.data() + p0, 1);   // an image's blocks on one XCD: its two matrices in one L2
     }
     j.rows_t_off = E.pb.add(rt.data(), rt.size());
+    j.fused_t_off = E.pb.add(ft.data(), ft.size());
+    j.n_fused_tiles = (int)ft.size();
     j.cols_t_off = E.pb.add(ct.data(), ct.size());
     // XCD-aware order of the column blocks (speed only; any order is correct):
     // blocks b and b+8 are dealt to the same XCD, so give all the blocks of
@@ -1443,7 +1465,8 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
                          (int64_t)ctx->fft_enabled * 2 + (int64_t)ctx->fft_spec_enabled + 4 * ctx->bluestein +
                              64 * ctx->t_alias + 1024 * ctx->xcd_order + 2048 * ctx->gemm_x3 +
                              4096 * ctx->cols512b + 8192 * ctx->rows_kernel + 65536 * ctx->gemm_h2 +
-                             131072 * ctx->fft_odd + 262144 * ctx->fft_generic + 524288 * ctx->tperm,
+                             131072 * ctx->fft_odd + 262144 * ctx->fft_generic + 524288 * ctx->tperm +
+                             1048576 * ctx->rows_fused,
                          (int64_t)(intptr_t)ctx->ws});
   for (int i = 0; i < n; ++i) {
     key.push_back(imgs->img_off[i]);
@@ -1538,7 +1561,18 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     uint32_t* amax = reinterpret_cast<uint32_t*>(ctx->ws + j.amax_off);
-    if (j.h2) hipMemsetAsync(amax, 0, 8 * (size_t)(j.i1 - j.i0), st);   // errors surface at hipGetLastError
+    if (j.h2 || j.any_fused) hipMemsetAsync(amax, 0, 12 * (size_t)(j.i1 - j.i0) + 4, st);   // errors surface at hipGetLastError
+    if (j.any_fused) {
+      int* flags = reinterpret_cast<int*>(amax + 2 * (j.i1 - j.i0));
+      {
+        Timer t(ctx, st, "rows_fused");
+        launch_rows_fused((const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.fused_t_off), j.n_fused_tiles,
+                          dd, imgs->rgb_dev, ctx->cm, amax, flags, j.i1 - j.i0, st, false);
+      }
+      Timer t(ctx, st, "rows_fixup");
+      launch_rows_fused((const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + j.fused_t_off), j.n_fused_tiles, dd,
+                        imgs->rgb_dev, ctx->cm, amax, flags, j.i1 - j.i0, st, true);
+    }
     if (j.any_gemm_rows) {
       {
         Timer t(ctx, st, "rgb_to_ipt");

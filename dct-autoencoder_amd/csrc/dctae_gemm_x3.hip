@@ -516,6 +516,34 @@ struct H2rShape {
   static constexpr int NDMA = NDMA_A + (BR ? 0 : 4);        //   ... and matrix
 };
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS writes done, then
+// s_barrier.  __syncthreads() is a release fence as well, which on gfx9
+// (loads and stores share vmcnt) waits for EVERY outstanding vector memory
+// operation -- the prefetched loads in flight included -- so with it no load
+// or LDS-DMA chunk could stay in flight across a chunk's barriers.  Users wait
+// for their own LDS-DMA chunks (wait_vm) before it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// One 16-byte-per-lane buffer_load ... lds (lane i -> lds + 16 i), written
+// out so the compiler does not see an LDS DMA in flight: it otherwise waits
+// for every outstanding vector load (vmcnt(0)) before the next LDS read it
+// cannot prove disjoint, prefetched register loads included.  The caller
+// waits for the chunk (wait_vm) before its barrier.  rsrc: the raw buffer
+// descriptor words (base, num_records, 0x00020000).
+__device__ __forceinline__ void dma_lds16(u32x4 rsrc, const void* lds, int voff) {
+  const uint32_t m0 = (uint32_t)(uintptr_t)lds;
+  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m0) : "memory");
+}
+__device__ __forceinline__ u32x4 rsrc_words(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  u32x4 r;
+  r[0] = (uint32_t)a;
+  r[1] = (uint32_t)(a >> 32) & 0xffffu;   // stride 0
+  r[2] = bytes;
+  r[3] = 0x00020000u;
+  return r;
+}
+
 // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt in bits 3:0 and 15:14, expcnt and lgkmcnt left at their maxima)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -757,6 +785,327 @@ void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles,
     hipLaunchKernelGGL((k_gemm_h2<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
   else
     hipLaunchKernelGGL((k_gemm_h2<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+}
+
+// ---------------------------------------------------------------------------
+// k_rows_fused: colour transform, (x, y) folds and row GEMM of both parities
+// in one pass, for the images whose rows and columns both run on the GEMM DCT
+// (ImgDesc::tperm; reference util.py:70-82 then util.py:333).  The separate
+// path writes the folded IPT (k_rgb_to_ipt, 3.4 GB on config 4) and reads it
+// back in the row GEMM.  Here a block owns 16 row pairs (y, H-1-y) -- 32
+// folded rows: 16 sums, 16 differences -- and every output column of both
+// parities (N <= 256 each: Kw <= 512).  Per 32-deep k chunk each of its 512
+// threads loads the 4 pixels (y, k), (y, W-1-k), (H-1-y, k), (H-1-y, W-1-k),
+// computes their IPT and the folds of both parities in registers
+// (k_rgb_to_ipt's arithmetic, value for value: every pixel is transformed
+// once), and writes the fp16 pieces to LDS; waves 0-3 run the even-kx
+// columns against the even half DCT matrix, waves 4-7 the odd ones (64
+// columns of 32 rows and 3 channels each, 96 accumulator VGPRs).  The
+// matrices stream through a two-stage LDS ring (LDS DMA), the pixels two
+// chunks ahead in registers.
+// Scale: the image's |max| (k_gemm_h2's operand scale) is unknown before the
+// transform, so the first pass splits at a fixed 2^DCTAE_FUSED_SE and records
+// the |max| of the folded values; an image with a value outside the safe fp16
+// range (|v| 2^SE >= 2^15, or not finite) is flagged, and the fix-up launch
+// (fix = 1, flagged images only, grid-stride) redoes it at the scale k_gemm_h2
+// derives from that |max| -- the old path's arithmetic for those images.
+// ---------------------------------------------------------------------------
+#ifndef DCTAE_FUSED_SE
+#define DCTAE_FUSED_SE 11
+#endif
+constexpr int kFusedPairs = 16;    // row pairs per block
+constexpr int kFusedTN = 256;      // output columns per parity
+
+__global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __restrict__ probs,
+                                                      const TileRef* __restrict__ tiles, int n_tiles,
+                                                      const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
+                                                      ColorMats cm, uint32_t* __restrict__ amax, int* __restrict__ flags,
+                                                      int n_img, int fix) {
+  constexpr int TN = kFusedTN, NPR = kFusedPairs;
+  constexpr int B_PL = TN * XK * 2;          // 16 KB: one plane of one parity's matrix chunk
+  constexpr int B_ST = 4 * B_PL;             // 64 KB: 2 parities x 2 planes
+  constexpr int A_CQ = 2 * NPR * XK;         // halves per (parity, channel, piece): 32 rows x 32 k
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * B_ST + 12 * A_CQ * 2];
+  uint16_t* As = reinterpret_cast<uint16_t*>(lds + 2 * B_ST);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int pw = wave >> 2, wc = wave & 3;   // this wave's parity and 64-column slice
+  const float gam = 0.430000007152557373046875f;
+  if (fix && flags[n_img] == 0) return;      // fix-up: no image of the job flagged
+  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const TileRef tr = tiles[t];
+    if (tr.problem < 0) continue;   // padding of an XCD-dealt list
+    const GemmProblem pu = probs[tr.problem], pv = probs[tr.problem + 1];   // the even and odd parity problems
+    const int li = pu.pad2;
+    if (fix && flags[li] == 0) continue;
+    const ImgDesc d = imgs[li];
+    const int H = d.H, W = d.W, Hh = (H + 1) >> 1, Ku = pu.K, Kv = pv.K;
+    const int j0 = tr.tile * NPR;
+    // operand scale 2^se: fixed in the first pass, k_gemm_h2's rule on the recorded |max| in the fix-up
+    int se = DCTAE_FUSED_SE;
+    if (fix) {
+      const uint32_t mb = amax[2 * li];
+      se = 0;
+      if (mb != 0u && mb < 0x7f800000u) {
+        int e;
+        frexpf(__uint_as_float(mb), &e);
+        se = min(max(14 - e, -100), 100);
+      }
+    }
+    // the matrices: wave-instruction j: parity j / 4, plane (j / 2) % 2, rows
+    // 16 rg + lane / 4 with rg = wave + 8 (j % 2) (16 rows of 64 bytes per 1 KB),
+    // LDS slot lane % 4 = k quad (lane % 4) ^ swz(row), as k_gemm_h2r
+    const u32x4 brs[2] = {rsrc_words(pu.Xh, (uint32_t)(2 * pu.xs_plane * 2)),
+                          rsrc_words(pv.Xh, (uint32_t)(2 * pv.xs_plane * 2))};
+    int boff[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 16 * (wave + 8 * h) + (lane >> 2), kq = (lane & 3) ^ swz(row);
+      boff[0][h] = (row * pu.xs_ld + 8 * kq) * 2;
+      boff[1][h] = (row * pv.xs_ld + 8 * kq) * 2;
+    }
+    const int xsp2[2] = {(int)(pu.xs_plane * 2), (int)(pv.xs_plane * 2)};
+    const int nrow[2] = {(pu.N + 31) & ~31, (pv.N + 31) & ~31};   // matrix rows the MFMAs read
+    auto dma_b = [&](int st, int k0) {
+#if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 8)
+      return;   // profiling ablation: no matrix loads (wrong output)
+#endif
+      uint8_t* base = lds + st * B_ST;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int par = j >> 2, pl = (j >> 1) & 1, h = j & 1;
+        if (16 * (wave + 8 * h) < nrow[par])   // rows past the parity's N (rounded to the MFMA blocks) are never read
+          dma_lds16(brs[par], base + (2 * par + pl) * B_PL + (wave + 8 * h) * 1024,
+                    boff[par][h] + k0 * 2 + pl * xsp2[par]);
+      }
+    };
+    // the pixels: row pair pr = tid / 32 (y = j0 + pr, y2 = H-1-y), column k = k0 + tid % 32 and W-1-k
+    const int pr = tid >> 5, kk0 = tid & 31;
+    const int y = j0 + pr;
+    const bool vy = y < Hh;
+    const int yy = vy ? y : 0, y2 = H - 1 - yy;
+    const bool yp = y2 != yy;
+    const int hw = H * W;
+    const auto rrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(rgb + d.rgb_off), 0, 3 * hw * 4, 0x00020000);
+    typedef float Px[4][3];
+    Px pxa, pxb;
+    auto load_rgb = [&](Px& px, int k0) {
+#if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 4)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)   // profiling ablation: no pixel loads (wrong output)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) px[q][c] = 0.001f * (float)(k0 + q + c + kk0);
+      return;
+#endif
+      const int k = k0 + kk0, kk = k < Ku ? k : 0, x2 = W - 1 - kk;
+      const int o[4] = {yy * W + kk, yy * W + x2, y2 * W + kk, y2 * W + x2};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          px[q][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrsrc, (c * hw + o[q]) * 4, 0, 0));
+    };
+    bool bad = false;
+    uint32_t fmx = 0;   // |max| of the folded values (the fix-up's scale)
+    auto transform = [&](const Px& px, int k0) {
+#if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 1)
+      // profiling ablation: no colour transform / folds / split (wrong output)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int pq = 0; pq < 8; ++pq) {
+          const int row = pr + NPR * (pq & 1);
+          const int o = row * XK + 8 * (((kk0 >> 3)) ^ swz(row)) + (kk0 & 7);
+          As[((pq >> 2) * 3 + c) * 2 * A_CQ + ((pq >> 1) & 1) * A_CQ + o] =
+              (uint16_t)(__float_as_uint(px[pq & 3][c]) & 0x3bffu);
+        }
+      return;
+#endif
+      const int k = k0 + kk0;
+      const int kk = k < Ku ? k : 0;
+      const bool xp = W - 1 - kk != kk;
+      const bool oku = vy && k < Ku, okv = vy && k < Kv;
+      float pi[4][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // util.py:70-82 (k_rgb_to_ipt)
+        const float r = px[q][0], g = px[q][1], b = px[q][2];
+        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), gam);
+        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), gam);
+        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), gam);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) pi[q][c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
+      }
+      const int kq = (k & 31) >> 3, kw = k & 7;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {   // k_rgb_to_ipt's folds: row y (sum) and row H-1-y (difference)
+        const float pb = xp ? pi[1][c] : 0.0f, pd = xp ? pi[3][c] : 0.0f;
+        const float a = yp ? pi[0][c] + pi[2][c] : pi[0][c];
+        const float bb = yp ? pb + pd : pb;
+        const float c2 = pi[0][c] - pi[2][c], d2 = pb - pd;
+        const float v[2][2] = {{oku ? (xp ? a + bb : a) : 0.0f, oku && yp ? (xp ? c2 + d2 : c2) : 0.0f},
+                               {okv ? a - bb : 0.0f, okv && yp ? c2 - d2 : 0.0f}};
+#pragma unroll
+        for (int par = 0; par < 2; ++par)
+#pragma unroll
+          for (int rr = 0; rr < 2; ++rr) {
+            const float vv = v[par][rr];
+            fmx = max(fmx, __float_as_uint(vv) & 0x7fffffffu);
+            const float vsc = ldexpf(vv, se);
+            bad |= !(fabsf(vsc) < 32768.0f);
+            const _Float16 h0 = (_Float16)vsc;
+            const _Float16 h1 = (_Float16)(vsc - (float)h0);
+            const int row = pr + NPR * rr;
+            const int o = row * XK + 8 * (kq ^ swz(row)) + kw;
+            As[((par * 3 + c) * 2 + 0) * A_CQ + o] = __builtin_bit_cast(uint16_t, h0);
+            As[((par * 3 + c) * 2 + 1) * A_CQ + o] = __builtin_bit_cast(uint16_t, h1);
+          }
+      }
+    };
+    floatx16 acc[3][2];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][x][r] = 0.0f;
+    const int nw = pw ? pv.N : pu.N;   // this wave's parity's output columns
+    auto mfma_chunk = [&](int st) {
+#if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 2)
+      return;   // profiling ablation: no MFMAs (wrong output)
+#endif
+      const uint16_t* Bp = reinterpret_cast<const uint16_t*>(lds + st * B_ST + 2 * pw * B_PL);
+#pragma unroll
+      for (int ks = 0; ks < XK / 16; ++ks) {
+        const int kq = 2 * ks + half;
+        bf16x8 b[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+          const int rb = wc * 64 + 32 * x + l32;
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl)
+            b[x][pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + lds_off(rb, kq));
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          bf16x8 a[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            a[q] = *reinterpret_cast<const bf16x8*>(As + ((pw * 3 + c) * 2 + q) * A_CQ + lds_off(l32, kq));
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+            if (wc * 64 + 32 * x < nw) mfma_pieces(acc[c][x], a, b[x]);   // (wave-uniform) columns past N: none
+        }
+      }
+    };
+    // Pixels two chunks ahead (pxa: even chunks, pxb: odd), the matrices one;
+    // issue order per step i: [matrices i + 1] [pixels i + 2], so at its top at
+    // most pixels i + 1's 12 loads may be outstanding.  Every step issues the
+    // same loads (past the last chunk: clamped pixels, matrix offsets reading
+    // zeros), and the loop body is unconditional, so the compiler's own waits
+    // on the pixel registers count exactly.
+    const int nk = (Ku + XK - 1) / XK;
+    load_rgb(pxa, 0);
+    dma_b(0, 0);
+    load_rgb(pxb, XK);
+    auto step = [&](int i, Px& cur) {
+      wait_vm<12>();      // this wave's pixels and matrix chunk i
+      lds_barrier();      // every wave's; chunk i - 1's MFMAs done (the pieces and stage (i + 1) % 2 free)
+      dma_b((i + 1) & 1, (i + 1) * XK);
+      transform(cur, i * XK);
+      load_rgb(cur, (i + 2) * XK);
+      lds_barrier();      // the pieces of chunk i
+      mfma_chunk(i & 1);
+    };
+    int i = 0;
+    for (; i + 1 < nk; i += 2) {
+      step(i, pxa);
+      step(i + 1, pxb);
+    }
+    if (i < nk) step(i, pxa);
+    wait_vm<0>();   // no LDS DMA may outlive the loop (the LDS is reused, and released at exit)
+    const GemmProblem& p = pw ? pv : pu;
+    const int N = p.N;
+    const float unscale = ldexpf(1.0f, -(se + p.xh_exp));
+    // C/D map: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5):
+    // rows < 16 are the sums (T row j0 + row), the rest the differences (T row
+    // H - 1 - (j0 + row - 16)); the middle row of an odd H has no difference
+    uint32_t mx = 0;
+    int trow[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rr = (r & 3) + 8 * (r >> 2) + 4 * half;
+      const int j = j0 + (rr & (NPR - 1));
+      const int ty = rr < NPR ? j : H - 1 - j;
+      trow[r] = (j < Hh && (rr < NPR || ty != j)) ? ty : -1;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const bool vn = wc * 64 + 32 * x + l32 < N;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          acc[c][x][r] *= unscale;
+          if (vn && trow[r] >= 0) mx = max(mx, __float_as_uint(acc[c][x][r]) & 0x7fffffffu);
+        }
+      }
+    // block reductions: flag, |max| of the folded values, |max| of T
+    uint32_t* part = reinterpret_cast<uint32_t*>(lds);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+      fmx = max(fmx, (uint32_t)__shfl_xor((int)fmx, o));
+    }
+    const int any_bad = __syncthreads_or(bad ? 1 : 0);   // also: every wave past its last LDS read
+    if (lane == 0) {
+      part[wave] = mx;
+      part[8 + wave] = fmx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t m = 0, f = 0;
+      for (int w = 0; w < 8; ++w) {
+        m = max(m, part[w]);
+        f = max(f, part[8 + w]);
+      }
+      if (!fix) {
+        if (f) atomicMax(amax + 2 * li, f);
+        if (any_bad) {
+          flags[li] = 1;
+          flags[n_img] = 1;   // the job's "any" word, read first by the fix-up
+        }
+      }
+      // T's |max| for the column GEMM; a flagged block leaves it to the fix-up
+      if (pu.omax && (fix || !any_bad)) atomicMax(pu.omax, m);
+    }
+    const int64_t ext = (int64_t)(p.M - 1) * p.sOm + (int64_t)(N - 1) * p.sOn + 1;
+    const int sOm4 = (int)(p.sOm * 4);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.O + (int64_t)c * p.sOc, 0, (int)(ext * 4), 0x00020000);
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int n = wc * 64 + 32 * x + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int vo = (n < N && trow[r] >= 0) ? trow[r] * sOm4 + n * 4 : kOob;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c][x][r]), rsrc, vo, 0, 0);
+        }
+      }
+    }
+    __syncthreads();   // the partials / LDS reused by the next tile
+  }
+}
+
+int fused_pairs_per_block() { return kFusedPairs; }
+int fused_max_n() { return kFusedTN; }
+
+void launch_rows_fused(const GemmProblem* probs, const TileRef* tiles, int n_tiles, const ImgDesc* imgs,
+                       const float* rgb, const ColorMats& cm, uint32_t* amax, int* flags, int n_img, hipStream_t s,
+                       bool fixup) {
+  if (n_tiles <= 0) return;
+  // the fix-up: a short grid-stride launch (every block exits at once when no image is flagged)
+  hipLaunchKernelGGL(k_rows_fused, dim3(fixup ? std::min(n_tiles, 256) : n_tiles), dim3(512), 0, s, probs, tiles,
+                     n_tiles, imgs, rgb, cm, amax, flags, n_img, fixup ? 1 : 0);
 }
 
 void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {

@@ -29,6 +29,14 @@ void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int 
 // three bf16 planes [3][Rp][Kp] of a row-major fp32 matrix (GemmProblem::Xs)
 void split_matrix_x3(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp);
 // the encode's DCT GEMMs on fp16 MFMAs, two-piece scaled operands (k_gemm_h2; 3 channels, share 1 or 2)
+// colour transform + folds + row GEMM of the tperm images (k_rows_fused), or
+// the fix-up of the images it flagged; tiles = (even-parity row problem, block
+// of row pairs), the odd parity's problem next to it
+int fused_pairs_per_block();
+int fused_max_n();
+void launch_rows_fused(const GemmProblem* probs, const TileRef* tiles, int n_tiles, const ImgDesc* imgs,
+                       const float* rgb, const ColorMats& cm, uint32_t* amax, int* flags, int n_img, hipStream_t s,
+                       bool fixup);
 // share 1 (the encode's row GEMM: A k-contiguous, sAm > 0): dma = k_gemm_h2r
 void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma);
 void split_matrix_h2(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp, int* e_out);

@@ -1022,14 +1022,47 @@ def test_gemm_dma_bit_identical(fe, pn, lfq):
     xs = [torch.from_numpy(a).to(DEV) for a in
           rng.synth_images(62, [(333, 517), (512, 512), (29, 700), (448, 449), (130, 128), (1000, 67)])]
     outs = []
-    for dm in (0, 1):
-        ops.set_option("gemm_dma", dm)
-        try:
-            ((dp, codes),) = fe.encode_batch(xs, pn, lfq, return_raw=True, return_scores=True)
-        finally:
-            ops.set_option("gemm_dma", 1)
-        outs.append((dp, codes))
+    ops.set_option("rows_fused", 0)   # the separate colour pass + row GEMM
+    try:
+        for dm in (0, 1):
+            ops.set_option("gemm_dma", dm)
+            try:
+                ((dp, codes),) = fe.encode_batch(xs, pn, lfq, return_raw=True, return_scores=True)
+            finally:
+                ops.set_option("gemm_dma", 1)
+            outs.append((dp, codes))
+    finally:
+        ops.set_option("rows_fused", 1)
     (d0, c0), (d1, c1) = outs
     assert torch.equal(c0, c1)
     assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
     assert torch.equal(d0._data["scores"], d1._data["scores"])
+
+
+def test_rows_fused_fixup_matches_separate_path(fe, pn, lfq):
+    """k_rows_fused splits at a fixed scale and flags an image whose folded IPT
+    leaves the safe fp16 range (large or non-finite pixels); the fix-up launch
+    redoes it at k_gemm_h2's per-image scale, which is the separate path's
+    (k_rgb_to_ipt + k_gemm_h2r) arithmetic: codes, raw tokens and scores equal
+    option rows_fused=0's bit for bit (GEMM-DCT sides only, so every image takes
+    the fused path; odd / even sides, a side < 32)."""
+    ops = _ops()
+    shapes = [(333, 517), (130, 128), (29, 700), (448, 449)]
+    xs = [torch.from_numpy(a).to(DEV) for a in rng.synth_images(63, shapes)]
+    xs[0] = xs[0] * 3000.0          # |folded IPT| * 2^11 far above 2^15
+    xs[1] = xs[1] * 500.0
+    xs[2] = xs[2] * 1.0e6
+    xs[3] = xs[3].clone()
+    xs[3][1, 17, 301] = float("inf")   # a non-finite pixel
+    outs = []
+    for fz in (0, 1):
+        ops.set_option("rows_fused", fz)
+        try:
+            ((dp, codes),) = fe.encode_batch(xs, pn, lfq, return_raw=True, return_scores=True)
+        finally:
+            ops.set_option("rows_fused", 1)
+        outs.append((dp, codes))
+    (d0, c0), (d1, c1) = outs
+    assert torch.equal(c0, c1)
+    assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
+    assert torch.equal(d0._data["scores"].view(torch.int32), d1._data["scores"].view(torch.int32))
