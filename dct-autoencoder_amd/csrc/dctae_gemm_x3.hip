@@ -1088,6 +1088,9 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int vo = (n < N && trow[r] >= 0) ? trow[r] * sOm4 + n * 4 : kOob;
+#if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 16)
+          if (acc[c][x][r] == 1.2345f)   // profiling ablation: (almost) no T stores (wrong output)
+#endif
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c][x][r]), rsrc, vo, 0, 0);
         }
       }

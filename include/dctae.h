@@ -401,7 +401,13 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * "tperm" (1, default: images with both passes on the GEMM DCT keep their
  * row-pass output T and spectrum Y parity-planar, so each parity problem of
  * the row GEMM stores whole lines; 0: interleaved columns; outputs
- * bit-identical), "gemm_dma" (1, default: the encode's row GEMM on
+ * bit-identical), "rows_fused" (1, default: images whose rows and columns
+ * both run on the GEMM DCT take the colour transform, both folds and both
+ * parities' row GEMM in one pass, k_rows_fused, its fp16 pieces at a fixed
+ * scale; an image whose folded IPT leaves that scale's range, or is not
+ * finite, is redone at the per-image scale -- bit-identical to 0 then, and for
+ * [0, 1] RGB, where the two scales coincide; 0: k_rgb_to_ipt + the row GEMM),
+ * "gemm_dma" (1, default: the encode's row GEMM on
  * k_gemm_h2r, both operands streamed into a two-stage LDS ring by
  * buffer_load ... lds; 0: k_gemm_h2's register staging; outputs
  * bit-identical).  Profiling builds only (make PROFILING=1; the shipped
