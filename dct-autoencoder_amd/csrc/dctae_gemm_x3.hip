@@ -813,6 +813,13 @@ void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles,
 #ifndef DCTAE_FUSED_SE
 #define DCTAE_FUSED_SE 11
 #endif
+// the matrices' MFMA fragments: 0 = a two-stage LDS ring by LDS DMA; 1 =
+// loaded by each wave straight into registers during the previous chunk's
+// MFMAs (its own 64 columns: no LDS copy, plain loads instead of LDS DMA;
+// config 4 rows_fused 3.09 -> 3.59 ms, same box)
+#ifndef DCTAE_FUSED_BREG
+#define DCTAE_FUSED_BREG 0
+#endif
 constexpr int kFusedPairs = 16;    // row pairs per block
 constexpr int kFusedTN = 256;      // output columns per parity
 
@@ -823,11 +830,15 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
                                                       int n_img, int fix) {
   constexpr int TN = kFusedTN, NPR = kFusedPairs;
   constexpr int B_PL = TN * XK * 2;          // 16 KB: one plane of one parity's matrix chunk
-  constexpr int B_ST = 4 * B_PL;             // 64 KB: 2 parities x 2 planes
+  constexpr int B_ST = DCTAE_FUSED_BREG ? 0 : 4 * B_PL;   // 64 KB: 2 parities x 2 planes (LDS-DMA form)
   constexpr int A_CQ = 2 * NPR * XK;         // halves per (parity, channel, piece): 32 rows x 32 k
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * B_ST + 12 * A_CQ * 2];
   uint16_t* As = reinterpret_cast<uint16_t*>(lds + 2 * B_ST);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, l32 = lane & 31;
+  // the wave index as a uniform value: the parity's matrix descriptor and the
+  // column-range tests stay scalar (from tid they were per-lane: a waterfall
+  // loop around every matrix load and a divergent branch around every MFMA)
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pw = wave >> 2, wc = wave & 3;   // this wave's parity and 64-column slice
   const float gam = 0.430000007152557373046875f;
   if (fix && flags[n_img] == 0) return;      // fix-up: no image of the job flagged
@@ -968,7 +979,22 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[c][x][r] = 0.0f;
     const int nw = pw ? pv.N : pu.N;   // this wave's parity's output columns
-    auto mfma_chunk = [&](int st) {
+    // DCTAE_FUSED_BREG: this lane's fragments of the next chunk, [ks][x][plane]:
+    // matrix row wc 64 + 32 x + l32, k = 16 ks + 8 half (16 bytes)
+    const auto brw = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(pw ? pv.Xh : pu.Xh), 0,
+                                                      (int)(2 * (pw ? pv.xs_plane : pu.xs_plane) * 2), 0x00020000);
+    const int bro = ((wc * 64 + l32) * (pw ? pv.xs_ld : pu.xs_ld) + 8 * half) * 2;
+    const int brx = 32 * (pw ? pv.xs_ld : pu.xs_ld) * 2, brp = (int)(2 * (pw ? pv.xs_plane : pu.xs_plane));
+    bf16x8 bq[XK / 16][2][2];
+    auto load_bq = [&](int ks, int k0) {
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+          bq[ks][x][pl] = __builtin_bit_cast(
+              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brw, bro + x * brx + pl * brp + (k0 + 16 * ks) * 2, 0, 0));
+    };
+    auto mfma_chunk = [&](int st, int k0n) {
 #if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 2)
       return;   // profiling ablation: no MFMAs (wrong output)
 #endif
@@ -982,7 +1008,8 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
           const int rb = wc * 64 + 32 * x + l32;
 #pragma unroll
           for (int pl = 0; pl < 2; ++pl)
-            b[x][pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + lds_off(rb, kq));
+            b[x][pl] = DCTAE_FUSED_BREG ? bq[ks][x][pl]
+                                        : *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + lds_off(rb, kq));
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -994,6 +1021,7 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
           for (int x = 0; x < 2; ++x)
             if (wc * 64 + 32 * x < nw) mfma_pieces(acc[c][x], a, b[x]);   // (wave-uniform) columns past N: none
         }
+        if (DCTAE_FUSED_BREG) load_bq(ks, k0n);   // this k step's fragments consumed: the next chunk's in flight
       }
     };
     // Pixels two chunks ahead (pxa: even chunks, pxb: odd), the matrices one;
@@ -1003,18 +1031,25 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
     // zeros), and the loop body is unconditional, so the compiler's own waits
     // on the pixel registers count exactly.
     const int nk = (Ku + XK - 1) / XK;
-    load_rgb(pxa, 0);
-    dma_b(0, 0);
-    load_rgb(pxb, XK);
     auto step = [&](int i, Px& cur) {
       wait_vm<12>();      // this wave's pixels and matrix chunk i
       lds_barrier();      // every wave's; chunk i - 1's MFMAs done (the pieces and stage (i + 1) % 2 free)
-      dma_b((i + 1) & 1, (i + 1) * XK);
+      if (!DCTAE_FUSED_BREG) dma_b((i + 1) & 1, (i + 1) * XK);
       transform(cur, i * XK);
-      load_rgb(cur, (i + 2) * XK);
+      if (!DCTAE_FUSED_BREG) load_rgb(cur, (i + 2) * XK);
       lds_barrier();      // the pieces of chunk i
-      mfma_chunk(i & 1);
+      mfma_chunk(i & 1, (i + 1) * XK);
+      // BREG issue order per step: [matrix i + 1] [pixels i + 2] (after the MFMAs)
+      if (DCTAE_FUSED_BREG) load_rgb(cur, (i + 2) * XK);
     };
+    load_rgb(pxa, 0);
+    if (DCTAE_FUSED_BREG) {
+      load_bq(0, 0);
+      load_bq(1, 0);
+    } else {
+      dma_b(0, 0);
+    }
+    load_rgb(pxb, XK);
     int i = 0;
     for (; i + 1 < nk; i += 2) {
       step(i, pxa);
