@@ -141,6 +141,8 @@ struct dctae_ctx {
   // images with rows and columns on the GEMM DCT: 1 = colour transform, folds
   // and row GEMM in one pass (k_rows_fused), 0 = k_rgb_to_ipt + the row GEMM
   int rows_fused = 1;
+  // the encode's column GEMM (with gemm_h2): 1 = k_gemm_h2c (LDS DMA), 0 = k_gemm_h2<3, 2>
+  int cols_dma = 1;
   // images with both passes on the GEMM DCT: T / Y parity-planar (ImgDesc::tperm)
   int tperm = 1;
   // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
@@ -991,6 +993,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "gemm_h2") ctx->gemm_h2 = value != 0;
   else if (k == "gemm_dma") ctx->gemm_dma = value != 0;
   else if (k == "rows_fused") ctx->rows_fused = value != 0;
+  else if (k == "cols_dma") ctx->cols_dma = value != 0;
   else if (k == "lfq_ws") ctx->lfq_ws = value != 0;
   else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
   else if (k == "fft_generic") ctx->fft_generic = value != 0;
@@ -1554,7 +1557,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   auto gemm = [&](const ChunkJob& j, size_t tiles_off, int n_tiles, hipStream_t st, int share) {
     if (j.h2)
       launch_gemm_h2((const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share,
-                     ctx->gemm_dma != 0);
+                     ctx->gemm_dma != 0, ctx->cols_dma != 0);
     else
       ctx_gemm(ctx, 3, (const GemmProblem*)(pd + j.gp_off), (const TileRef*)(pd + tiles_off), n_tiles, st, share);
   };

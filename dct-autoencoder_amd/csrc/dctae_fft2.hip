@@ -55,7 +55,7 @@ __device__ __forceinline__ void rows2_item(const ImgDesc& d, int y_first, const 
   static_assert(3 * B1 <= 64 && 3 * B2 <= 64, "one butterfly per lane per pass");
   static_assert(R1 == 16, "first radix 16 (Ns of pass 2 = 16)");
   const int tid = opaque_tid();
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   float2(*z)[MP] = L.z[wave];
   float* zf0 = reinterpret_cast<float*>(z[0]);
   float* zf1 = reinterpret_cast<float*>(z[1]);
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void k_rows224p(const ImgDesc* __restrict__ im
   const int2 jb = blocks[blockIdx.x];
   const ImgDesc d = imgs[jb.x];
   const int tid = opaque_tid();
-  const int wave = tid >> 6, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int H = d.H, Kw = d.Kw;
   const int y0 = jb.y + RW * wave;
   const bool live = y0 < H;   // wave-uniform; dead waves still reach the barrier

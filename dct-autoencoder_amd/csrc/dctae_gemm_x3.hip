@@ -251,7 +251,7 @@ __device__ __forceinline__ void gemm_x3_body(const GemmProblem& p, int tm, int t
   constexpr bool preA = PRE && SH == 2, preB = PRE && SH == 1;
   constexpr int SAM = preA ? 0 : BM, SBN = preB ? 0 : BN;   // fp32 sources per channel
   const int m0 = tm * TM, n0 = tn * TN;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int half = lane >> 5, l32 = lane & 31;
 
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(256, (H2rShape<NS, BR>::BPC)) void k_gemm_h2r(const
   const GemmProblem p = probs[tr.problem];
   const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
   const int m0 = tm * TM, n0 = tn * TN;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1, half = lane >> 5, l32 = lane & 31;
   // the per-channel operand scaled by 2^ea (|max| < 2^14), the output unscaled (gemm_x3_body)
   // (v_ldexp_f32 on the fragments: exact as the multiply, and beside MFMAs a
@@ -776,13 +776,190 @@ __global__ __launch_bounds__(256, (H2rShape<NS, BR>::BPC)) void k_gemm_h2r(const
   }
 }
 
-void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma) {
+// k_gemm_h2c: k_gemm_h2<3, 2> (the encode's column GEMM: A = the pre-split
+// half DCT matrix of H, shared; B = T per channel, n = kx contiguous, k = y
+// strided by +-Kw) with both operands streamed by LDS DMA into a two-stage
+// ring: the matrix as k_gemm_h2r's (128 rows x 32 k x 2 planes), T as 32
+// k-rows x 64 columns of fp32 per channel, four rows per 1 KB wave-instruction
+// (24 KB a stage, 40 KB with the matrix: two blocks per CU).  The MFMA
+// fragment of T (8 consecutive k of one column) is 8 ds_read_b32 down a
+// column; the 16-byte column groups of rows with (k >> 3) odd are swapped by
+// 8 slots, so the two half-waves (k groups 8 apart) read disjoint banks.  The
+// fragment is split in registers as k_gemm_h2r's; products and their order
+// are k_gemm_h2's (bit-identical, option cols_dma).
+__global__ __launch_bounds__(256, 2) void k_gemm_h2c(const GemmProblem* __restrict__ probs,
+                                                    const TileRef* __restrict__ tiles) {
+  constexpr int NC = 3, TM = 128, TN = 64;
+  constexpr int A_PL = TM * XK * 2;          // 8 KB per matrix plane
+  constexpr int A_BYTES = 2 * A_PL;          // 16 KB
+  constexpr int B_CH = XK * TN * 4;          // 8 KB per channel: 32 rows of 256 bytes
+  constexpr int STAGE = A_BYTES + NC * B_CH;   // 40 KB
+  __shared__ __attribute__((aligned(16))) uint8_t ring[2 * STAGE];
+  const TileRef tr = tiles[blockIdx.x];
+  if (tr.problem < 0) return;   // padding of an XCD-dealt list
+  const GemmProblem p = probs[tr.problem];
+  const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  int ea = 0;   // T scaled by 2^ea (|max| < 2^14), the output unscaled (gemm_x3_body)
+  {
+    const uint32_t mb = *p.amax;
+    if (mb != 0u && mb < 0x7f800000u) {
+      int e;
+      frexpf(__uint_as_float(mb), &e);
+      ea = min(max(14 - e, -100), 100);
+    }
+  }
+  const float unscale = ldexpf(1.0f, -(ea + p.xh_exp));
+  // the matrix: plane j / 2, rows 16 rg + lane / 4 with rg = wave + 4 (j & 1), slot lane % 4 = k quad ^ swz(row)
+  const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(p.Xh), 0, (int)(2 * p.xs_plane * 2),
+                                                      0x00020000);
+  int aoff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 16 * (wave + 4 * h) + (lane >> 2), kq = (lane & 3) ^ swz(row);
+    aoff[h] = ((m0 + row) * p.xs_ld + 8 * kq) * 2;
+  }
+  const int xsp2 = (int)(p.xs_plane * 2);
+  // T: channel c's element range [lo, hi] (sBn = 1, sBk = +-Kw) plus 64 floats,
+  // so a 16-byte piece straddling its end is read whole (it stays inside the
+  // workspace's padded regions); wave-instruction j: channel j / 2, rows
+  // 4 g + lane / 16 with g = wave + 4 (j & 1), LDS slot lane % 16 = column
+  // group (lane % 16) ^ (8 ((row >> 3) & 1)); k past K is zeroed at the split
+  const int64_t lo = p.sBk < 0 ? (int64_t)(p.K - 1) * p.sBk : 0;
+  const int64_t hi = (int64_t)(p.N - 1) + (p.sBk > 0 ? (int64_t)(p.K - 1) * p.sBk : 0);
+  __amdgpu_buffer_rsrc_t brsrc[3];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    brsrc[c] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.B + (int64_t)c * p.sBc + lo), 0,
+                                                 (int)((hi - lo + 1 + 64) * 4), 0x00020000);
+  int boff[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 4 * (wave + 4 * h) + (lane >> 4), q = (lane & 15) ^ (8 * ((row >> 3) & 1));
+    boff[h] = (int)(((int64_t)row * p.sBk + n0 + 4 * q - lo) * 4);
+  }
+  const int bstep = (int)(p.sBk * 4);   // bytes per k row (negative for the odd parity's descending rows)
+  auto dma = [&](int st, int k0) {
+    uint8_t* base = ring + st * STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pl = j >> 1, h = j & 1;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_void_t*)(base + pl * A_PL + (wave + 4 * h) * 1024), 16,
+                                               aoff[h] + k0 * 2 + pl * xsp2, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * NC; ++j) {
+      const int c = j >> 1, h = j & 1;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc[c], (lds_void_t*)(base + A_BYTES + c * B_CH + (wave + 4 * h) * 1024),
+                                               16, boff[h] + k0 * bstep, 0, 0, 0);
+    }
+  };
+  floatx16 acc[NC][2];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[c][x][r] = 0.0f;
+  const int nb = wn * 32 + l32;   // this lane's T column in the tile
+  const int bcol = 4 * ((nb >> 2) ^ (8 * half)) + (nb & 3);   // its float within a 64-float row (rows 8 half + e)
+  auto compute = [&](int st, int k0) {
+    const uint8_t* base = ring + st * STAGE;
+    const uint16_t* Ap = reinterpret_cast<const uint16_t*>(base);
+    const float* Bf = reinterpret_cast<const float*>(base + A_BYTES);
+#pragma unroll
+    for (int ks = 0; ks < XK / 16; ++ks) {
+      const int kq = 2 * ks + half;
+      bf16x8 a[2][2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int ra = wm * 64 + 32 * x + l32;
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) a[x][pl] = *reinterpret_cast<const bf16x8*>(Ap + pl * (A_PL / 2) + lds_off(ra, kq));
+      }
+      const int kb = k0 + 8 * kq;   // this lane's first k
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const float* bc = Bf + c * (B_CH / 4) + (8 * kq) * TN + bcol;
+        f32x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = bc[e * TN];
+        if (k0 + XK > p.K) {   // the last chunk (uniform): k past K -> 0
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = kb + e < p.K ? v[e] : 0.0f;
+        }
+        f32x8 vs;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vs[e] = ldexpf(v[e], ea);
+        const hv8 h0 = __builtin_convertvector(vs, hv8);
+        const u32x4 hw = __builtin_bit_cast(u32x4, h0);
+        f32x8 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r[2 * e]) : "v"(hw[e]), "v"(vs[2 * e]));
+          asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r[2 * e + 1]) : "v"(hw[e]), "v"(vs[2 * e + 1]));
+        }
+        const hv8 h1 = __builtin_convertvector(r, hv8);
+        const bf16x8 b[2] = {__builtin_bit_cast(bf16x8, h0), __builtin_bit_cast(bf16x8, h1)};
+#pragma unroll
+        for (int x = 0; x < 2; ++x) mfma_pieces(acc[c][x], a[x], b);
+      }
+    }
+  };
+  const int nk = (p.K + XK - 1) / XK;
+  dma(0, 0);
+  for (int i = 0; i < nk; ++i) {
+    wait_vm<0>();
+    __syncthreads();
+    if (i + 1 < nk) dma((i + 1) & 1, (i + 1) * XK);
+    compute(i & 1, i * XK);
+  }
+  // C/D map: column = lane & 31 (n), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (m);
+  // row-major outputs through buffer stores on the channel's range (gemm_x3_body)
+  const int64_t ext = (int64_t)(p.M - 1) * p.sOm + (int64_t)(p.N - 1) * p.sOn + 1;
+  if (p.sOm > 0 && p.sOn > 0 && p.sOm >= (int64_t)(p.N - 1) * p.sOn + 1 && (ext + 160 * p.sOm) * 4 < kOob) {
+    const int sOm4 = (int)(p.sOm * 4);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(p.O + (int64_t)c * p.sOc, 0, (int)(ext * 4), 0x00020000);
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const int gm = m0 + wm * 64 + 32 * x + 4 * half, gn = n0 + nb;
+        const int vo = gn < p.N ? gm * sOm4 + (int)(gn * p.sOn * 4) : kOob;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[c][x][r] * unscale), rsrc,
+                                                vo + ((r & 3) + 8 * (r >> 2)) * sOm4, 0, 0);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float* O = p.O + (int64_t)c * p.sOc;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int gm = m0 + wm * 64 + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * half, gn = n0 + nb;
+        if (gm < p.M && gn < p.N) O[(int64_t)gm * p.sOm + (int64_t)gn * p.sOn] = acc[c][x][r] * unscale;
+      }
+  }
+}
+
+void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma,
+                    bool dma_cols) {
   if (n_tiles <= 0) return;
   if (share == 1 && dma && DCTAE_GEMM_DMA)
     hipLaunchKernelGGL((k_gemm_h2r<DCTAE_GEMM_DMA_NS, DCTAE_GEMM_DMA_BR != 0>), dim3(n_tiles), dim3(256), 0, s, probs,
                        tiles);
   else if (share == 1)
     hipLaunchKernelGGL((k_gemm_h2<3, 1>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
+  else if (dma_cols)
+    hipLaunchKernelGGL(k_gemm_h2c, dim3(n_tiles), dim3(256), 0, s, probs, tiles);
   else
     hipLaunchKernelGGL((k_gemm_h2<3, 2>), dim3(n_tiles), dim3(256), 0, s, probs, tiles);
 }

@@ -360,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_f32(const GemmProblem* __restri
   const GemmProblem p = probs[tr.problem];
   const int tm = tr.tile / p.tiles_n, tn = tr.tile % p.tiles_n;
   const int m0 = tm * GT, n0 = tn * GT;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int half = lane >> 5, l32 = lane & 31;
   const bool a_shared = SH == 2 ? true : SH == 1 ? false : (p.sAc == 0);

@@ -38,7 +38,9 @@ void launch_rows_fused(const GemmProblem* probs, const TileRef* tiles, int n_til
                        const float* rgb, const ColorMats& cm, uint32_t* amax, int* flags, int n_img, hipStream_t s,
                        bool fixup);
 // share 1 (the encode's row GEMM: A k-contiguous, sAm > 0): dma = k_gemm_h2r
-void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma);
+// share 2 (the encode's column GEMM: B = T, sBn = 1): dma_cols = k_gemm_h2c
+void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share, bool dma,
+                    bool dma_cols);
 void split_matrix_h2(const float* m, int R, int K, std::vector<uint16_t>& out, int* Rp, int* Kp, int* e_out);
 void launch_tile_epilogue(const ImgDesc* imgs, int n_img, int max_T, const float* ws, const EncParams& ep,
                           const TokenSinks& sk, hipStream_t s, const int2* list = nullptr, int n_list = 0);

@@ -1066,3 +1066,27 @@ def test_rows_fused_fixup_matches_separate_path(fe, pn, lfq):
     assert torch.equal(c0, c1)
     assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
     assert torch.equal(d0._data["scores"].view(torch.int32), d1._data["scores"].view(torch.int32))
+
+
+def test_cols_dma_bit_identical(fe, pn, lfq):
+    """Option cols_dma (the column GEMM k_gemm_h2c streaming the matrix and T by
+    LDS DMA, T's MFMA fragments read down LDS columns, against the
+    register-staged k_gemm_h2<3, 2>): the same fp16 pieces in the same MFMA
+    order, so codes, raw tokens and scores are bit-identical (both parities'
+    row directions, k past K, columns past N, a side < 32, an FFT-row image
+    whose T is folded by k_fold_t)."""
+    ops = _ops()
+    xs = [torch.from_numpy(a).to(DEV) for a in
+          rng.synth_images(64, [(333, 517), (29, 700), (448, 449), (130, 128), (1000, 67), (300, 512)])]
+    outs = []
+    for cd in (0, 1):
+        ops.set_option("cols_dma", cd)
+        try:
+            ((dp, codes),) = fe.encode_batch(xs, pn, lfq, return_raw=True, return_scores=True)
+        finally:
+            ops.set_option("cols_dma", 1)
+        outs.append((dp, codes))
+    (d0, c0), (d1, c1) = outs
+    assert torch.equal(c0, c1)
+    assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
+    assert torch.equal(d0._data["scores"], d1._data["scores"])
