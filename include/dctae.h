@@ -407,6 +407,9 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * scale; an image whose folded IPT leaves that scale's range, or is not
  * finite, is redone at the per-image scale -- bit-identical to 0 then, and for
  * [0, 1] RGB, where the two scales coincide; 0: k_rgb_to_ipt + the row GEMM),
+ * "cols_dma" (1, default: the encode's column GEMM on k_gemm_h2c, the matrix
+ * and T streamed into a two-stage LDS ring by buffer_load ... lds; 0:
+ * k_gemm_h2's register staging; outputs bit-identical),
  * "gemm_dma" (1, default: the encode's row GEMM on
  * k_gemm_h2r, both operands streamed into a two-stage LDS ring by
  * buffer_load ... lds; 0: k_gemm_h2's register staging; outputs
