@@ -990,12 +990,11 @@ void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles,
 #ifndef DCTAE_FUSED_SE
 #define DCTAE_FUSED_SE 11
 #endif
-// the matrices' MFMA fragments: 0 = a two-stage LDS ring by LDS DMA; 1 =
-// loaded by each wave straight into registers during the previous chunk's
-// MFMAs (its own 64 columns: no LDS copy, plain loads instead of LDS DMA;
-// config 4 rows_fused 3.09 -> 3.59 ms, same box)
-#ifndef DCTAE_FUSED_BREG
-#define DCTAE_FUSED_BREG 0
+// 1: the colour transform of chunk i + 1 interleaved with chunk i's MFMAs
+// (double-buffered pieces; TN = 224 so that the ring and both piece buffers
+// fit 160 KB of LDS), 0: transform and MFMA phases between two barriers
+#ifndef DCTAE_FUSED_PIPE
+#define DCTAE_FUSED_PIPE 1
 #endif
 constexpr int kFusedPairs = 16;    // row pairs per block
 constexpr int kFusedTN = 256;      // output columns per parity
@@ -1005,11 +1004,12 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
                                                       const ImgDesc* __restrict__ imgs, const float* __restrict__ rgb,
                                                       ColorMats cm, uint32_t* __restrict__ amax, int* __restrict__ flags,
                                                       int n_img, int fix) {
-  constexpr int TN = kFusedTN, NPR = kFusedPairs;
+  constexpr bool PIPE = DCTAE_FUSED_PIPE != 0;
+  constexpr int TN = PIPE ? 224 : kFusedTN, NPR = kFusedPairs;
   constexpr int B_PL = TN * XK * 2;          // 16 KB: one plane of one parity's matrix chunk
-  constexpr int B_ST = DCTAE_FUSED_BREG ? 0 : 4 * B_PL;   // 64 KB: 2 parities x 2 planes (LDS-DMA form)
+  constexpr int B_ST = 4 * B_PL;             // 64 KB (56 KB, PIPE): 2 parities x 2 planes
   constexpr int A_CQ = 2 * NPR * XK;         // halves per (parity, channel, piece): 32 rows x 32 k
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * B_ST + 12 * A_CQ * 2];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * B_ST + (PIPE ? 2 : 1) * 12 * A_CQ * 2];   // 152 / 160 KB
   uint16_t* As = reinterpret_cast<uint16_t*>(lds + 2 * B_ST);
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, l32 = lane & 31;
   // the wave index as a uniform value: the parity's matrix descriptor and the
@@ -1094,7 +1094,47 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
     };
     bool bad = false;
     uint32_t fmx = 0;   // |max| of the folded values (the fix-up's scale)
-    auto transform = [&](const Px& px, int k0) {
+    float pi[4][3];     // the IPT of the chunk position's 4 pixels
+    // the colour transform of pixel q (util.py:70-82, k_rgb_to_ipt's arithmetic)
+    auto pix = [&](const Px& px, int q) {
+      const float r = px[q][0], g = px[q][1], b = px[q][2];
+      const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), gam);
+      const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), gam);
+      const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), gam);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) pi[q][c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
+    };
+    // k_rgb_to_ipt's folds of channel c: row y (sum) and row H-1-y (difference)
+    // of both parities, split into fp16 pieces into Ab
+    auto fold = [&](int k0, int c, uint16_t* Ab) {
+      const int k = k0 + kk0;
+      const int kk = k < Ku ? k : 0;
+      const bool xp = W - 1 - kk != kk;
+      const bool oku = vy && k < Ku, okv = vy && k < Kv;
+      const int kq = (k & 31) >> 3, kw = k & 7;
+      const float pb = xp ? pi[1][c] : 0.0f, pd = xp ? pi[3][c] : 0.0f;
+      const float a = yp ? pi[0][c] + pi[2][c] : pi[0][c];
+      const float bb = yp ? pb + pd : pb;
+      const float c2 = pi[0][c] - pi[2][c], d2 = pb - pd;
+      const float v[2][2] = {{oku ? (xp ? a + bb : a) : 0.0f, oku && yp ? (xp ? c2 + d2 : c2) : 0.0f},
+                             {okv ? a - bb : 0.0f, okv && yp ? c2 - d2 : 0.0f}};
+#pragma unroll
+      for (int par = 0; par < 2; ++par)
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const float vv = v[par][rr];
+          fmx = max(fmx, __float_as_uint(vv) & 0x7fffffffu);
+          const float vsc = ldexpf(vv, se);
+          bad |= !(fabsf(vsc) < 32768.0f);
+          const _Float16 h0 = (_Float16)vsc;
+          const _Float16 h1 = (_Float16)(vsc - (float)h0);
+          const int row = pr + NPR * rr;
+          const int o = row * XK + 8 * (kq ^ swz(row)) + kw;
+          Ab[((par * 3 + c) * 2 + 0) * A_CQ + o] = __builtin_bit_cast(uint16_t, h0);
+          Ab[((par * 3 + c) * 2 + 1) * A_CQ + o] = __builtin_bit_cast(uint16_t, h1);
+        }
+    };
+    auto transform = [&](const Px& px, int k0, uint16_t* Ab) {
 #if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 1)
       // profiling ablation: no colour transform / folds / split (wrong output)
 #pragma unroll
@@ -1103,50 +1143,15 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
         for (int pq = 0; pq < 8; ++pq) {
           const int row = pr + NPR * (pq & 1);
           const int o = row * XK + 8 * (((kk0 >> 3)) ^ swz(row)) + (kk0 & 7);
-          As[((pq >> 2) * 3 + c) * 2 * A_CQ + ((pq >> 1) & 1) * A_CQ + o] =
+          Ab[((pq >> 2) * 3 + c) * 2 * A_CQ + ((pq >> 1) & 1) * A_CQ + o] =
               (uint16_t)(__float_as_uint(px[pq & 3][c]) & 0x3bffu);
         }
       return;
 #endif
-      const int k = k0 + kk0;
-      const int kk = k < Ku ? k : 0;
-      const bool xp = W - 1 - kk != kk;
-      const bool oku = vy && k < Ku, okv = vy && k < Kv;
-      float pi[4][3];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {   // util.py:70-82 (k_rgb_to_ipt)
-        const float r = px[q][0], g = px[q][1], b = px[q][2];
-        const float l0 = signed_pow_fast(mat3_row(cm.rgb2lms, 0, r, g, b), gam);
-        const float l1 = signed_pow_fast(mat3_row(cm.rgb2lms, 1, r, g, b), gam);
-        const float l2 = signed_pow_fast(mat3_row(cm.rgb2lms, 2, r, g, b), gam);
+      for (int q = 0; q < 4; ++q) pix(px, q);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) pi[q][c] = mat3_row(cm.lms2ipt, c, l0, l1, l2);
-      }
-      const int kq = (k & 31) >> 3, kw = k & 7;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {   // k_rgb_to_ipt's folds: row y (sum) and row H-1-y (difference)
-        const float pb = xp ? pi[1][c] : 0.0f, pd = xp ? pi[3][c] : 0.0f;
-        const float a = yp ? pi[0][c] + pi[2][c] : pi[0][c];
-        const float bb = yp ? pb + pd : pb;
-        const float c2 = pi[0][c] - pi[2][c], d2 = pb - pd;
-        const float v[2][2] = {{oku ? (xp ? a + bb : a) : 0.0f, oku && yp ? (xp ? c2 + d2 : c2) : 0.0f},
-                               {okv ? a - bb : 0.0f, okv && yp ? c2 - d2 : 0.0f}};
-#pragma unroll
-        for (int par = 0; par < 2; ++par)
-#pragma unroll
-          for (int rr = 0; rr < 2; ++rr) {
-            const float vv = v[par][rr];
-            fmx = max(fmx, __float_as_uint(vv) & 0x7fffffffu);
-            const float vsc = ldexpf(vv, se);
-            bad |= !(fabsf(vsc) < 32768.0f);
-            const _Float16 h0 = (_Float16)vsc;
-            const _Float16 h1 = (_Float16)(vsc - (float)h0);
-            const int row = pr + NPR * rr;
-            const int o = row * XK + 8 * (kq ^ swz(row)) + kw;
-            As[((par * 3 + c) * 2 + 0) * A_CQ + o] = __builtin_bit_cast(uint16_t, h0);
-            As[((par * 3 + c) * 2 + 1) * A_CQ + o] = __builtin_bit_cast(uint16_t, h1);
-          }
-      }
+      for (int c = 0; c < 3; ++c) fold(k0, c, Ab);
     };
     floatx16 acc[3][2];
 #pragma unroll
@@ -1156,83 +1161,96 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[c][x][r] = 0.0f;
     const int nw = pw ? pv.N : pu.N;   // this wave's parity's output columns
-    // DCTAE_FUSED_BREG: this lane's fragments of the next chunk, [ks][x][plane]:
-    // matrix row wc 64 + 32 x + l32, k = 16 ks + 8 half (16 bytes)
-    const auto brw = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(pw ? pv.Xh : pu.Xh), 0,
-                                                      (int)(2 * (pw ? pv.xs_plane : pu.xs_plane) * 2), 0x00020000);
-    const int bro = ((wc * 64 + l32) * (pw ? pv.xs_ld : pu.xs_ld) + 8 * half) * 2;
-    const int brx = 32 * (pw ? pv.xs_ld : pu.xs_ld) * 2, brp = (int)(2 * (pw ? pv.xs_plane : pu.xs_plane));
-    bf16x8 bq[XK / 16][2][2];
-    auto load_bq = [&](int ks, int k0) {
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-          bq[ks][x][pl] = __builtin_bit_cast(
-              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brw, bro + x * brx + pl * brp + (k0 + 16 * ks) * 2, 0, 0));
-    };
-    auto mfma_chunk = [&](int st, int k0n) {
+    // the MFMAs of k step ks and channel c of one chunk (stage st, pieces Ab)
+    auto mfma_unit = [&](int st, const uint16_t* Ab, int ks, int c) {
 #if defined(DCTAE_PROFILING) && defined(DCTAE_FUSED_ABL) && (DCTAE_FUSED_ABL & 2)
       return;   // profiling ablation: no MFMAs (wrong output)
 #endif
       const uint16_t* Bp = reinterpret_cast<const uint16_t*>(lds + st * B_ST + 2 * pw * B_PL);
+      const int kq = 2 * ks + half;
+      bf16x8 a[2];
 #pragma unroll
-      for (int ks = 0; ks < XK / 16; ++ks) {
-        const int kq = 2 * ks + half;
-        bf16x8 b[2][2];
+      for (int q = 0; q < 2; ++q)
+        a[q] = *reinterpret_cast<const bf16x8*>(Ab + ((pw * 3 + c) * 2 + q) * A_CQ + lds_off(l32, kq));
 #pragma unroll
-        for (int x = 0; x < 2; ++x) {
+      for (int x = 0; x < 2; ++x)
+        if (wc * 64 + 32 * x < nw) {   // (wave-uniform) columns past N: none
           const int rb = wc * 64 + 32 * x + l32;
+          bf16x8 b[2];
 #pragma unroll
           for (int pl = 0; pl < 2; ++pl)
-            b[x][pl] = DCTAE_FUSED_BREG ? bq[ks][x][pl]
-                                        : *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + lds_off(rb, kq));
+            b[pl] = *reinterpret_cast<const bf16x8*>(Bp + pl * (B_PL / 2) + lds_off(rb, kq));
+          mfma_pieces(acc[c][x], a, b);
         }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          bf16x8 a[2];
-#pragma unroll
-          for (int q = 0; q < 2; ++q)
-            a[q] = *reinterpret_cast<const bf16x8*>(As + ((pw * 3 + c) * 2 + q) * A_CQ + lds_off(l32, kq));
-#pragma unroll
-          for (int x = 0; x < 2; ++x)
-            if (wc * 64 + 32 * x < nw) mfma_pieces(acc[c][x], a, b[x]);   // (wave-uniform) columns past N: none
-        }
-        if (DCTAE_FUSED_BREG) load_bq(ks, k0n);   // this k step's fragments consumed: the next chunk's in flight
-      }
     };
-    // Pixels two chunks ahead (pxa: even chunks, pxb: odd), the matrices one;
-    // issue order per step i: [matrices i + 1] [pixels i + 2], so at its top at
-    // most pixels i + 1's 12 loads may be outstanding.  Every step issues the
-    // same loads (past the last chunk: clamped pixels, matrix offsets reading
-    // zeros), and the loop body is unconditional, so the compiler's own waits
-    // on the pixel registers count exactly.
     const int nk = (Ku + XK - 1) / XK;
-    auto step = [&](int i, Px& cur) {
-      wait_vm<12>();      // this wave's pixels and matrix chunk i
-      lds_barrier();      // every wave's; chunk i - 1's MFMAs done (the pieces and stage (i + 1) % 2 free)
-      if (!DCTAE_FUSED_BREG) dma_b((i + 1) & 1, (i + 1) * XK);
-      transform(cur, i * XK);
-      if (!DCTAE_FUSED_BREG) load_rgb(cur, (i + 2) * XK);
-      lds_barrier();      // the pieces of chunk i
-      mfma_chunk(i & 1, (i + 1) * XK);
-      // BREG issue order per step: [matrix i + 1] [pixels i + 2] (after the MFMAs)
-      if (DCTAE_FUSED_BREG) load_rgb(cur, (i + 2) * XK);
-    };
-    load_rgb(pxa, 0);
-    if (DCTAE_FUSED_BREG) {
-      load_bq(0, 0);
-      load_bq(1, 0);
-    } else {
+    if constexpr (!PIPE) {
+      // Pixels two chunks ahead (pxa: even chunks, pxb: odd), the matrices one;
+      // issue order per step i: [matrices i + 1] [pixels i + 2], so at its top at
+      // most pixels i + 1's 12 loads may be outstanding.  Every step issues the
+      // same loads (past the last chunk: clamped pixels, matrix offsets reading
+      // zeros), and the loop body is unconditional, so the compiler's own waits
+      // on the pixel registers count exactly.
+      auto step = [&](int i, Px& cur) {
+        wait_vm<12>();      // this wave's pixels and matrix chunk i
+        lds_barrier();      // every wave's; chunk i - 1's MFMAs done (the pieces and stage (i + 1) % 2 free)
+        dma_b((i + 1) & 1, (i + 1) * XK);
+        transform(cur, i * XK, As);
+        load_rgb(cur, (i + 2) * XK);
+        lds_barrier();      // the pieces of chunk i
+#pragma unroll
+        for (int ks = 0; ks < XK / 16; ++ks)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) mfma_unit(i & 1, As, ks, c);
+      };
+      load_rgb(pxa, 0);
       dma_b(0, 0);
+      load_rgb(pxb, XK);
+      int i = 0;
+      for (; i + 1 < nk; i += 2) {
+        step(i, pxa);
+        step(i + 1, pxb);
+      }
+      if (i < nk) step(i, pxa);
+    } else {
+      // DCTAE_FUSED_PIPE: the transform of chunk i + 1 interleaved with chunk i's
+      // MFMAs (double-buffered pieces As / As + 12 A_CQ), one barrier per chunk.
+      // Issue order per step i: [matrices i + 1] [pixels i + 3]; at its top the
+      // wave needs matrices i and pixels i + 1, pixels i + 2 may be in flight.
+      uint16_t* A0 = As;
+      uint16_t* A1 = As + 12 * A_CQ;
+      auto step = [&](int i, Px& cur, const uint16_t* Ac, uint16_t* An) {
+        wait_vm<12>();
+        lds_barrier();      // pieces of chunk i from every wave; chunk i - 1's MFMAs done (An, stage (i + 1) % 2 free)
+        dma_b((i + 1) & 1, (i + 1) * XK);
+        const int kn = (i + 1) * XK;
+        mfma_unit(i & 1, Ac, 0, 0);
+        pix(cur, 0);
+        mfma_unit(i & 1, Ac, 0, 1);
+        pix(cur, 1);
+        mfma_unit(i & 1, Ac, 0, 2);
+        pix(cur, 2);
+        mfma_unit(i & 1, Ac, 1, 0);
+        pix(cur, 3);
+        mfma_unit(i & 1, Ac, 1, 1);
+        fold(kn, 0, An);
+        fold(kn, 1, An);
+        mfma_unit(i & 1, Ac, 1, 2);
+        fold(kn, 2, An);
+        load_rgb(cur, (i + 3) * XK);
+      };
+      load_rgb(pxa, 0);
+      load_rgb(pxb, XK);
+      dma_b(0, 0);
+      transform(pxa, 0, A0);
+      load_rgb(pxa, 2 * XK);
+      int i = 0;
+      for (; i + 1 < nk; i += 2) {
+        step(i, pxb, A0, A1);
+        step(i + 1, pxa, A1, A0);
+      }
+      if (i < nk) step(i, pxb, A0, A1);
     }
-    load_rgb(pxb, XK);
-    int i = 0;
-    for (; i + 1 < nk; i += 2) {
-      step(i, pxa);
-      step(i + 1, pxb);
-    }
-    if (i < nk) step(i, pxa);
     wait_vm<0>();   // no LDS DMA may outlive the loop (the LDS is reused, and released at exit)
     const GemmProblem& p = pw ? pv : pu;
     const int N = p.N;
@@ -1267,17 +1285,20 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
       mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
       fmx = max(fmx, (uint32_t)__shfl_xor((int)fmx, o));
     }
-    const int any_bad = __syncthreads_or(bad ? 1 : 0);   // also: every wave past its last LDS read
+    const bool wbad = __ballot(bad) != 0;   // (__syncthreads_or brings 256 bytes of LDS of its own)
+    __syncthreads();   // every wave past its last LDS read: the partials alias the ring
     if (lane == 0) {
       part[wave] = mx;
       part[8 + wave] = fmx;
+      part[16 + wave] = wbad ? 1u : 0u;
     }
     __syncthreads();
     if (tid == 0) {
-      uint32_t m = 0, f = 0;
+      uint32_t m = 0, f = 0, any_bad = 0;
       for (int w = 0; w < 8; ++w) {
         m = max(m, part[w]);
         f = max(f, part[8 + w]);
+        any_bad |= part[16 + w];
       }
       if (!fix) {
         if (f) atomicMax(amax + 2 * li, f);
@@ -1312,7 +1333,7 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
 }
 
 int fused_pairs_per_block() { return kFusedPairs; }
-int fused_max_n() { return kFusedTN; }
+int fused_max_n() { return DCTAE_FUSED_PIPE ? 224 : kFusedTN; }
 
 void launch_rows_fused(const GemmProblem* probs, const TileRef* tiles, int n_tiles, const ImgDesc* imgs,
                        const float* rgb, const ColorMats& cm, uint32_t* amax, int* flags, int n_img, hipStream_t s,
