@@ -1198,7 +1198,7 @@ static int build_encode_plan(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dcta
       j.max_hw = std::max<int64_t>(j.max_hw, (int64_t)d.H * d.W);
     }
     j.amax_off = wsf;
-    wsf += up(3ll * (j.i1 - j.i0) + 1);   // |max| pairs, then k_rows_fused's per-image flags and "any" word
+    wsf += up(3ll * (j.i1 - j.i0) + 9);   // |max| pairs, then k_rows_fused's per-image flags, "any" word, 8 tile counters
     E.ws_need = std::max<size_t>(E.ws_need, (size_t)wsf * 4);
     E.max_T = std::max(E.max_T, j.max_T);
   }
@@ -1564,7 +1564,7 @@ static int encode_impl(dctae_ctx* ctx, const dctae_fe_cfg* cfg, const dctae_imag
   auto do_rows = [&](const ChunkJob& j, hipStream_t st) {
     const ImgDesc* dd = (const ImgDesc*)(pd + j.desc_off);
     uint32_t* amax = reinterpret_cast<uint32_t*>(ctx->ws + j.amax_off);
-    if (j.h2 || j.any_fused) hipMemsetAsync(amax, 0, 12 * (size_t)(j.i1 - j.i0) + 4, st);   // errors surface at hipGetLastError
+    if (j.h2 || j.any_fused) hipMemsetAsync(amax, 0, 12 * (size_t)(j.i1 - j.i0) + 36, st);   // errors surface at hipGetLastError
     if (j.any_fused) {
       int* flags = reinterpret_cast<int*>(amax + 2 * (j.i1 - j.i0));
       {

@@ -996,6 +996,9 @@ void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles,
 #ifndef DCTAE_FUSED_PIPE
 #define DCTAE_FUSED_PIPE 1
 #endif
+#ifndef DCTAE_FUSED_DYN
+#define DCTAE_FUSED_DYN 1   // persistent first pass with per-XCD tile counters (below)
+#endif
 constexpr int kFusedPairs = 16;    // row pairs per block
 constexpr int kFusedTN = 256;      // output columns per parity
 
@@ -1019,12 +1022,34 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
   const int pw = wave >> 2, wc = wave & 3;   // this wave's parity and 64-column slice
   const float gam = 0.430000007152557373046875f;
   if (fix && flags[n_img] == 0) return;      // fix-up: no image of the job flagged
-  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+  // DCTAE_FUSED_DYN (first pass): a persistent grid taking tiles from
+  // per-XCD counters (flags[n_img + 1 + x]): block b runs on XCD b % 8 and
+  // takes the dealt list's positions x + 8 k of its XCD lane in counter order,
+  // so the image-per-XCD dealing holds without a static split's imbalance, and
+  // the next tile's counter value is fetched while this tile runs
+  const bool dyn = DCTAE_FUSED_DYN && !fix;
+  const int xl = (int)(blockIdx.x & 7);
+  int* ctr = flags + n_img + 1 + xl;
+  for (int t = blockIdx.x; t < n_tiles;) {
+    int t_next = 0;   // (dyn, thread 0) the next position of this XCD lane
+    if (dyn && tid == 0) t_next = xl + 8 * ((int)(gridDim.x >> 3) + atomicAdd(ctr, 1));
     const TileRef tr = tiles[t];
-    if (tr.problem < 0) continue;   // padding of an XCD-dealt list
-    const GemmProblem pu = probs[tr.problem], pv = probs[tr.problem + 1];   // the even and odd parity problems
+    const GemmProblem pu = probs[max(tr.problem, 0)], pv = probs[max(tr.problem, 0) + 1];   // even and odd parity
     const int li = pu.pad2;
-    if (fix && flags[li] == 0) continue;
+    // padding of an XCD-dealt list, or (fix-up) an image not flagged: the next tile
+    if (tr.problem < 0 || (fix && flags[li] == 0)) {
+      if (dyn) {
+        uint32_t* part = reinterpret_cast<uint32_t*>(lds);
+        __syncthreads();
+        if (tid == 0) part[24] = (uint32_t)t_next;
+        __syncthreads();
+        t = __builtin_amdgcn_readfirstlane((int)part[24]);   // uniform: the descriptors stay scalar
+        __syncthreads();
+      } else {
+        t += (int)gridDim.x;
+      }
+      continue;
+    }
     const ImgDesc d = imgs[li];
     const int H = d.H, W = d.W, Hh = (H + 1) >> 1, Ku = pu.K, Kv = pv.K;
     const int j0 = tr.tile * NPR;
@@ -1328,6 +1353,14 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
         }
       }
     }
+    if (dyn) {
+      uint32_t* part = reinterpret_cast<uint32_t*>(lds);
+      if (tid == 0) part[24] = (uint32_t)t_next;
+      __syncthreads();
+      t = __builtin_amdgcn_readfirstlane((int)part[24]);   // uniform: the descriptors stay scalar
+    } else {
+      t += (int)gridDim.x;
+    }
     __syncthreads();   // the partials / LDS reused by the next tile
   }
 }
@@ -1340,8 +1373,9 @@ void launch_rows_fused(const GemmProblem* probs, const TileRef* tiles, int n_til
                        bool fixup) {
   if (n_tiles <= 0) return;
   // the fix-up: a short grid-stride launch (every block exits at once when no image is flagged)
-  hipLaunchKernelGGL(k_rows_fused, dim3(fixup ? std::min(n_tiles, 256) : n_tiles), dim3(512), 0, s, probs, tiles,
-                     n_tiles, imgs, rgb, cm, amax, flags, n_img, fixup ? 1 : 0);
+  const int g = fixup || DCTAE_FUSED_DYN ? std::min((n_tiles + 7) & ~7, 256) : n_tiles;
+  hipLaunchKernelGGL(k_rows_fused, dim3(g), dim3(512), 0, s, probs, tiles, n_tiles, imgs, rgb, cm, amax, flags, n_img,
+                     fixup ? 1 : 0);
 }
 
 void launch_gemm_x3(int nc, const GemmProblem* probs, const TileRef* tiles, int n_tiles, hipStream_t s, int share) {
