@@ -18,6 +18,8 @@ Tolerances: tokens 2e-6 x max|Y|; codes equal outside the guard band (DCT) /
 the fp32 rounding band |h| <= 4e-6 (|W||y| + |b|) (projection); decoded RGB
 1e-5 x image range + 2e-5 relative.  Run on an MI355X.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -44,6 +46,10 @@ def setup(pkg, ref_tables):
     pn.frozen = True
     pn.eval()
     lfq = pkg.LFQ(dim=196, codebook_size=2 ** 14, num_codebooks=14).to(DEV).eval()
+    # A/B hook: DCTAE_TEST_OPTS="key=value,..." (library options for this module's tests)
+    for kv in filter(None, os.environ.get("DCTAE_TEST_OPTS", "").split(",")):
+        k, v = kv.split("=")
+        ops.set_option(k, int(v))
     return ops, fe_mod, fe, pn, lfq
 
 
@@ -100,7 +106,11 @@ def test_config4_full_batch_vs_oracle_and_small_batch(setup, ref_tables):
     for i in pick:
         r, _, tj = slots[i]
         assert len(tj) == 3 * min(int(hw[i][0]) // 14, 32) * min(int(hw[i][1]) // 14, 32)
-        f, m = _check_image_vs_oracle(raw[r, tj], cod[r, tj], pos[r, tj], ch[r, tj], imgs[i].cpu().numpy(), ref_tables)
+        try:
+            f, m = _check_image_vs_oracle(raw[r, tj], cod[r, tj], pos[r, tj], ch[r, tj], imgs[i].cpu().numpy(),
+                                          ref_tables)
+        except AssertionError as e:
+            raise AssertionError(f"image {i} {tuple(map(int, hw[i]))}: {e}") from None
         flips, n = flips + f, n + m
     print(f"[config 4, images {pick}, sizes {[tuple(map(int, hw[i])) for i in pick]}] "
           f"code mismatches inside the guard band: {flips} / {n}")
