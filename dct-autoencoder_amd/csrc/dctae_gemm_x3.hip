@@ -530,9 +530,15 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // cannot prove disjoint, prefetched register loads included.  The caller
 // waits for the chunk (wait_vm) before its barrier.  rsrc: the raw buffer
 // descriptor words (base, num_records, 0x00020000).
+// The s_nop: nothing inside an asm string gets the wait states hipcc adds to
+// its own instructions (cdna_hip_programming.md, "What hipcc does not do" 2):
+// an LDS DMA needs one after the s_mov to M0, and a descriptor or soffset SGPR
+// written by VALU (readfirstlane) needs five before a buffer instruction reads
+// it.  Without them a piece could land at the previous M0 -- seen as rare
+// run-to-run differences of a few tokens on the config-4 batch.
 __device__ __forceinline__ void dma_lds16(u32x4 rsrc, const void* lds, int voff) {
   const uint32_t m0 = (uint32_t)(uintptr_t)lds;
-  asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m0) : "memory");
+  asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "{m0}"(m0) : "memory");
 }
 __device__ __forceinline__ u32x4 rsrc_words(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)(uintptr_t)base;
