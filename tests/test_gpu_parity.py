@@ -1090,3 +1090,17 @@ def test_cols_dma_bit_identical(fe, pn, lfq):
     assert torch.equal(c0, c1)
     assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
     assert torch.equal(d0._data["scores"], d1._data["scores"])
+
+
+def test_rows_fused_deterministic(fe, pn, lfq):
+    """k_rows_fused streams its matrices by inline LDS DMA and takes tiles from
+    per-XCD counters in whatever order the blocks reach them: the same batch
+    must encode bit-identically call after call (a missing wait state after the
+    M0 write once made a few tokens of the config-4 batch differ between calls)."""
+    xs = [torch.from_numpy(a).to(DEV) for a in
+          rng.synth_images(65, [(1000, 1000), (777, 1013), (333, 517), (1021, 65), (448, 449), (96, 998)])]
+    ((d0, c0),) = fe.encode_batch(xs, pn, lfq, return_raw=True)
+    for _ in range(4):
+        ((d1, c1),) = fe.encode_batch(xs, pn, lfq, return_raw=True)
+        assert torch.equal(c0, c1)
+        assert torch.equal(d0.patches.view(torch.int32), d1.patches.view(torch.int32))
