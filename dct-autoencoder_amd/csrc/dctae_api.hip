@@ -145,6 +145,10 @@ struct dctae_ctx {
   int cols_dma = 1;
   // images with both passes on the GEMM DCT: T / Y parity-planar (ImgDesc::tperm)
   int tperm = 1;
+  // debug: fill the workspace and staging buffers with NaN bits (0xff) before
+  // every call that sizes them, so a read of a word the call did not write
+  // shows in its outputs (env DCTAE_WS_POISON=1 sets it at context creation)
+  int ws_poison = 0;
   // LFQ projections on the fp16 form with the conf/patch14-l.json shapes
   // (192 < in, out <= 208 / 224): 1 = the W-stationary kernel k_lfq_ws
   // (dctae_lfq_ws.hip), 0 = k_lfq_proj_h2
@@ -343,6 +347,12 @@ int ensure_ws(dctae_ctx* ctx, size_t ws_bytes, size_t stage_bytes) {
     if (hipMalloc((void**)&ctx->stage, stage_bytes) != hipSuccess)
       return fail(ctx, DCTAE_ENOMEM, "staging allocation of " + std::to_string(stage_bytes) + " bytes failed");
     ctx->stage_bytes = stage_bytes;
+  }
+  if (ctx->ws_poison) {   // a request of <= 256 bytes leaves that buffer alone (a call's second ensure_ws)
+    HIPCHK(ctx, hipDeviceSynchronize());
+    if (ws_bytes > 256) HIPCHK(ctx, hipMemset(ctx->ws, 0xff, ctx->ws_bytes));
+    if (stage_bytes > 256) HIPCHK(ctx, hipMemset(ctx->stage, 0xff, ctx->stage_bytes));
+    HIPCHK(ctx, hipDeviceSynchronize());
   }
   return 0;
 }
@@ -878,6 +888,10 @@ int dctae_ctx_create(int device, dctae_ctx** out) {
     return DCTAE_EHIP;
   }
   c->fft_tab_cap = 1 << 20;
+  {
+    const char* e = getenv("DCTAE_WS_POISON");
+    c->ws_poison = e && e[0] == '1';
+  }
   if (hipMalloc((void**)&c->fft_tab, c->fft_tab_cap * sizeof(float2)) != hipSuccess) {
     g_err = "FFT table allocation failed";
     delete c;
@@ -998,6 +1012,7 @@ int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value) {
   else if (k == "fft_odd") ctx->fft_odd = value != 0;   // checked before the plan cache (fft_plan_for)
   else if (k == "fft_generic") ctx->fft_generic = value != 0;
   else if (k == "tperm") ctx->tperm = value != 0;
+  else if (k == "ws_poison") ctx->ws_poison = value != 0;
   else return fail(ctx, DCTAE_EINVAL, "unknown option or bad value: " + k);
   return 0;
 }

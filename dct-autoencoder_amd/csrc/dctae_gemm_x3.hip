@@ -998,9 +998,14 @@ void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles,
 #endif
 // 1: the colour transform of chunk i + 1 interleaved with chunk i's MFMAs
 // (double-buffered pieces; TN = 224 so that the ring and both piece buffers
-// fit 160 KB of LDS), 0: transform and MFMA phases between two barriers
+// fit 160 KB of LDS), 0: transform and MFMA phases between two barriers.
+// Off: on the config-4 batch the interleaved form encoded 3-6 % of calls
+// differently from the previous call (whole coefficient columns of the first
+// images' low kx -- stale or unwritten matrix rows read by the MFMAs; NaN on
+// a fresh GPU without the persistent loop), the two-barrier form 0 of 280
+// (tools/c4_stress.py)
 #ifndef DCTAE_FUSED_PIPE
-#define DCTAE_FUSED_PIPE 1
+#define DCTAE_FUSED_PIPE 0
 #endif
 #ifndef DCTAE_FUSED_DYN
 #define DCTAE_FUSED_DYN 1   // persistent first pass with per-XCD tile counters (below)
@@ -1251,7 +1256,11 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
       uint16_t* A0 = As;
       uint16_t* A1 = As + 12 * A_CQ;
       auto step = [&](int i, Px& cur, const uint16_t* Ac, uint16_t* An) {
+#ifdef DCTAE_FUSED_WAIT0
+        wait_vm<0>();
+#else
         wait_vm<12>();
+#endif
         lds_barrier();      // pieces of chunk i from every wave; chunk i - 1's MFMAs done (An, stage (i + 1) % 2 free)
         dma_b((i + 1) & 1, (i + 1) * XK);
         const int kn = (i + 1) * XK;
