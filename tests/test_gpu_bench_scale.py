@@ -202,3 +202,27 @@ def test_lfq_projections_full_batch_vs_linear(setup):
         flips, n = flips + int(diff.sum()), n + g.numel()
     print(f"[lfq projections 1024 x 512^2, images {pick}] codes inside the rounding band: {flips} / {n}")
     assert flips <= max(2, n // 1000)
+
+
+@pytest.mark.parametrize("n,side,calls", [(1024, 512, 10), (256, 224, 20)])
+def test_default_paths_run_to_run_identical(setup, n, side, calls):
+    """The headline (1024 x 512^2: k_rows512pk / k_cols512b / k_sort_pack2) and
+    config-2 (256 x 224^2: k_rows224p / k_cols224) encodes, and the 512^2
+    FFT decode, are bit-identical call after call at the bench's batch sizes
+    (the config-4 stress above found a schedule that was not)."""
+    ops, fe_mod, fe, pn, lfq = setup
+    x = ops.synth_images(n, side, side, seed=3, device=DEV)
+    ((d0, c0),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+    p0 = d0.patches.view(torch.int32)
+    for it in range(calls):
+        ((d1, c1),) = fe.encode_batch(x, pn, lfq, return_raw=True)
+        assert torch.equal(c0, c1), f"call {it}: codes differ"
+        assert torch.equal(p0, d1.patches.view(torch.int32)), f"call {it}: raw tokens differ"
+    if side == 512:
+        del p0, d1, c1
+        r0 = fe.decode_batch(d0, c0, pn, lfq)
+        for it in range(3):
+            r1 = fe.decode_batch(d0, c0, pn, lfq)
+            assert all(torch.equal(a.view(torch.int32), b.view(torch.int32)) for a, b in zip(r0, r1)), \
+                f"decode call {it} differs"
+    ops.check_device_errors(c0.device)
