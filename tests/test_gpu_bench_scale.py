@@ -184,6 +184,8 @@ def test_lfq_projections_full_batch_vs_linear(setup):
     codes_b = enc(x)["codes"].clone()
     ops.check_device_errors(codes_b.device)
     assert codes_b.shape == (1024, 3072, 16)
+    for it in range(8):   # run to run: k_lfq_ws's persistent multi-tile loop, call after call
+        assert torch.equal(enc(x)["codes"], codes_b), f"BatchEncoder call {it + 1} differs from the first"
     pick = [0, 511, 1023]
     ((dp, codes_s),) = fe.encode_batch([x[i] for i in pick], pn, lfq_p, return_patches=True)
     W, b = lfq_p.project_in.weight.detach().cpu(), lfq_p.project_in.bias.detach().cpu()
