@@ -1002,7 +1002,7 @@ void launch_gemm_h2(const GemmProblem* probs, const TileRef* tiles, int n_tiles,
 // Off: on the config-4 batch the interleaved form encoded 3-6 % of calls
 // differently from the first call (whole coefficient columns of the first
 // images' low kx -- stale or unwritten matrix rows read by the MFMAs; NaN on
-// a fresh GPU without the persistent loop), the two-barrier form 0 of 230
+// a fresh GPU without the persistent loop), the two-barrier form 0 of 690
 // (tools/c4_stress.py); with vmcnt(0) at each step top 0 of 100, but slower
 #ifndef DCTAE_FUSED_PIPE
 #define DCTAE_FUSED_PIPE 0
