@@ -413,7 +413,11 @@ int dctae_set_chunk_bytes(dctae_ctx* ctx, int64_t bytes);
  * "gemm_dma" (1, default: the encode's row GEMM on
  * k_gemm_h2r, both operands streamed into a two-stage LDS ring by
  * buffer_load ... lds; 0: k_gemm_h2's register staging; outputs
- * bit-identical).  Profiling builds only (make PROFILING=1; the shipped
+ * bit-identical), "ws_poison" (0, default; 1: a debug check that fills the
+ * workspace and staging buffers with NaN bits before every call that sizes
+ * them, so a read of a word the call did not write shows in its outputs;
+ * also set by the environment variable DCTAE_WS_POISON=1 at context
+ * creation; slow).  Profiling builds only (make PROFILING=1; the shipped
  * library returns DCTAE_EUNSUP): "bs_ablate", "t_alias", "gate" (these write
  * wrong outputs on purpose). */
 int dctae_set_option(dctae_ctx* ctx, const char* key, int64_t value);
