@@ -1256,9 +1256,9 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
       uint16_t* A0 = As;
       uint16_t* A1 = As + 12 * A_CQ;
       auto step = [&](int i, Px& cur, const uint16_t* Ac, uint16_t* An) {
-#ifdef DCTAE_FUSED_WAIT0
+#if defined(DCTAE_FUSED_WAIT0)
         wait_vm<0>();
-#else
+#elif !defined(DCTAE_FUSED_EARLYWAIT)
         wait_vm<12>();
 #endif
         lds_barrier();      // pieces of chunk i from every wave; chunk i - 1's MFMAs done (An, stage (i + 1) % 2 free)
@@ -1272,18 +1272,34 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
         pix(cur, 2);
         mfma_unit(i & 1, Ac, 1, 0);
         pix(cur, 3);
+#ifdef DCTAE_FUSED_EARLYWAIT
+        // (experiment) the pixels of chunk i + 3 issued as soon as cur is
+        // consumed, and the wait for matrices i + 1 two MFMA units before the
+        // next barrier instead of right before it
+        load_rgb(cur, (i + 3) * XK);
+        mfma_unit(i & 1, Ac, 1, 1);
+        fold(kn, 0, An);
+        fold(kn, 1, An);
+        wait_vm<12>();
+        mfma_unit(i & 1, Ac, 1, 2);
+        fold(kn, 2, An);
+#else
         mfma_unit(i & 1, Ac, 1, 1);
         fold(kn, 0, An);
         fold(kn, 1, An);
         mfma_unit(i & 1, Ac, 1, 2);
         fold(kn, 2, An);
         load_rgb(cur, (i + 3) * XK);
+#endif
       };
       load_rgb(pxa, 0);
       load_rgb(pxb, XK);
       dma_b(0, 0);
       transform(pxa, 0, A0);
       load_rgb(pxa, 2 * XK);
+#ifdef DCTAE_FUSED_EARLYWAIT
+      wait_vm<12>();   // matrices 0
+#endif
       int i = 0;
       for (; i + 1 < nk; i += 2) {
         step(i, pxb, A0, A1);
