@@ -1256,6 +1256,9 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
       uint16_t* A0 = As;
       uint16_t* A1 = As + 12 * A_CQ;
       auto step = [&](int i, Px& cur, const uint16_t* Ac, uint16_t* An) {
+#ifdef DCTAE_FUSED_SB   // pin the issue order the counted wait assumes (no load moved across it)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #if defined(DCTAE_FUSED_WAIT0)
         wait_vm<0>();
 #elif !defined(DCTAE_FUSED_EARLYWAIT)
@@ -1280,6 +1283,9 @@ __global__ __launch_bounds__(512, 1) void k_rows_fused(const GemmProblem* __rest
         mfma_unit(i & 1, Ac, 1, 1);
         fold(kn, 0, An);
         fold(kn, 1, An);
+#ifdef DCTAE_FUSED_SB
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         wait_vm<12>();
         mfma_unit(i & 1, Ac, 1, 2);
         fold(kn, 2, An);
